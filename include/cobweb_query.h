@@ -1,0 +1,151 @@
+/*
+ * cobweb_query.h -- C ABI of libcwq, the MI355X (gfx950) query engine for the
+ * Cobweb retrieval path of Teachable-AI-Lab/RAG-Cobweb (reference @ 2025-09-26).
+ *
+ * The reference exposes no native boundary: its interface is the Python class
+ * CobwebWrapper (src/cobweb/CobwebWrapper.py).  Each entry point below replaces
+ * one op sequence of that class (file:line cited per function).  The Python
+ * drop-in (rag-cobweb_amd/wrapper.py) binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - Every function returns int status: CWQ_OK (0) or a negative CWQ_ERR_*;
+ *     cwq_last_error() returns a thread-local message for the last failure.
+ *   - Pointers documented "device" are HIP device pointers (e.g. a torch tensor's
+ *     data_ptr()); "host" pointers are ordinary CPU memory.  Outputs are written
+ *     into caller-allocated buffers; the library never frees caller memory.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  All
+ *     query calls are stream-ordered and asynchronous unless stated otherwise.
+ *   - Node numbering is the reference's BFS order (CobwebWrapper.py:107-132):
+ *     node 0 is the root and the children of a node are consecutive, in the
+ *     order of its children list.  Sentence ids are the reference's sentence ids.
+ *   - One query call at a time per index handle (the handle owns its workspace);
+ *     use one handle per device / per concurrent stream.
+ */
+#ifndef COBWEB_QUERY_H
+#define COBWEB_QUERY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CWQ_OK 0
+#define CWQ_ERR_ARG (-1)        /* invalid argument / malformed tree            */
+#define CWQ_ERR_HIP (-2)        /* HIP runtime error                            */
+#define CWQ_ERR_OOM (-3)        /* device allocation failed                     */
+#define CWQ_ERR_NOT_FOUND (-4)  /* categorize retrieved < k nodes (the reference
+                                   raises IndexError, CobwebTorchTree.py:289)    */
+
+typedef struct cwq_index cwq_index;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int cwq_version(void);
+
+/* Thread-local message describing the last error on this thread. */
+const char* cwq_last_error(void);
+
+/*
+ * Build the immutable query index from a flattened tree.
+ * Replaces CobwebWrapper.build_prediction_index (CobwebWrapper.py:91-208): the
+ * caller passes the BFS-ordered node statistics the reference caches in
+ * _node_means / _node_vars (:186-203) and the structure the reference keeps in
+ * _index_to_node / _leaf_to_path_indices / _path_matrix (:107-184).
+ *
+ *   device            HIP device ordinal the index lives on
+ *   n_nodes, dim      Nn nodes of dimension D
+ *   mean, var         device, [n_nodes*dim] fp32 row-major; var = compute_var
+ *                     (meanSq/count + prior_var, or prior_var for empty nodes)
+ *   parent            host, [n_nodes] int64; parent[0] = -1 and parent is
+ *                     non-decreasing (BFS order)
+ *   node_of_sentence  host, [n_sent] int64; the BFS node holding sentence id s
+ *                     (-1: the sentence is not in the tree)
+ *   level_w, n_w      host level weights (CobwebWrapper.py:153-166); depth >= n_w
+ *                     uses 1.0; each path term is weighted level_w[depth]/len(path)
+ *   stream            stream for the build kernels (the call synchronises it)
+ */
+int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var,
+                     const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
+                     const double* level_w, int32_t n_w, void* stream, cwq_index** out);
+
+int cwq_index_destroy(cwq_index* idx);
+
+/* Index facts: out[0]=n_nodes out[1]=dim out[2]=n_sent out[3]=internal nodes
+ * out[4]=leaf-class rows out[5]=isotropic rows out[6]=max depth out[7]=device bytes */
+int cwq_index_info(const cwq_index* idx, int64_t* out8);
+
+/*
+ * "Cobweb Fast" batched top-k (A6).  Replaces CobwebWrapper.cobweb_predict_indexed
+ * (CobwebWrapper.py:210-265, alias cobweb_predict_fast :428-433) for nq queries:
+ * score(s) = sum over the root->leaf path of (w[depth]/len) * lp'(node), with
+ * lp'(n) = -0.5*(sum_d log v + sum_d (x-mu)^2/v) (:230-241); top-k descending.
+ *   q        device [nq*dim] fp32 queries
+ *   ids      device [nq*k] int64 sentence ids (-1 past the number of sentences)
+ *   scores   device [nq*k] fp32 scores (may be NULL)
+ * Ties are broken by lower node index, then lower sentence id (the reference
+ * adds randn*1e-6 noise instead, :246-256).  Any k >= 1 is accepted; k >= n_sent
+ * returns the full ranking like the reference's argsort branch (:246-251).
+ */
+int cwq_score_topk(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                   void* stream);
+
+/*
+ * All sentence scores (A8).  Replaces CobwebWrapper.cobweb_rank_scores
+ * (CobwebWrapper.py:267-294).  out: device [nq*n_sent] fp32 (sentences that are
+ * not in the tree get -inf).
+ */
+int cwq_rank_scores(cwq_index* idx, const float* q, int64_t nq, float* out, void* stream);
+
+/*
+ * Per-node Gaussian log-likelihood for every node in BFS order.
+ *   full = 0: lp'(n) as CobwebWrapper.py:232-236 (no 2*pi term)
+ *   full = 1: CobwebTorchNode.log_prob (CobwebTorchNode.py:100-104, with 2*pi)
+ * out: device [nq*n_nodes] fp32.
+ */
+int cwq_node_logprob(cwq_index* idx, const float* q, int64_t nq, int32_t full, float* out, void* stream);
+
+/*
+ * "Cobweb Basic" best-first categorize (A4).  Replaces CobwebTorchTree.categorize
+ * / _cobweb_categorize with retrieve_k=k (CobwebTorchTree.py:235-310) as called by
+ * CobwebWrapper.cobweb_predict (CobwebWrapper.py:435-461).
+ *   nodes     device [nq*k] int64: BFS indices of the retrieved nodes in pop order
+ *   n_found   device [nq] int32: number retrieved (< k where the reference raises
+ *             IndexError: too few leaves, or max_nodes reached, :264-289)
+ *   n_calls   device [nq] int64: log_prob evaluations the reference would make
+ *             (may be NULL)
+ * Heap ties: (-lp, parent lp, BFS index) -- the reference uses random() as the
+ * third key.  The call synchronises `stream` (it may re-run hard queries).
+ * Returns CWQ_OK also when some queries found < k nodes: callers check n_found
+ * (the Python drop-in raises IndexError there, as the reference does).
+ */
+int cwq_categorize(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
+                   int32_t* n_found, int64_t* n_calls, void* stream);
+
+/*
+ * Device timing of the phases of the last cwq_score_topk call, measured with HIP
+ * events recorded on the stream the kernels run on (enable first; timing mode
+ * synchronises the stream once per query chunk).
+ *   out[0] leaf-row scan (the fused score + top-k kernel)   out[1] internal-node pass
+ *   out[2] merge + sentence expansion                      out[3] whole call
+ *   (milliseconds; out[4] = number of leaf-scan launches)
+ */
+int cwq_set_timing(cwq_index* idx, int enable);
+int cwq_last_timing(cwq_index* idx, float* out5);
+
+/*
+ * Sequential Welford statistics of row groups (synthetic-tree builder).
+ * For group g, folds rows X[order[group_ptr[g]] .. order[group_ptr[g+1]-1]] in
+ * that order with exactly the fp32 op sequence of CobwebTorchNode.increment_counts
+ * (CobwebTorchNode.py:57-68: count += 1; delta = x - mean; mean += delta / count;
+ * meanSq += delta * (x - mean)), so a synthesised internal node carries the stats
+ * the reference's ifit would accumulate for those inserts.
+ *   X [n_rows*dim], order [n_order], group_ptr [n_groups+1]: device
+ *   count [n_groups], mean/meanSq [n_groups*dim]: device outputs
+ */
+int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order, const int64_t* group_ptr,
+                       int64_t n_groups, float* count, float* mean, float* meanSq, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COBWEB_QUERY_H */

@@ -1,0 +1,70 @@
+"""ctypes binding of libcwq (include/cobweb_query.h).
+
+The library is built in-tree (``__graft_entry__.build()`` / ``python -m
+rag_cobweb_amd.build``) as ``rag-cobweb_amd/libcwq.so``.  There is no fallback: if
+the library is missing or fails to load, every query entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcwq.so")
+
+CWQ_OK = 0
+CWQ_ERR_ARG = -1
+CWQ_ERR_HIP = -2
+CWQ_ERR_OOM = -3
+CWQ_ERR_NOT_FOUND = -4
+
+# symbol -> (restype, argtypes); mirrors include/cobweb_query.h
+_c = ctypes
+_P = _c.c_void_p
+_I64 = _c.c_int64
+_I32 = _c.c_int32
+SIGNATURES = {
+    "cwq_version": (_c.c_int, []),
+    "cwq_last_error": (_c.c_char_p, []),
+    "cwq_index_create": (_c.c_int, [_c.c_int, _I64, _I32, _P, _P, _P, _P, _I64, _P, _I32, _P, _c.POINTER(_P)]),
+    "cwq_index_destroy": (_c.c_int, [_P]),
+    "cwq_index_info": (_c.c_int, [_P, _P]),
+    "cwq_score_topk": (_c.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
+    "cwq_rank_scores": (_c.c_int, [_P, _P, _I64, _P, _P]),
+    "cwq_node_logprob": (_c.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "cwq_categorize": (_c.c_int, [_P, _P, _I64, _I32, _I64, _P, _P, _P, _P]),
+    "cwq_set_timing": (_c.c_int, [_P, _c.c_int]),
+    "cwq_last_timing": (_c.c_int, [_P, _P]),
+    "cwq_welford_groups": (_c.c_int, [_P, _I64, _I32, _P, _P, _I64, _P, _P, _P, _P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class CwqError(RuntimeError):
+    """A libcwq call returned an error status."""
+
+    def __init__(self, rc, msg):
+        super().__init__(f"libcwq error {rc}: {msg}")
+        self.rc = rc
+
+
+def lib():
+    """Load libcwq.so (once).  Raises ImportError when it is not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(f"{LIB_PATH} is missing: build it with __graft_entry__.build()")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != CWQ_OK:
+        raise CwqError(rc, lib().cwq_last_error().decode(errors="replace"))

@@ -1,0 +1,799 @@
+// libcwq C ABI: index construction and query orchestration (host side).
+// Public contract: include/cobweb_query.h.  Kernels: cwq_kernels.hip.
+//
+// Index layout in HBM:
+//   internal nodes (nodes with children), BFS order:     A = 1/sigma, B = mu/sigma  [DP][ld_int]
+//   leaf-class rows (childless nodes + internal nodes that hold sentences),
+//     isotropic rows first (var identical across d):    M = mu                      [DP][ld_iso]
+//     then anisotropic rows:                            A = 1/sigma, B = mu/sigma   [DP][ld_an]
+//   dim-major ("transposed") so a wave's 64 lanes = 64 consecutive rows read one
+//   coalesced 256-B line per dimension.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cobweb_query.h"
+#include "cwq_internal.h"
+
+using namespace cwq;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess) return fail(CWQ_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Bump allocator over the handle's workspace.
+struct Bump {
+  char* base;
+  size_t off = 0, cap;
+  Bump(void* b, size_t c) : base((char*)b), cap(c) {}
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~size_t(255);
+    T* p = (T*)(base + off);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct cwq_index {
+  int device = 0;
+  int64_t n_nodes = 0, n_sent = 0;
+  int D = 0, DP = 0;
+  int NI = 0, NL = 0, NL_iso = 0, NL_an = 0;
+  int64_t ld_int = 0, ld_iso = 0, ld_an = 0;
+  int max_depth = 0;
+  int cus = 256;
+  std::vector<std::pair<int, int>> levels;   // internal-node ranges, one per depth
+  std::vector<void*> allocs;
+  size_t bytes = 0;
+  // row data
+  float *int_A = nullptr, *int_B = nullptr, *iso_M = nullptr, *an_A = nullptr, *an_B = nullptr;
+  RowMeta* row_meta = nullptr;
+  int *row_par = nullptr, *row_flags = nullptr, *row_bfs = nullptr;
+  float* logdet_row = nullptr;
+  float *logdet_int = nullptr, *w_int = nullptr;
+  int *par_int = nullptr, *int_child_begin = nullptr, *int_child_end = nullptr, *int_nchild = nullptr;
+  int *int_bfs = nullptr, *int_has_sent = nullptr;
+  int *int_leaf_a0 = nullptr, *int_leaf_a1 = nullptr, *int_leaf_b0 = nullptr, *int_leaf_b1 = nullptr;
+  int64_t *sent_ptr = nullptr, *sent_ids = nullptr;
+  int* row_of_sent = nullptr;
+  int* node_src = nullptr;
+  float* dummy = nullptr;
+  // timing (cwq_set_timing)
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float t_ms[5] = {0, 0, 0, 0, 0};
+  // workspace
+  std::mutex mu;
+  void* ws = nullptr;
+  size_t ws_size = 0;
+
+  template <class T>
+  int alloc(T** p, size_t n) {
+    void* q = nullptr;
+    const size_t b = std::max<size_t>(n, 1) * sizeof(T);
+    if (hipMalloc(&q, b) != hipSuccess) return fail(CWQ_ERR_OOM, "hipMalloc failed (" + std::to_string(b) + " B)");
+    allocs.push_back(q);
+    bytes += b;
+    *p = (T*)q;
+    return CWQ_OK;
+  }
+  template <class T>
+  int upload(T** p, const std::vector<T>& v, hipStream_t s) {
+    int rc = alloc(p, v.size());
+    if (rc) return rc;
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return CWQ_OK;
+  }
+  int reserve(size_t b) {
+    if (b <= ws_size) return CWQ_OK;
+    if (ws) (void)hipFree(ws);
+    ws = nullptr;
+    ws_size = 0;
+    b = round_up((int64_t)b, 1 << 20);
+    if (hipMalloc(&ws, b) != hipSuccess) return fail(CWQ_ERR_OOM, "workspace hipMalloc failed (" + std::to_string(b) + " B)");
+    ws_size = b;
+    return CWQ_OK;
+  }
+  ~cwq_index() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (void* p : allocs) (void)hipFree(p);
+    if (ws) (void)hipFree(ws);
+  }
+};
+
+extern "C" int cwq_version(void) { return 100; }
+extern "C" const char* cwq_last_error(void) { return g_err.c_str(); }
+
+extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var,
+                                const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
+                                const double* level_w, int32_t n_w, void* stream, cwq_index** out) {
+  if (!out) return fail(CWQ_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n_nodes <= 0 || dim <= 0 || !mean || !var || !parent) return fail(CWQ_ERR_ARG, "empty tree or NULL inputs");
+  if (n_nodes >= (int64_t)INT32_MAX / 2) return fail(CWQ_ERR_ARG, "too many nodes");
+  if (n_sent < 0 || (n_sent > 0 && !node_of_sentence)) return fail(CWQ_ERR_ARG, "bad sentence map");
+  DevGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+
+  // ---- structure (host) ----
+  if (parent[0] != -1) return fail(CWQ_ERR_ARG, "parent[0] must be -1 (root first, BFS order)");
+  std::vector<int> depth(n_nodes, 0), nchild(n_nodes, 0);
+  for (int64_t i = 1; i < n_nodes; ++i) {
+    const int64_t p = parent[i];
+    if (p < 0 || p >= i) return fail(CWQ_ERR_ARG, "parent[i] must be in [0, i) (BFS order)");
+    if (p < parent[i - 1]) return fail(CWQ_ERR_ARG, "parent array must be non-decreasing (BFS order)");
+    depth[i] = depth[p] + 1;
+    nchild[p]++;
+  }
+  std::vector<std::vector<int64_t>> sents(n_nodes);
+  for (int64_t sidx = 0; sidx < n_sent; ++sidx) {
+    const int64_t nd = node_of_sentence[sidx];
+    if (nd < -1 || nd >= n_nodes) return fail(CWQ_ERR_ARG, "node_of_sentence out of range");
+    if (nd >= 0) sents[nd].push_back(sidx);
+  }
+  std::unique_ptr<cwq_index> ix(new cwq_index());
+  ix->device = device;
+  ix->n_nodes = n_nodes;
+  ix->n_sent = n_sent;
+  ix->D = dim;
+  ix->DP = (int)round_up(dim, kDChunk);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ix->cus = prop.multiProcessorCount;
+
+  std::vector<int64_t> int_nodes, leaf_nodes;
+  std::vector<int> int_id(n_nodes, -1);
+  for (int64_t i = 0; i < n_nodes; ++i) {
+    if (nchild[i] > 0) {
+      int_id[i] = (int)int_nodes.size();
+      int_nodes.push_back(i);
+    }
+    if (nchild[i] == 0 || !sents[i].empty()) leaf_nodes.push_back(i);
+    ix->max_depth = std::max(ix->max_depth, depth[i]);
+  }
+  ix->NI = (int)int_nodes.size();
+  const int64_t nleaf = (int64_t)leaf_nodes.size();
+
+  // isotropy of leaf-class rows (device)
+  int64_t* d_leaf_nodes = nullptr;
+  int* d_iso = nullptr;
+  int rc = ix->upload(&d_leaf_nodes, leaf_nodes, s);
+  if (rc) return rc;
+  if ((rc = ix->alloc(&d_iso, nleaf))) return rc;
+  HIPCHK(launch_iso_flags(var, dim, d_leaf_nodes, nleaf, d_iso, s));
+  std::vector<int> iso(nleaf);
+  HIPCHK(hipMemcpyAsync(iso.data(), d_iso, nleaf * sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+
+  std::vector<int64_t> rows_iso, rows_an;
+  for (int64_t r = 0; r < nleaf; ++r) (iso[r] ? rows_iso : rows_an).push_back(leaf_nodes[r]);
+  ix->NL_iso = (int)rows_iso.size();
+  ix->NL_an = (int)rows_an.size();
+  ix->NL = ix->NL_iso + ix->NL_an;
+  std::vector<int64_t> rows(rows_iso);
+  rows.insert(rows.end(), rows_an.begin(), rows_an.end());
+  std::vector<int> row_of_node(n_nodes, -1);
+  for (int r = 0; r < ix->NL; ++r) row_of_node[rows[r]] = r;
+
+  auto wdepth = [&](int d) -> double { return d < n_w ? level_w[d] : 1.0; };
+
+  // leaf-row metadata
+  std::vector<RowMeta> meta(ix->NL);
+  std::vector<int> row_par(ix->NL), row_flags(ix->NL), row_bfs(ix->NL);
+  std::vector<int64_t> sptr(ix->NL + 1, 0), sids;
+  std::vector<int> row_of_sent(n_sent, -1);
+  for (int r = 0; r < ix->NL; ++r) {
+    const int64_t nd = rows[r];
+    const int L = depth[nd] + 1;
+    meta[r].cw = (float)(wdepth(depth[nd]) / L);
+    meta[r].invL = (float)(1.0 / L);
+    row_par[r] = parent[nd] >= 0 ? int_id[parent[nd]] : -1;
+    row_flags[r] = (sents[nd].empty() ? 0 : FLAG_HAS_SENT) | (nchild[nd] > 0 ? FLAG_INT_COPY : 0);
+    row_bfs[r] = (int)nd;
+    for (int64_t sidx : sents[nd]) {
+      sids.push_back(sidx);
+      row_of_sent[sidx] = r;
+    }
+    sptr[r + 1] = (int64_t)sids.size();
+  }
+  // internal-node metadata
+  std::vector<int> par_int(ix->NI), cb(ix->NI, 0), ce(ix->NI, 0), ibfs(ix->NI), ihs(ix->NI), inch(ix->NI);
+  std::vector<int> la0(ix->NI, 0), la1(ix->NI, 0), lb0(ix->NI, 0), lb1(ix->NI, 0);
+  std::vector<float> w_int(ix->NI);
+  for (int i = 0; i < ix->NI; ++i) {
+    const int64_t nd = int_nodes[i];
+    par_int[i] = parent[nd] >= 0 ? int_id[parent[nd]] : -1;
+    ibfs[i] = (int)nd;
+    ihs[i] = sents[nd].empty() ? 0 : 1;
+    inch[i] = nchild[nd];
+    w_int[i] = (float)wdepth(depth[nd]);
+    cb[i] = ce[i] = -1;
+    la0[i] = la1[i] = lb0[i] = lb1[i] = -1;
+  }
+  for (int64_t nd = 1; nd < n_nodes; ++nd) {   // children ranges (contiguous in each ordering)
+    const int pi = int_id[parent[nd]];
+    if (int_id[nd] >= 0) {
+      if (cb[pi] < 0) cb[pi] = int_id[nd];
+      ce[pi] = int_id[nd] + 1;
+    }
+    const int r = row_of_node[nd];
+    if (r >= 0) {
+      if (r < ix->NL_iso) {
+        if (la0[pi] < 0) la0[pi] = r;
+        la1[pi] = r + 1;
+      } else {
+        if (lb0[pi] < 0) lb0[pi] = r;
+        lb1[pi] = r + 1;
+      }
+    }
+  }
+  for (int i = 0; i < ix->NI; ++i) {
+    if (cb[i] < 0) cb[i] = ce[i] = 0;
+    if (la0[i] < 0) la0[i] = la1[i] = 0;
+    if (lb0[i] < 0) lb0[i] = lb1[i] = 0;
+  }
+  for (int i = 0; i < ix->NI;) {   // levels (BFS -> depth non-decreasing)
+    int j = i;
+    const int d0 = depth[int_nodes[i]];
+    while (j < ix->NI && depth[int_nodes[j]] == d0) ++j;
+    ix->levels.push_back({i, j});
+    i = j;
+  }
+  std::vector<int> node_src(n_nodes);
+  for (int64_t nd = 0; nd < n_nodes; ++nd) node_src[nd] = int_id[nd] >= 0 ? int_id[nd] : -(row_of_node[nd] + 1);
+
+  // ---- device arrays ----
+  const int DP = ix->DP;
+  ix->ld_int = round_up(std::max(ix->NI, 1), kWave);
+  ix->ld_iso = round_up(std::max(ix->NL_iso, 1), kWave);
+  ix->ld_an = round_up(std::max(ix->NL_an, 1), kWave);
+  int64_t *d_int_nodes = nullptr, *d_rows = nullptr;
+  if ((rc = ix->upload(&d_int_nodes, int_nodes, s))) return rc;
+  if ((rc = ix->upload(&d_rows, rows, s))) return rc;
+  if ((rc = ix->alloc(&ix->int_A, (size_t)DP * ix->ld_int))) return rc;
+  if ((rc = ix->alloc(&ix->int_B, (size_t)DP * ix->ld_int))) return rc;
+  if ((rc = ix->alloc(&ix->iso_M, (size_t)DP * ix->ld_iso))) return rc;
+  if ((rc = ix->alloc(&ix->an_A, (size_t)DP * ix->ld_an))) return rc;
+  if ((rc = ix->alloc(&ix->an_B, (size_t)DP * ix->ld_an))) return rc;
+  HIPCHK(launch_gather_T(mean, var, dim, d_int_nodes, ix->NI, 1, ix->int_A, ix->ld_int, DP, s));
+  HIPCHK(launch_gather_T(mean, var, dim, d_int_nodes, ix->NI, 2, ix->int_B, ix->ld_int, DP, s));
+  HIPCHK(launch_gather_T(mean, var, dim, d_rows, ix->NL_iso, 0, ix->iso_M, ix->ld_iso, DP, s));
+  HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 1, ix->an_A, ix->ld_an, DP, s));
+  HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 2, ix->an_B, ix->ld_an, DP, s));
+
+  if ((rc = ix->alloc(&ix->logdet_int, ix->NI))) return rc;
+  if ((rc = ix->alloc(&ix->logdet_row, ix->NL))) return rc;
+  HIPCHK(launch_logdet(var, dim, d_int_nodes, ix->NI, ix->logdet_int, s));
+  HIPCHK(launch_logdet(var, dim, d_rows, ix->NL, ix->logdet_row, s));
+  float* d_iv = nullptr;
+  if ((rc = ix->alloc(&d_iv, ix->NL))) return rc;
+  HIPCHK(hipMemsetAsync(d_iv, 0, std::max(ix->NL, 1) * sizeof(float), s));
+  HIPCHK(launch_inv_var0(var, dim, d_rows, ix->NL_iso, d_iv, s));
+  std::vector<float> ldr(ix->NL), ivh(ix->NL);
+  if (ix->NL) {
+    HIPCHK(hipMemcpyAsync(ldr.data(), ix->logdet_row, ix->NL * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ivh.data(), d_iv, ix->NL * sizeof(float), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  for (int r = 0; r < ix->NL; ++r) {
+    meta[r].logdet = ldr[r];
+    meta[r].iv = ivh[r];
+  }
+  if ((rc = ix->upload(&ix->row_meta, meta, s))) return rc;
+  if ((rc = ix->upload(&ix->row_par, row_par, s))) return rc;
+  if ((rc = ix->upload(&ix->row_flags, row_flags, s))) return rc;
+  if ((rc = ix->upload(&ix->row_bfs, row_bfs, s))) return rc;
+  if ((rc = ix->upload(&ix->par_int, par_int, s))) return rc;
+  if ((rc = ix->upload(&ix->w_int, w_int, s))) return rc;
+  if ((rc = ix->upload(&ix->int_child_begin, cb, s))) return rc;
+  if ((rc = ix->upload(&ix->int_child_end, ce, s))) return rc;
+  if ((rc = ix->upload(&ix->int_nchild, inch, s))) return rc;
+  if ((rc = ix->upload(&ix->int_bfs, ibfs, s))) return rc;
+  if ((rc = ix->upload(&ix->int_has_sent, ihs, s))) return rc;
+  if ((rc = ix->upload(&ix->int_leaf_a0, la0, s))) return rc;
+  if ((rc = ix->upload(&ix->int_leaf_a1, la1, s))) return rc;
+  if ((rc = ix->upload(&ix->int_leaf_b0, lb0, s))) return rc;
+  if ((rc = ix->upload(&ix->int_leaf_b1, lb1, s))) return rc;
+  if ((rc = ix->upload(&ix->sent_ptr, sptr, s))) return rc;
+  if ((rc = ix->upload(&ix->sent_ids, sids, s))) return rc;
+  if ((rc = ix->upload(&ix->row_of_sent, row_of_sent, s))) return rc;
+  if ((rc = ix->upload(&ix->node_src, node_src, s))) return rc;
+  if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
+  HIPCHK(hipStreamSynchronize(s));
+  *out = ix.release();
+  return CWQ_OK;
+}
+
+extern "C" int cwq_index_destroy(cwq_index* idx) {
+  if (!idx) return CWQ_OK;
+  DevGuard dg(idx->device);
+  delete idx;
+  return CWQ_OK;
+}
+
+extern "C" int cwq_index_info(const cwq_index* idx, int64_t* o) {
+  if (!idx || !o) return fail(CWQ_ERR_ARG, "NULL argument");
+  o[0] = idx->n_nodes;
+  o[1] = idx->D;
+  o[2] = idx->n_sent;
+  o[3] = idx->NI;
+  o[4] = idx->NL;
+  o[5] = idx->NL_iso;
+  o[6] = idx->max_depth;
+  o[7] = (int64_t)idx->bytes;
+  return CWQ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Query orchestration
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kQPad = 128;   // queries are padded to a multiple of the largest query block
+
+struct Chunk {
+  int nq = 0;           // valid queries
+  int64_t nq_pad = 0;
+  float* X = nullptr;   // [nq_pad][DP]
+  float *S_int = nullptr, *P = nullptr, *BF = nullptr, *LPF = nullptr;   // [nq_pad][NI]
+};
+
+// Choose the slab split of a segment so that the grid has ~8 waves of workgroups.
+int pick_nslab(const cwq_index* ix, int nrows, int n_qblocks) {
+  if (nrows <= 0) return 0;
+  const int target = std::max(1, 8 * 4 * ix->cus);
+  const int max_slab = (int)std::max<int64_t>(1, round_up(nrows, kWave) / 256);
+  int n = (target + n_qblocks - 1) / n_qblocks;
+  return std::max(1, std::min(n, max_slab));
+}
+
+ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.DP = ix->DP;
+  a.nq = c.nq;
+  a.meta = ix->row_meta;
+  a.par = ix->row_par;
+  a.flags = ix->row_flags;
+  a.P = c.P ? c.P : ix->dummy;
+  a.ldP = std::max(ix->NI, 1);
+  return a;
+}
+
+// Internal nodes: raw sums -> P (path prefix), BF (bottleneck), LPF (full lp).
+int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
+  if (ix->NI == 0) return CWQ_OK;
+  ScanArgs a = base_args(ix, c);
+  const int kl = 64, tq = scan_tq(kl);
+  a.ld = ix->ld_int;
+  a.nrows = ix->NI;
+  a.nrows_pad = (int)round_up(ix->NI, kWave);
+  a.n_qblocks = (int)((c.nq + 4 * tq - 1) / (4 * tq));
+  const int nslab = pick_nslab(ix, ix->NI, a.n_qblocks);
+  a.rows_per_slab = (int)round_up((a.nrows_pad + nslab - 1) / nslab, kWave);
+  const int nslab2 = (a.nrows_pad + a.rows_per_slab - 1) / a.rows_per_slab;
+  a.out = c.S_int;
+  a.ldo = ix->NI;
+  HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
+  const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
+  for (auto& lv : ix->levels)
+    HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
+                               dfull, c.P, c.BF, c.LPF, s));
+  return CWQ_OK;
+}
+
+// One scan over both leaf-row segments.
+int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
+                  float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s) {
+  const int tq = scan_tq(kl);
+  const int nqb = (int)((c.nq + 4 * tq - 1) / (4 * tq));
+  struct Seg {
+    bool iso;
+    int n;
+    int base;
+    const float *A, *B;
+    int64_t ld;
+  } segs[2] = {{true, ix->NL_iso, 0, ix->iso_M, ix->iso_M, ix->ld_iso},
+               {false, ix->NL_an, ix->NL_iso, ix->an_A, ix->an_B, ix->ld_an}};
+  int ns[2], rps[2];
+  for (int i = 0; i < 2; ++i) {
+    ns[i] = 0;
+    rps[i] = 0;
+    if (segs[i].n == 0) continue;
+    const int npad = (int)round_up(segs[i].n, kWave);
+    const int n = pick_nslab(ix, segs[i].n, nqb);
+    rps[i] = (int)round_up((npad + n - 1) / n, kWave);
+    ns[i] = (npad + rps[i] - 1) / rps[i];
+  }
+  const int nslab_total = ns[0] + ns[1];
+  if (nslab_total_out) *nslab_total_out = nslab_total;
+  int slab_off = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (segs[i].n == 0) continue;
+    ScanArgs a = base_args(ix, c);
+    a.ld = segs[i].ld;
+    a.nrows = segs[i].n;
+    a.nrows_pad = (int)round_up(segs[i].n, kWave);
+    a.rows_per_slab = rps[i];
+    a.n_qblocks = nqb;
+    a.seg_base = segs[i].base;
+    a.meta = ix->row_meta + segs[i].base;
+    a.par = ix->row_par + segs[i].base;
+    a.flags = ix->row_flags + segs[i].base;
+    a.dconst = dconst;
+    a.out = out;
+    a.ldo = ldo;
+    a.out_base = segs[i].base;
+    a.pkey = pkey;
+    a.paux = paux;
+    a.prow = prow;
+    a.nslab_total = nslab_total;
+    a.slab_off = slab_off;
+    a.K = K;
+    HIPCHK(launch_scan(segs[i].iso, epi, cat, kl, c.X, segs[i].A, segs[i].B, a, ns[i], s));
+    slab_off += ns[i];
+  }
+  return CWQ_OK;
+}
+
+// Workspace for one chunk: X + internal arrays.
+size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad) {
+  return (size_t)nq_pad * ix->DP * 4 + 4 * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256;
+}
+
+void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
+  c.nq = nq;
+  c.nq_pad = round_up(nq, kQPad);
+  c.X = b.take<float>((size_t)c.nq_pad * ix->DP);
+  if (ix->NI > 0) {
+    const size_t n = (size_t)c.nq_pad * ix->NI;
+    c.S_int = b.take<float>(n);
+    c.P = b.take<float>(n);
+    c.BF = b.take<float>(n);
+    c.LPF = b.take<float>(n);
+  }
+}
+
+// Query-chunk size that keeps the per-chunk workspace within ~2 GiB (min 128).
+int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
+  const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
+  const size_t budget = (size_t)2 << 30;
+  int64_t c = (int64_t)std::max<size_t>(kQPad, budget / std::max<size_t>(per_q, 1));
+  c = std::max<int64_t>(kQPad, c / kQPad * kQPad);
+  return std::min(nq, c);
+}
+
+}  // namespace
+
+extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                              void* stream) {
+  if (!ix || (!q && nq > 0) || (!ids && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  for (float& t : ix->t_ms) t = 0.f;
+  const bool general = k > 64;
+  const int kl = k <= 16 ? 16 : 64;
+  const int K = std::min<int>(k, 64);
+  const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));
+  // partial-list entries per query (upper bound over both segments)
+  const int tq = scan_tq(kl);
+  const int64_t nq_est = std::min<int64_t>(nq, 1 << 20);
+  const int nqb_est = (int)((nq_est + 4 * tq - 1) / (4 * tq));
+  const int max_slabs = pick_nslab(ix, ix->NL_iso, std::max(1, nqb_est / 64)) +
+                        pick_nslab(ix, ix->NL_an, std::max(1, nqb_est / 64)) + 2;
+  const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8 : (size_t)max_slabs * K * 12 + K * 12;
+  const int64_t cq = chunk_queries(ix, nq, extra);
+  int rc;
+  for (int64_t q0 = 0; q0 < nq; q0 += cq) {
+    const int nqc = (int)std::min(cq, nq - q0);
+    const int64_t nq_pad = round_up(nqc, kQPad);
+    const int nqb = (int)((nqc + 4 * tq - 1) / (4 * tq));
+    const int slabs = pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2;
+    size_t need = chunk_bytes(ix, nq_pad) + 16 * 256;
+    need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
+                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12);
+    if ((rc = ix->reserve(need))) return rc;
+    Bump b(ix->ws, ix->ws_size);
+    Chunk c;
+    carve_chunk(ix, b, c, nqc);
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
+    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if ((rc = run_internal(ix, c, s))) return rc;
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
+    if (!general) {
+      float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
+      float* paux = b.take<float>((size_t)nq_pad * slabs * K);
+      int* prow = b.take<int>((size_t)nq_pad * slabs * K);
+      float* okey = b.take<float>((size_t)nq_pad * K);
+      float* oaux = b.take<float>((size_t)nq_pad * K);
+      int* orow = b.take<int>((size_t)nq_pad * K);
+      int nst = 0;
+      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s))) return rc;
+      if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
+      HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
+      HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
+                           scores ? scores + q0 * k : nullptr, s));
+    } else {
+      float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
+      float* skey = b.take<float>((size_t)nq_pad * n_pow2);
+      int* srow = b.take<int>((size_t)nq_pad * n_pow2);
+      if ((rc = run_leaf_scan(ix, c, EPI_KEY, false, 16, 0.f, rowkey, ix->NL, nullptr, nullptr, nullptr, 1, nullptr, s)))
+        return rc;
+      if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
+      HIPCHK(launch_init_rows(rowkey, ix->NL, nqc, ix->NL, n_pow2, skey, srow, s));
+      HIPCHK(launch_sort_rows(skey, srow, nqc, ix->NL, n_pow2, s));
+      HIPCHK(launch_expand(skey, srow, nqc, n_pow2, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
+                           scores ? scores + q0 * k : nullptr, s));
+    }
+    if (ix->timing) {
+      HIPCHK(hipEventRecord(ix->ev[3], s));
+      HIPCHK(hipEventSynchronize(ix->ev[3]));
+      float a = 0, b = 0, c2 = 0, d = 0;
+      HIPCHK(hipEventElapsedTime(&a, ix->ev[1], ix->ev[2]));
+      HIPCHK(hipEventElapsedTime(&b, ix->ev[0], ix->ev[1]));
+      HIPCHK(hipEventElapsedTime(&c2, ix->ev[2], ix->ev[3]));
+      HIPCHK(hipEventElapsedTime(&d, ix->ev[0], ix->ev[3]));
+      ix->t_ms[0] += a;
+      ix->t_ms[1] += b;
+      ix->t_ms[2] += c2;
+      ix->t_ms[3] += d;
+      ix->t_ms[4] += (ix->NL_iso > 0) + (ix->NL_an > 0);
+    }
+  }
+  return CWQ_OK;
+}
+
+extern "C" int cwq_set_timing(cwq_index* ix, int enable) {
+  if (!ix) return fail(CWQ_ERR_ARG, "NULL index");
+  DevGuard dg(ix->device);
+  for (int i = 0; i < 4; ++i)
+    if (!ix->ev[i]) HIPCHK(hipEventCreate(&ix->ev[i]));
+  ix->timing = enable != 0;
+  return CWQ_OK;
+}
+
+extern "C" int cwq_last_timing(cwq_index* ix, float* out) {
+  if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
+  for (int i = 0; i < 5; ++i) out[i] = ix->t_ms[i];
+  return CWQ_OK;
+}
+
+extern "C" int cwq_rank_scores(cwq_index* ix, const float* q, int64_t nq, float* out, void* stream) {
+  if (!ix || (!q && nq > 0) || (!out && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
+  int rc;
+  for (int64_t q0 = 0; q0 < nq; q0 += cq) {
+    const int nqc = (int)std::min(cq, nq - q0);
+    const int64_t nq_pad = round_up(nqc, kQPad);
+    if ((rc = ix->reserve(chunk_bytes(ix, nq_pad) + (size_t)nq_pad * std::max(ix->NL, 1) * 4 + 8 * 256))) return rc;
+    Bump b(ix->ws, ix->ws_size);
+    Chunk c;
+    carve_chunk(ix, b, c, nqc);
+    float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
+    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if ((rc = run_internal(ix, c, s))) return rc;
+    if ((rc = run_leaf_scan(ix, c, EPI_KEY, false, 16, 0.f, rowkey, ix->NL, nullptr, nullptr, nullptr, 1, nullptr, s)))
+      return rc;
+    HIPCHK(launch_gather_sentences(rowkey, ix->NL, nqc, ix->row_of_sent, ix->n_sent, out + q0 * ix->n_sent, s));
+  }
+  return CWQ_OK;
+}
+
+extern "C" int cwq_node_logprob(cwq_index* ix, const float* q, int64_t nq, int32_t full, float* out, void* stream) {
+  if (!ix || (!q && nq > 0) || (!out && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  const float dconst = full ? (float)((double)ix->D * (double)logf(2.0f * (float)M_PI)) : 0.f;
+  const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
+  int rc;
+  for (int64_t q0 = 0; q0 < nq; q0 += cq) {
+    const int nqc = (int)std::min(cq, nq - q0);
+    const int64_t nq_pad = round_up(nqc, kQPad);
+    if ((rc = ix->reserve(chunk_bytes(ix, nq_pad) + (size_t)nq_pad * std::max(ix->NL, 1) * 4 + 8 * 256))) return rc;
+    Bump b(ix->ws, ix->ws_size);
+    Chunk c;
+    carve_chunk(ix, b, c, nqc);
+    float* sleaf = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
+    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if ((rc = run_internal(ix, c, s))) return rc;
+    if ((rc = run_leaf_scan(ix, c, EPI_RAW, false, 16, 0.f, sleaf, ix->NL, nullptr, nullptr, nullptr, 1, nullptr, s)))
+      return rc;
+    HIPCHK(launch_node_lp(c.S_int ? c.S_int : ix->dummy, std::max(ix->NI, 1), sleaf, std::max(ix->NL, 1), nqc,
+                          ix->node_src, ix->logdet_int, ix->logdet_row, dconst, ix->n_nodes, out + q0 * ix->n_nodes, s));
+  }
+  return CWQ_OK;
+}
+
+extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
+                              int32_t* n_found, int64_t* n_calls, void* stream) {
+  if (!ix || (!q && nq > 0) || (nq > 0 && (!nodes || !n_found))) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
+  const int R = std::max(1, std::min(64, ix->NL));
+  const bool complete = ix->NL <= R;
+  const int64_t cap_list = 1 + (int64_t)ix->NI + R;
+  const int kl = 64, tq = scan_tq(kl);
+  int rc;
+  const int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + 64 * 12 * 64);
+  for (int64_t q0 = 0; q0 < nq; q0 += cq) {
+    const int nqc = (int)std::min(cq, nq - q0);
+    const int64_t nq_pad = round_up(nqc, kQPad);
+    const int nqb = (int)((nqc + 4 * tq - 1) / (4 * tq));
+    const int slabs = pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2;
+    size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
+                                                              (size_t)cap_list * 16 + 8) + 16 * 256;
+    if ((rc = ix->reserve(need))) return rc;
+    Bump b(ix->ws, ix->ws_size);
+    Chunk c;
+    carve_chunk(ix, b, c, nqc);
+    float* pkey = b.take<float>((size_t)nq_pad * slabs * R);
+    float* paux = b.take<float>((size_t)nq_pad * slabs * R);
+    int* prow = b.take<int>((size_t)nq_pad * slabs * R);
+    float* okey = b.take<float>((size_t)nq_pad * R);
+    float* oaux = b.take<float>((size_t)nq_pad * R);
+    int* orow = b.take<int>((size_t)nq_pad * R);
+    HeapEnt* heap = b.take<HeapEnt>((size_t)nq_pad * cap_list);
+    int* status = b.take<int>((size_t)nq_pad);
+    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if ((rc = run_internal(ix, c, s))) return rc;
+    int nst = 0;
+    if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s))) return rc;
+    HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s));
+    SimArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.nq = nqc;
+    sa.k = k;
+    sa.R = R;
+    sa.max_nodes = max_nodes;
+    sa.NI = ix->NI;
+    sa.NL = ix->NL;
+    sa.LPF = c.LPF ? c.LPF : ix->dummy;
+    sa.BF = c.BF ? c.BF : ix->dummy;
+    sa.ldI = std::max(ix->NI, 1);
+    sa.lkey = okey;
+    sa.laux = oaux;
+    sa.lrow = orow;
+    sa.complete = complete ? 1 : 0;
+    sa.int_child_begin = ix->int_child_begin;
+    sa.int_child_end = ix->int_child_end;
+    sa.int_nchild = ix->int_nchild;
+    sa.int_bfs = ix->int_bfs;
+    sa.int_has_sent = ix->int_has_sent;
+    sa.int_leaf_a0 = ix->int_leaf_a0;
+    sa.int_leaf_a1 = ix->int_leaf_a1;
+    sa.int_leaf_b0 = ix->int_leaf_b0;
+    sa.int_leaf_b1 = ix->int_leaf_b1;
+    sa.row_par = ix->row_par;
+    sa.row_bfs = ix->row_bfs;
+    sa.row_flags = ix->row_flags;
+    sa.heap = heap;
+    sa.heap_cap = cap_list;
+    sa.out_nodes = nodes + q0 * k;
+    sa.n_found = n_found + q0;
+    sa.n_calls = n_calls ? n_calls + q0 : nullptr;
+    sa.status = status;
+    HIPCHK(launch_simulate(sa, s));
+    std::vector<int> st(nqc);
+    HIPCHK(hipMemcpyAsync(st.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<int> redo;
+    for (int i = 0; i < nqc; ++i)
+      if (st[i]) redo.push_back(i);
+    if (redo.empty()) continue;
+
+    // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
+    const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
+    const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ix->NL * 4 +
+                         (size_t)cap_dense * 16 + 64;
+    const int64_t sub = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q));
+    std::vector<float> hx;
+    for (size_t r0 = 0; r0 < redo.size(); r0 += sub) {
+      const int ns = (int)std::min<int64_t>(sub, (int64_t)redo.size() - (int64_t)r0);
+      const int64_t ns_pad = round_up(ns, kQPad);
+      if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) + (size_t)ns_pad * ((size_t)ix->NL * 4 + cap_dense * 16 + 64) +
+                            16 * 256 + (size_t)ns_pad * ix->D * 4)))
+        return rc;
+      Bump b2(ix->ws, ix->ws_size);
+      Chunk c2;
+      carve_chunk(ix, b2, c2, ns);
+      float* qsub = b2.take<float>((size_t)ns * ix->D);
+      float* dense = b2.take<float>((size_t)ns_pad * std::max(ix->NL, 1));
+      HeapEnt* heap2 = b2.take<HeapEnt>((size_t)ns_pad * cap_dense);
+      int* status2 = b2.take<int>(ns_pad);
+      int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
+      int* found2 = b2.take<int>(ns_pad);
+      int64_t* calls2 = b2.take<int64_t>(ns_pad);
+      for (int i = 0; i < ns; ++i)
+        HIPCHK(hipMemcpyAsync(qsub + (size_t)i * ix->D, q + (q0 + redo[r0 + i]) * ix->D, ix->D * sizeof(float),
+                              hipMemcpyDeviceToDevice, s));
+      HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
+      if ((rc = run_internal(ix, c2, s))) return rc;
+      if ((rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1, nullptr,
+                              s)))
+        return rc;
+      SimArgs sd = sa;
+      sd.nq = ns;
+      sd.R = 0;
+      sd.LPF = c2.LPF ? c2.LPF : ix->dummy;
+      sd.BF = c2.BF ? c2.BF : ix->dummy;
+      sd.dense_lpf = dense;
+      sd.ldL = std::max(ix->NL, 1);
+      sd.lkey = okey;
+      sd.laux = oaux;
+      sd.lrow = orow;
+      sd.heap = heap2;
+      sd.heap_cap = cap_dense;
+      sd.out_nodes = nodes2;
+      sd.n_found = found2;
+      sd.n_calls = calls2;
+      sd.status = status2;
+      HIPCHK(launch_simulate(sd, s));
+      for (int i = 0; i < ns; ++i) {
+        const int64_t qq = q0 + redo[r0 + i];
+        HIPCHK(hipMemcpyAsync(nodes + qq * k, nodes2 + (size_t)i * k, k * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(n_found + qq, found2 + i, sizeof(int), hipMemcpyDeviceToDevice, s));
+        if (n_calls) HIPCHK(hipMemcpyAsync(n_calls + qq, calls2 + i, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+      }
+      HIPCHK(hipStreamSynchronize(s));
+    }
+  }
+  return CWQ_OK;
+}
+
+extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order,
+                                  const int64_t* group_ptr, int64_t n_groups, float* count, float* mean,
+                                  float* meanSq, void* stream) {
+  if (!X || !order || !group_ptr || !count || !mean || !meanSq || dim <= 0 || n_rows < 0)
+    return fail(CWQ_ERR_ARG, "bad arguments");
+  if (n_groups > 65535) return fail(CWQ_ERR_ARG, "at most 65535 groups per call");
+  HIPCHK(launch_welford_groups(X, dim, order, group_ptr, n_groups, count, mean, meanSq, (hipStream_t)stream));
+  return CWQ_OK;
+}

@@ -1,0 +1,117 @@
+// Internal declarations shared by the libcwq kernels (cwq_kernels.hip) and the
+// C-ABI host runtime (cwq_api.hip).  Not part of the public interface.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cwq {
+
+constexpr int kWave = 64;        // CDNA wavefront
+constexpr int kWavesPerWG = 4;   // 256-thread workgroups
+constexpr int kDChunk = 16;      // dimensions held in registers per step (D padded to this)
+
+// Per leaf-class row constants (one float4 load per lane in the epilogue).
+struct RowMeta {
+  float logdet;  // sum_d log v  (fp64-accumulated, rounded once)
+  float iv;      // 1/v for isotropic rows (v identical across d), unused otherwise
+  float cw;      // fp32(level_w[depth] / path_len)   -- CobwebWrapper.py:166-168
+  float invL;    // fp32(1 / path_len)
+};
+
+enum Epi { EPI_RAW = 0, EPI_KEY = 1, EPI_TOPK = 2 };
+
+// Row flags
+constexpr int FLAG_HAS_SENT = 1;   // the row's node holds >= 1 sentence
+constexpr int FLAG_INT_COPY = 2;   // the row duplicates an internal node that holds sentences
+
+// Arguments of the scan (score) kernel that are not hot pointers.
+struct ScanArgs {
+  int DP;              // padded dimension (multiple of kDChunk)
+  int nq;              // valid queries in this call
+  int64_t ld;          // leading dimension of the dim-major row arrays
+  int nrows;           // valid rows in the segment
+  int nrows_pad;       // rows rounded up to 64
+  int rows_per_slab;   // rows per workgroup (multiple of 64)
+  int n_qblocks;       // query blocks of (4 * TQ) queries
+  int seg_base;        // global leaf-row id of segment row 0
+  const RowMeta* meta; // [nrows]
+  const int* par;      // [nrows] internal-node id of the parent (-1: none)
+  const int* flags;    // [nrows]
+  const float* P;      // [nq_pad][ldP] prefix sums (fast) or bottleneck lp (categorize)
+  int64_t ldP;
+  float dconst;        // 0 for lp', D*log(2*pi) for the full log-likelihood
+  float* out;          // RAW / KEY output [nq][ldo]
+  int64_t ldo;
+  int out_base;        // column offset of segment row 0 in `out`
+  float* pkey;         // TOPK partial lists [nq_pad][nslab_total][K]
+  float* paux;
+  int* prow;
+  int nslab_total;
+  int slab_off;
+  int K;
+};
+
+// Heap entry of the categorize simulation.
+struct HeapEnt {
+  float score;   // lp(node) (full, with 2*pi) -- CobwebTorchTree.py:243,285
+  float pscore;  // parent's lp (0 for the root)
+  int tb;        // BFS index (deterministic stand-in for random())
+  int node;      // >= 0: internal id; < 0: -(leaf row + 1)
+};
+
+struct SimArgs {
+  int nq, k, R;
+  int64_t max_nodes;
+  int NI, NL;
+  const float* LPF;  // [nq_pad][NI] full lp of internal nodes
+  const float* BF;   // [nq_pad][NI] bottleneck (path-min) lp of internal nodes
+  int64_t ldI;
+  // LIST mode: top-R leaf rows by bottleneck key; DENSE mode (R == 0): all rows
+  const float* lkey; const float* laux; const int* lrow;   // [nq][R]
+  const float* dense_lpf;                                   // [nq][NL] (DENSE)
+  int64_t ldL;
+  int complete;      // the LIST covers every leaf row
+  const int* int_child_begin; const int* int_child_end;     // internal children ranges [NI]
+  const int* int_nchild;     // all children (for the log_prob call count)
+  const int* int_bfs; const int* int_has_sent;
+  const int* int_leaf_a0; const int* int_leaf_a1;           // leaf-row child ranges (iso segment)
+  const int* int_leaf_b0; const int* int_leaf_b1;           // (aniso segment)
+  const int* row_par; const int* row_bfs; const int* row_flags;
+  HeapEnt* heap; int64_t heap_cap;
+  int64_t* out_nodes; int* n_found; int64_t* n_calls; int* status;
+};
+
+// ---- launchers (cwq_kernels.hip) ----
+hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s);
+hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s);
+// mode 0: dst = mean, 1: dst = 1/sqrt(var), 2: dst = mean/sqrt(var)
+hipError_t launch_gather_T(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n, int mode,
+                           float* dst, int64_t ld, int DP, hipStream_t s);
+hipError_t launch_logdet(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
+hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
+
+// The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
+hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
+                       const ScanArgs& a, int nslab, hipStream_t s);
+int scan_tq(int kl);   // queries per wave for a list width
+
+hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
+                               const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
+                               float* LPF, hipStream_t s);
+hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
+                        float* okey, float* oaux, int* orow, hipStream_t s);
+hipError_t launch_expand(const float* okey, const int* orow, int nq, int K, int k, const int64_t* sent_ptr,
+                         const int64_t* sent_ids, int64_t* ids, float* scores, hipStream_t s);
+hipError_t launch_sort_rows(float* keys, int* rows, int nq, int n, int n_pow2, hipStream_t s);
+hipError_t launch_init_rows(const float* src, int64_t lds, int nq, int n, int n_pow2, float* keys, int* rows,
+                            hipStream_t s);
+hipError_t launch_gather_sentences(const float* rowkey, int64_t ldr, int nq, const int* row_of_sent, int64_t n_sent,
+                                   float* out, hipStream_t s);
+hipError_t launch_node_lp(const float* S_int, int64_t ldI, const float* S_leaf, int64_t ldL, int nq,
+                          const int* node_src, const float* logdet_int, const float* logdet_row, float dconst,
+                          int64_t n_nodes, float* out, hipStream_t s);
+hipError_t launch_simulate(const SimArgs& a, hipStream_t s);
+hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, const int64_t* gptr, int64_t n_groups,
+                                 float* count, float* mean, float* meanSq, hipStream_t s);
+
+}  // namespace cwq

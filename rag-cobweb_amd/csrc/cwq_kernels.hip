@@ -1,0 +1,808 @@
+// libcwq kernels for gfx950 (MI355X, CDNA4).
+//
+// The hot kernel is `scan_kernel`: it evaluates the Gaussian log-likelihood of
+// every leaf-class node for a block of queries and folds it straight into the
+// path score and a per-query top-k, so the Q x Nn score matrix is never
+// materialised (SURVEY.md §7 "Hard parts" 3).  Reference op sequence it fuses:
+// CobwebWrapper.py:230-257 (diff_sq, log-var sum, sparse path mm, topk) and,
+// for categorize, CobwebTorchNode.log_prob (CobwebTorchNode.py:100-104).
+//
+// Mapping to CDNA4:
+//   * a lane owns one node row; its 16-dim slice of the node statistics sits
+//     in VGPRs (dim-major layout -> each load is a coalesced 256-B wave load);
+//   * the queries of a wave are wave-uniform, so their 16-dim slices come in
+//     through the scalar cache (s_load) and feed v_sub/v_fma as SGPR operands:
+//     2 VALU ops per (query, node, dim), no LDS traffic at all;
+//   * the 4 waves of a workgroup share the node rows (L1 reuse) and own
+//     disjoint query sets; the per-(wave, query) top-k list lives in VGPRs
+//     (16 lanes per query, shifted with DPP row_shr) -- no LDS, no atomics.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+#include <stdint.h>
+
+#include "cwq_internal.h"
+
+namespace cwq {
+
+#define CWQ_INF __builtin_inff()
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float rl_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// Shift a per-lane list entry one slot up (slot i receives slot i-1) inside a
+// group of KL lanes.  KL = 16: DPP row_shr:1 (rows of 16 lanes); KL = 64: bpermute.
+template <int KL>
+__device__ __forceinline__ int shift_up(int v);
+template <>
+__device__ __forceinline__ int shift_up<16>(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x111, 0xF, 0xF, false);
+}
+template <>
+__device__ __forceinline__ int shift_up<64>(int v) {
+  return __shfl_up(v, 1, 64);
+}
+
+// Insert candidate (ck, ca, cr) into the sorted list held by lane group g.
+// Order: key descending, then row ascending.  The first K slots are the top-K.
+template <int KL>
+__device__ __forceinline__ void list_insert(float& lk, float& la, int& lr, int g, int lane, float ck, float ca,
+                                            int cr, int K) {
+  const bool ing = (KL == 64) || ((lane >> 4) == g);
+  const int slot = lane & (KL - 1);
+  const bool prec = ing && (lk > ck || (lk == ck && lr < cr));
+  const int pos = __popcll(__ballot(prec));
+  if (pos < K) {
+    const float sk = __int_as_float(shift_up<KL>(__float_as_int(lk)));
+    const float sa = __int_as_float(shift_up<KL>(__float_as_int(la)));
+    const int sr = shift_up<KL>(lr);
+    if (ing) {
+      if (slot == pos) {
+        lk = ck;
+        la = ca;
+        lr = cr;
+      } else if (slot > pos) {
+        lk = sk;
+        la = sa;
+        lr = sr;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The scan kernel.
+//   ISO : rows are isotropic (v_d == v for all d): A = mean (dim-major),
+//         S = (1/v) * sum_d (x_d - mu_d)^2
+//   !ISO: A = 1/sigma, B = mu/sigma (dim-major), S = sum_d (x_d*A_d - B_d)^2
+//   lp = -0.5*(logdet + dconst + S)
+//   fast key  = P[parent]/L + fp32(w/L) * lp      (path-weighted mean, A6)
+//   cat key   = min(BF[parent], lp)               (bottleneck of the path, A4)
+// Grid: blockIdx = slab * n_qblocks + qblock (queries fastest: the workgroups
+// that run together stream the same rows, so a slab is read from HBM once).
+// ---------------------------------------------------------------------------
+template <bool ISO, int EPI, int TQ, int KL, bool CAT>
+__global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X, const float* __restrict__ A,
+                                                   const float* __restrict__ B, const ScanArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int qb = blockIdx.x % a.n_qblocks;
+  const int slab = blockIdx.x / a.n_qblocks;
+  const int q0 = (qb * kWavesPerWG + wave) * TQ;
+  const int r_begin = slab * a.rows_per_slab;
+  const int r_end = min(r_begin + a.rows_per_slab, a.nrows_pad);
+  const float* __restrict__ xw = X + (size_t)q0 * a.DP;
+
+  constexpr int QPR = 64 / KL;                                   // queries per list register
+  constexpr int NLR = (EPI == EPI_TOPK) ? (TQ + QPR - 1) / QPR : 1;
+  float lk[NLR], la[NLR];
+  int lr[NLR];
+#pragma unroll
+  for (int r = 0; r < NLR; ++r) {
+    lk[r] = -CWQ_INF;
+    la[r] = 0.f;
+    lr[r] = 0x7fffffff;
+  }
+
+  const int DP16 = a.DP / kDChunk;
+  const f32x16* __restrict__ xv = reinterpret_cast<const f32x16*>(xw);   // wave-uniform -> s_load_dwordx16
+  for (int rt = r_begin; rt < r_end; rt += kWave) {
+    const int row = rt + lane;
+    float acc[TQ];
+#pragma unroll
+    for (int i = 0; i < TQ; ++i) acc[i] = 0.f;
+    const float* __restrict__ pa = A + row;
+    const float* __restrict__ pb = B + row;
+    // node slice for chunk 0; the next chunk's slice is prefetched while computing
+    float m[kDChunk], s[kDChunk];
+#pragma unroll
+    for (int j = 0; j < kDChunk; ++j) m[j] = pa[(size_t)j * a.ld];
+    if constexpr (!ISO) {
+#pragma unroll
+      for (int j = 0; j < kDChunk; ++j) s[j] = pb[(size_t)j * a.ld];
+    }
+    for (int c = 0; c < DP16; ++c) {
+      float mn[kDChunk], sn[kDChunk];
+      const int cn = (c + 1 < DP16) ? c + 1 : c;
+#pragma unroll
+      for (int j = 0; j < kDChunk; ++j) mn[j] = pa[(size_t)(cn * kDChunk + j) * a.ld];
+      if constexpr (!ISO) {
+#pragma unroll
+        for (int j = 0; j < kDChunk; ++j) sn[j] = pb[(size_t)(cn * kDChunk + j) * a.ld];
+      }
+      // query slices: scalar loads, double-buffered across queries
+      f32x16 xa = xv[c];
+#pragma unroll
+      for (int qi = 0; qi < TQ; ++qi) {
+        const f32x16 xn = xv[(size_t)(qi + 1 < TQ ? qi + 1 : qi) * DP16 + c];
+        float part;
+#pragma unroll
+        for (int j = 0; j < kDChunk; ++j) {
+          float t;
+          if constexpr (ISO)
+            t = xa[j] - m[j];
+          else
+            t = fmaf(xa[j], m[j], -s[j]);
+          part = (j == 0) ? t * t : fmaf(t, t, part);
+        }
+        acc[qi] += part;   // two-level sum: per-16 partials keep the fp32 error ~1e-7
+        xa = xn;
+      }
+#pragma unroll
+      for (int j = 0; j < kDChunk; ++j) {
+        m[j] = mn[j];
+        if constexpr (!ISO) s[j] = sn[j];
+      }
+    }
+
+    // ---- epilogue ----
+    const bool vrow = row < a.nrows;
+    RowMeta md{0.f, 0.f, 0.f, 0.f};
+    int p = -1, fl = 0;
+    if (vrow) {
+      md = a.meta[row];
+      p = a.par[row];
+      fl = a.flags[row];
+    }
+    const bool usable = vrow && (CAT ? !(fl & FLAG_INT_COPY) : (fl & FLAG_HAS_SENT) != 0);
+    const int rid = a.seg_base + row;
+#pragma unroll
+    for (int qi = 0; qi < TQ; ++qi) {
+      const int q = q0 + qi;
+      const float S = ISO ? md.iv * acc[qi] : acc[qi];
+      if constexpr (EPI == EPI_RAW) {
+        if (vrow && q < a.nq) a.out[(size_t)q * a.ldo + a.out_base + row] = S;
+      } else {
+        const float lp = -0.5f * (md.logdet + a.dconst + S);
+        float key;
+        if constexpr (CAT) {
+          const float bp = p >= 0 ? a.P[(size_t)q * a.ldP + p] : CWQ_INF;
+          key = fminf(bp, lp);
+        } else {
+          const float pp = p >= 0 ? a.P[(size_t)q * a.ldP + p] : 0.f;
+          key = fmaf(pp, md.invL, md.cw * lp);
+        }
+        if (!usable) key = -CWQ_INF;
+        if constexpr (EPI == EPI_KEY) {
+          if (vrow && q < a.nq) a.out[(size_t)q * a.ldo + a.out_base + row] = CAT ? (usable ? lp : -CWQ_INF) : key;
+        } else {
+          constexpr int dummy = 0;
+          (void)dummy;
+          const int r = qi / QPR;
+          const int g = qi % QPR;
+          const int tl = g * KL + a.K - 1;
+          const float tk = rl_f(lk[r], tl);
+          const int tr = rl_i(lr[r], tl);
+          const bool c = key != -CWQ_INF && (key > tk || (key == tk && rid < tr));
+          uint64_t mask = __ballot(c);
+          while (mask) {
+            const int j = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            list_insert<KL>(lk[r], la[r], lr[r], g, lane, rl_f(key, j), rl_f(lp, j), rl_i(rid, j), a.K);
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (EPI == EPI_TOPK) {
+    const int slot = lane & (KL - 1);
+#pragma unroll
+    for (int qi = 0; qi < TQ; ++qi) {
+      const int r = qi / QPR;
+      const int g = qi % QPR;
+      const int q = q0 + qi;
+      const bool ing = (KL == 64) || ((lane >> 4) == g);
+      if (q < a.nq && ing && slot < a.K) {
+        const size_t o = ((size_t)q * a.nslab_total + a.slab_off + slab) * a.K + slot;
+        a.pkey[o] = lk[r];
+        a.paux[o] = la[r];
+        a.prow[o] = lr[r];
+      }
+    }
+  }
+}
+
+int scan_tq(int kl) { return kl == 16 ? 32 : 16; }
+
+template <bool ISO, int EPI, bool CAT>
+static hipError_t launch_scan_t(int kl, const float* X, const float* A, const float* B, const ScanArgs& a, int nslab,
+                                hipStream_t s) {
+  dim3 grid((unsigned)(nslab * a.n_qblocks)), block(256);
+  if (kl == 16)
+    hipLaunchKernelGGL((scan_kernel<ISO, EPI, 32, 16, CAT>), grid, block, 0, s, X, A, B, a);
+  else
+    hipLaunchKernelGGL((scan_kernel<ISO, EPI, 16, 64, CAT>), grid, block, 0, s, X, A, B, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
+                       const ScanArgs& a, int nslab, hipStream_t s) {
+#define CWQ_SCAN(I, E, C) \
+  if (iso == I && epi == E && cat == C) return launch_scan_t<I, E, C>(kl, X, A, B, a, nslab, s);
+  CWQ_SCAN(true, EPI_RAW, false)
+  CWQ_SCAN(false, EPI_RAW, false)
+  CWQ_SCAN(true, EPI_KEY, false)
+  CWQ_SCAN(false, EPI_KEY, false)
+  CWQ_SCAN(true, EPI_KEY, true)
+  CWQ_SCAN(false, EPI_KEY, true)
+  CWQ_SCAN(true, EPI_TOPK, false)
+  CWQ_SCAN(false, EPI_TOPK, false)
+  CWQ_SCAN(true, EPI_TOPK, true)
+  CWQ_SCAN(false, EPI_TOPK, true)
+#undef CWQ_SCAN
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------
+// Merge the per-slab partial lists of one query into its global top-K (K <= 64).
+// One wave per query; the list lives in the wave's 64 lanes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ pkey, const float* __restrict__ paux,
+                                                    const int* __restrict__ prow, int nq, int nent, int K,
+                                                    float* okey, float* oaux, int* orow) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  float lk = -CWQ_INF, la = 0.f;
+  int lr = 0x7fffffff;
+  const size_t base = (size_t)q * nent;
+  for (int e0 = 0; e0 < nent; e0 += kWave) {
+    const int e = e0 + lane;
+    float ek = -CWQ_INF, ea = 0.f;
+    int er = 0x7fffffff;
+    if (e < nent) {
+      ek = pkey[base + e];
+      ea = paux[base + e];
+      er = prow[base + e];
+    }
+    const float tk = rl_f(lk, K - 1);
+    const int tr = rl_i(lr, K - 1);
+    const bool c = ek != -CWQ_INF && (ek > tk || (ek == tk && er < tr));
+    uint64_t mask = __ballot(c);
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      list_insert<64>(lk, la, lr, 0, lane, rl_f(ek, j), rl_f(ea, j), rl_i(er, j), K);
+    }
+  }
+  if (lane < K) {
+    okey[(size_t)q * K + lane] = lk;
+    oaux[(size_t)q * K + lane] = la;
+    orow[(size_t)q * K + lane] = lr;
+  }
+}
+
+hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K, float* okey,
+                        float* oaux, int* orow, hipStream_t s) {
+  dim3 grid((unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG)), block(256);
+  hipLaunchKernelGGL(merge_kernel, grid, block, 0, s, pkey, paux, prow, nq, nent, K, okey, oaux, orow);
+  return hipGetLastError();
+}
+
+// Expand the top rows of each query into sentence ids (rows hold >= 1 sentence;
+// ids of one row ascending).  One thread per query.
+__global__ void expand_kernel(const float* __restrict__ okey, const int* __restrict__ orow, int nq, int K, int k,
+                              const int64_t* __restrict__ sent_ptr, const int64_t* __restrict__ sent_ids,
+                              int64_t* ids, float* scores) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  int cnt = 0;
+  for (int i = 0; i < K && cnt < k; ++i) {
+    const float key = okey[(size_t)q * K + i];
+    const int row = orow[(size_t)q * K + i];
+    if (key == -CWQ_INF || row == 0x7fffffff) break;
+    for (int64_t s = sent_ptr[row]; s < sent_ptr[row + 1] && cnt < k; ++s, ++cnt) {
+      ids[(size_t)q * k + cnt] = sent_ids[s];
+      if (scores) scores[(size_t)q * k + cnt] = key;
+    }
+  }
+  for (; cnt < k; ++cnt) {
+    ids[(size_t)q * k + cnt] = -1;
+    if (scores) scores[(size_t)q * k + cnt] = -CWQ_INF;
+  }
+}
+
+hipError_t launch_expand(const float* okey, const int* orow, int nq, int K, int k, const int64_t* sent_ptr,
+                         const int64_t* sent_ids, int64_t* ids, float* scores, hipStream_t s) {
+  hipLaunchKernelGGL(expand_kernel, dim3((nq + 127) / 128), dim3(128), 0, s, okey, orow, nq, K, k, sent_ptr, sent_ids,
+                     ids, scores);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Full per-query sort of materialised row keys (k > 64 / categorize fallback).
+// Order: key descending, row ascending.  Bitonic network on padded power-of-2
+// segments: one workgroup per query in LDS when the segment fits, else global
+// passes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool before(float ka, int ra, float kb, int rb) {
+  return ka > kb || (ka == kb && ra < rb);
+}
+
+__global__ void init_rows_kernel(const float* __restrict__ src, int64_t lds, int n, int n_pow2, float* keys,
+                                 int* rows) {
+  const int q = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_pow2; i += gridDim.x * blockDim.x) {
+    const size_t o = (size_t)q * n_pow2 + i;
+    keys[o] = i < n ? src[(size_t)q * lds + i] : -CWQ_INF;
+    rows[o] = i < n ? i : 0x7fffffff;
+  }
+}
+
+hipError_t launch_init_rows(const float* src, int64_t lds, int nq, int n, int n_pow2, float* keys, int* rows,
+                            hipStream_t s) {
+  dim3 grid((unsigned)std::min((n_pow2 + 255) / 256, 4096), (unsigned)nq);
+  hipLaunchKernelGGL(init_rows_kernel, grid, dim3(256), 0, s, src, lds, n, n_pow2, keys, rows);
+  return hipGetLastError();
+}
+
+constexpr int kSortLDS = 4096;
+
+__global__ __launch_bounds__(1024) void sort_lds_kernel(float* keys, int* rows, int n_pow2) {
+  __shared__ float sk[kSortLDS];
+  __shared__ int sr[kSortLDS];
+  const size_t base = (size_t)blockIdx.x * n_pow2;
+  for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+    sk[i] = keys[base + i];
+    sr[i] = rows[base + i];
+  }
+  __syncthreads();
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n_pow2 / 2; t += blockDim.x) {
+        const int i = 2 * t - (t & (stride - 1));
+        const int j = i + stride;
+        const bool up = (i & size) == 0;   // "up" segments sort in final order
+        const bool sw = up ? before(sk[j], sr[j], sk[i], sr[i]) : before(sk[i], sr[i], sk[j], sr[j]);
+        if (sw) {
+          const float tk = sk[i];
+          sk[i] = sk[j];
+          sk[j] = tk;
+          const int tr = sr[i];
+          sr[i] = sr[j];
+          sr[j] = tr;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+    keys[base + i] = sk[i];
+    rows[base + i] = sr[i];
+  }
+}
+
+__global__ void sort_pass_kernel(float* keys, int* rows, int n_pow2, int size, int stride) {
+  const int q = blockIdx.y;
+  const size_t base = (size_t)q * n_pow2;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_pow2 / 2; t += gridDim.x * blockDim.x) {
+    const int i = 2 * t - (t & (stride - 1));
+    const int j = i + stride;
+    const bool up = (i & size) == 0;
+    const float ki = keys[base + i], kj = keys[base + j];
+    const int ri = rows[base + i], rj = rows[base + j];
+    const bool sw = up ? before(kj, rj, ki, ri) : before(ki, ri, kj, rj);
+    if (sw) {
+      keys[base + i] = kj;
+      keys[base + j] = ki;
+      rows[base + i] = rj;
+      rows[base + j] = ri;
+    }
+  }
+}
+
+hipError_t launch_sort_rows(float* keys, int* rows, int nq, int n, int n_pow2, hipStream_t s) {
+  (void)n;
+  if (n_pow2 <= kSortLDS) {
+    hipLaunchKernelGGL(sort_lds_kernel, dim3((unsigned)nq), dim3(1024), 0, s, keys, rows, n_pow2);
+    return hipGetLastError();
+  }
+  dim3 grid((unsigned)std::min(n_pow2 / 2 / 256 + 1, 4096), (unsigned)nq);
+  for (int size = 2; size <= n_pow2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      hipLaunchKernelGGL(sort_pass_kernel, grid, dim3(256), 0, s, keys, rows, n_pow2, size, stride);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+// rank_scores: sentence s takes the key of its row.
+__global__ void gather_sent_kernel(const float* __restrict__ rowkey, int64_t ldr, const int* __restrict__ row_of_sent,
+                                   int64_t n_sent, float* out) {
+  const int q = blockIdx.y;
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n_sent; s += (int64_t)gridDim.x * blockDim.x) {
+    const int r = row_of_sent[s];
+    out[(size_t)q * n_sent + s] = r >= 0 ? rowkey[(size_t)q * ldr + r] : -CWQ_INF;
+  }
+}
+
+hipError_t launch_gather_sentences(const float* rowkey, int64_t ldr, int nq, const int* row_of_sent, int64_t n_sent,
+                                   float* out, hipStream_t s) {
+  dim3 grid((unsigned)std::min<int64_t>((n_sent + 255) / 256, 4096), (unsigned)nq);
+  hipLaunchKernelGGL(gather_sent_kernel, grid, dim3(256), 0, s, rowkey, ldr, row_of_sent, n_sent, out);
+  return hipGetLastError();
+}
+
+// Per-node log-likelihood in BFS order from the raw sums of both segments.
+__global__ void node_lp_kernel(const float* __restrict__ S_int, int64_t ldI, const float* __restrict__ S_leaf,
+                               int64_t ldL, const int* __restrict__ node_src, const float* __restrict__ logdet_int,
+                               const float* __restrict__ logdet_row, float dconst, int64_t n_nodes, float* out) {
+  const int q = blockIdx.y;
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < n_nodes;
+       n += (int64_t)gridDim.x * blockDim.x) {
+    const int src = node_src[n];
+    float S, ld;
+    if (src >= 0) {
+      S = S_int[(size_t)q * ldI + src];
+      ld = logdet_int[src];
+    } else {
+      const int r = -src - 1;
+      S = S_leaf[(size_t)q * ldL + r];
+      ld = logdet_row[r];
+    }
+    out[(size_t)q * n_nodes + n] = -0.5f * (ld + dconst + S);
+  }
+}
+
+hipError_t launch_node_lp(const float* S_int, int64_t ldI, const float* S_leaf, int64_t ldL, int nq,
+                          const int* node_src, const float* logdet_int, const float* logdet_row, float dconst,
+                          int64_t n_nodes, float* out, hipStream_t s) {
+  dim3 grid((unsigned)std::min<int64_t>((n_nodes + 255) / 256, 4096), (unsigned)nq);
+  hipLaunchKernelGGL(node_lp_kernel, grid, dim3(256), 0, s, S_int, ldI, S_leaf, ldL, node_src, logdet_int, logdet_row,
+                     dconst, n_nodes, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Internal nodes: turn raw sums into lp' / full lp and propagate down one level.
+//   P[i]  = P[parent] + w[depth_i] * lp'(i)          (prefix of the path sum)
+//   BF[i] = min(BF[parent], lp_full(i))              (path bottleneck, A4)
+// BFS order puts each level in a contiguous range; one launch per level.
+// ---------------------------------------------------------------------------
+__global__ void prefix_level_kernel(const float* __restrict__ S, int64_t ldS, int nq, int i0, int i1,
+                                    const int* __restrict__ par_int, const float* __restrict__ w_int,
+                                    const float* __restrict__ logdet_int, float dfull, float* P, float* BF,
+                                    float* LPF) {
+  const int n = i1 - i0;
+  const int64_t total = (int64_t)n * nq;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / n);
+    const int i = i0 + (int)(t % n);
+    const size_t o = (size_t)q * ldS + i;
+    const float s = S[o];
+    const float ld = logdet_int[i];
+    const float lp = -0.5f * (ld + s);
+    const float lpf = -0.5f * (ld + dfull + s);
+    const int p = par_int[i];
+    if (p >= 0) {
+      const size_t op = (size_t)q * ldS + p;
+      P[o] = fmaf(w_int[i], lp, P[op]);
+      BF[o] = fminf(BF[op], lpf);
+    } else {
+      P[o] = w_int[i] * lp;
+      BF[o] = lpf;
+    }
+    LPF[o] = lpf;
+  }
+}
+
+hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
+                               const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
+                               float* LPF, hipStream_t s) {
+  const int64_t total = (int64_t)(i1 - i0) * nq;
+  if (total <= 0) return hipSuccess;
+  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(prefix_level_kernel, grid, dim3(256), 0, s, S, ldS, nq, i0, i1, par_int, w_int, logdet_int,
+                     dfull, P, BF, LPF);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Best-first categorize on precomputed scores (CobwebTorchTree.py:235-289).
+// One thread per query; binary heap in global scratch.  Pops come out in
+// non-increasing path-bottleneck order, so with the top-R leaf rows by
+// bottleneck (LIST mode) the simulation is exact while every popped node's
+// bottleneck stays above the R-th key; otherwise status = 1 and the host
+// re-runs the query with every row materialised (DENSE mode).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool heap_before(const HeapEnt& a, const HeapEnt& b) {
+  if (a.score != b.score) return a.score > b.score;
+  if (a.pscore != b.pscore) return a.pscore < b.pscore;
+  return a.tb < b.tb;
+}
+
+__device__ void heap_push(HeapEnt* h, int64_t& n, const HeapEnt& e) {
+  int64_t i = n++;
+  while (i > 0) {
+    const int64_t p = (i - 1) >> 1;
+    if (!heap_before(e, h[p])) break;
+    h[i] = h[p];
+    i = p;
+  }
+  h[i] = e;
+}
+
+__device__ HeapEnt heap_pop(HeapEnt* h, int64_t& n) {
+  const HeapEnt top = h[0];
+  const HeapEnt last = h[--n];
+  int64_t i = 0;
+  for (;;) {
+    int64_t c = 2 * i + 1;
+    if (c >= n) break;
+    if (c + 1 < n && heap_before(h[c + 1], h[c])) ++c;
+    if (!heap_before(h[c], last)) break;
+    h[i] = h[c];
+    i = c;
+  }
+  if (n > 0) h[i] = last;
+  return top;
+}
+
+__global__ void simulate_kernel(const SimArgs a) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nq) return;
+  HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
+  int64_t hn = 0;
+  const bool dense = a.R == 0;
+  const float* lk = a.lkey + (size_t)q * a.R;
+  const float* lx = a.laux + (size_t)q * a.R;
+  const int* lw = a.lrow + (size_t)q * a.R;
+  const float tau = (dense || a.complete) ? -CWQ_INF : lk[a.R - 1];
+  const bool exact_all = dense || a.complete || tau == -CWQ_INF;
+  int status = 0, found = 0;
+  int64_t calls = 1, visited = 0;
+
+  if (a.NI > 0) {
+    heap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0});
+  } else {   // single-node tree: the root is leaf row 0
+    float lp = -CWQ_INF;
+    if (dense)
+      lp = a.dense_lpf[(size_t)q * a.ldL];
+    else
+      for (int i = 0; i < a.R; ++i)
+        if (lw[i] == 0) lp = lx[i];
+    heap_push(h, hn, HeapEnt{lp, 0.f, a.row_bfs[0], -1});
+  }
+
+  while (hn > 0) {
+    const HeapEnt e = heap_pop(h, hn);
+    ++visited;
+    const bool is_int = e.node >= 0;
+    const int row = is_int ? -1 : -e.node - 1;
+    if (!exact_all) {
+      float b;
+      if (is_int) {
+        b = a.BF[(size_t)q * a.ldI + e.node];
+      } else {
+        const int p = a.row_par[row];
+        b = p >= 0 ? fminf(a.BF[(size_t)q * a.ldI + p], e.score) : e.score;
+      }
+      if (!(b > tau)) {
+        status = 1;
+        break;
+      }
+    }
+    if (visited >= a.max_nodes) break;
+    const bool has_sent = is_int ? a.int_has_sent[e.node] != 0 : (a.row_flags[row] & FLAG_HAS_SENT) != 0;
+    if (has_sent) {
+      if (found < a.k) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+      ++found;
+    }
+    if (found == a.k) break;
+    if (is_int) {
+      const int u = e.node;
+      calls += a.int_nchild[u];
+      for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
+        heap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c});
+      if (dense) {
+        for (int pass = 0; pass < 2; ++pass) {
+          const int r0 = pass ? a.int_leaf_b0[u] : a.int_leaf_a0[u];
+          const int r1 = pass ? a.int_leaf_b1[u] : a.int_leaf_a1[u];
+          for (int r = r0; r < r1; ++r)
+            if (!(a.row_flags[r] & FLAG_INT_COPY))
+              heap_push(h, hn, HeapEnt{a.dense_lpf[(size_t)q * a.ldL + r], e.score, a.row_bfs[r], -(r + 1)});
+        }
+      } else {
+        for (int i = 0; i < a.R; ++i) {
+          const int r = lw[i];
+          if (lk[i] == -CWQ_INF || r == 0x7fffffff) break;
+          if (a.row_par[r] == u) heap_push(h, hn, HeapEnt{lx[i], e.score, a.row_bfs[r], -(r + 1)});
+        }
+      }
+    }
+  }
+  a.n_found[q] = found < a.k ? found : a.k;
+  if (a.n_calls) a.n_calls[q] = calls;
+  a.status[q] = status;
+}
+
+hipError_t launch_simulate(const SimArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(simulate_kernel, dim3((a.nq + 63) / 64), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Index build kernels
+// ---------------------------------------------------------------------------
+__global__ void pad_queries_kernel(const float* __restrict__ q, int64_t nq, int D, float* X, int64_t nq_pad, int DP) {
+  const int64_t total = nq_pad * DP;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / DP;
+    const int d = (int)(t % DP);
+    X[t] = (r < nq && d < D) ? q[r * D + d] : 0.f;
+  }
+}
+
+hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s) {
+  const int64_t total = nq_pad * DP;
+  hipLaunchKernelGGL(pad_queries_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)), dim3(256), 0, s, q, nq,
+                     D, X, nq_pad, DP);
+  return hipGetLastError();
+}
+
+// flags[r] = 1 when var[node[r], :] is one value repeated (bitwise).
+__global__ void iso_flags_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
+                                 int* flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const float* v = var + nodes[r] * (int64_t)D;
+  const float v0 = v[0];
+  bool same = true;
+  for (int d = lane; d < D; d += kWave) same &= (__float_as_uint(v[d]) == __float_as_uint(v0));
+  const bool all = __all(same);
+  if (lane == 0) flags[r] = all ? 1 : 0;
+}
+
+hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(iso_flags_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, var, D, nodes, n, flags);
+  return hipGetLastError();
+}
+
+// dst[d * ld + r] = f(mean[node[r], d], var[node[r], d]); zero padding for
+// d >= D or r >= n.  64x64 tile transpose through LDS (both sides coalesced).
+__global__ __launch_bounds__(256) void gather_T_kernel(const float* __restrict__ mean, const float* __restrict__ var,
+                                                       int D, const int64_t* __restrict__ nodes, int64_t n, int mode,
+                                                       float* dst, int64_t ld, int DP) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64;
+  const int d0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int rr = ty; rr < 64; rr += 4) {
+    const int64_t r = r0 + rr;
+    const int d = d0 + tx;
+    float v = 0.f;
+    if (r < n && d < D) {
+      const int64_t o = nodes[r] * (int64_t)D + d;
+      if (mode == 0) {
+        v = mean[o];
+      } else {
+        const float is = 1.0f / sqrtf(var[o]);
+        v = mode == 1 ? is : mean[o] * is;
+      }
+    }
+    tile[rr][tx] = v;
+  }
+  __syncthreads();
+  for (int dd = ty; dd < 64; dd += 4) {
+    const int d = d0 + dd;
+    const int64_t r = r0 + tx;
+    if (d < DP && r < ld) dst[(int64_t)d * ld + r] = tile[tx][dd];
+  }
+}
+
+hipError_t launch_gather_T(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n, int mode,
+                           float* dst, int64_t ld, int DP, hipStream_t s) {
+  if (ld <= 0) return hipSuccess;
+  dim3 grid((unsigned)((DP + 63) / 64), (unsigned)((ld + 63) / 64));
+  hipLaunchKernelGGL(gather_T_kernel, grid, dim3(256), 0, s, mean, var, D, nodes, n, mode, dst, ld, DP);
+  return hipGetLastError();
+}
+
+// logdet[r] = sum_d log(var[node[r], d]); fp32 logs (as torch.log), fp64 sum.
+__global__ void logdet_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
+                              float* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const float* v = var + nodes[r] * (int64_t)D;
+  double s = 0.0;
+  for (int d = lane; d < D; d += kWave) s += (double)logf(v[d]);
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[r] = (float)s;
+}
+
+hipError_t launch_logdet(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(logdet_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, var, D, nodes, n, out);
+  return hipGetLastError();
+}
+
+__global__ void inv_var0_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
+                                float* out) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    out[r] = 1.0f / var[nodes[r] * (int64_t)D];
+}
+
+hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(inv_var0_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, var, D,
+                     nodes, n, out);
+  return hipGetLastError();
+}
+
+// Sequential Welford per (group, dim) in the reference's fp32 op order
+// (CobwebTorchNode.py:57-68).  Contraction into FMA is disabled so every step
+// rounds exactly like torch's separate elementwise ops.
+__global__ void welford_groups_kernel(const float* __restrict__ X, int D, const int64_t* __restrict__ order,
+                                      const int64_t* __restrict__ gptr, int64_t n_groups, float* count, float* mean,
+                                      float* meanSq) {
+#pragma clang fp contract(off)
+  const int64_t g = blockIdx.y;
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups || d >= D) return;
+  float c = 0.f, m = 0.f, m2 = 0.f;
+  const int64_t i0 = gptr[g], i1 = gptr[g + 1];
+  constexpr int B = 16;   // loads batched ahead of the serial recurrence
+  int64_t i = i0;
+  for (; i + B <= i1; i += B) {
+    float xb[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) xb[u] = X[order[i + u] * (int64_t)D + d];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      c = c + 1.0f;
+      const float delta = xb[u] - m;
+      m = m + delta / c;
+      m2 = m2 + delta * (xb[u] - m);
+    }
+  }
+  for (; i < i1; ++i) {
+    const float x = X[order[i] * (int64_t)D + d];
+    c = c + 1.0f;
+    const float delta = x - m;
+    m = m + delta / c;
+    m2 = m2 + delta * (x - m);
+  }
+  mean[g * D + d] = m;
+  meanSq[g * D + d] = m2;
+  if (d == 0) count[g] = c;
+}
+
+hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, const int64_t* gptr, int64_t n_groups,
+                                 float* count, float* mean, float* meanSq, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  dim3 grid((unsigned)((D + 63) / 64), (unsigned)n_groups);
+  hipLaunchKernelGGL(welford_groups_kernel, grid, dim3(64), 0, s, X, D, order, gptr, n_groups, count, mean, meanSq);
+  return hipGetLastError();
+}
+
+}  // namespace cwq

@@ -1,0 +1,165 @@
+"""Device-resident Cobweb query index: a thin Python handle over libcwq.
+
+`CobwebIndex` owns one `cwq_index*` (include/cobweb_query.h).  It is the MI355X
+replacement of the flattened prediction index the reference caches in
+CobwebWrapper.build_prediction_index (CobwebWrapper.py:91-208) and of the query
+op sequences that read it (:210-294, CobwebTorchTree.py:235-310).
+
+Inputs/outputs are torch tensors on the index device; torch only supplies device
+memory and the current HIP stream -- every computation runs in libcwq.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+
+DEFAULT_LEVEL_WEIGHTS = (1.0, 1.0, 1.0, 1.0, 1.0, 1.0)   # CobwebWrapper.py:155
+
+
+def _dev(device):
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError(f"CobwebIndex lives on a GPU, got device {device}")
+    return device if device.index is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class CobwebIndex:
+    """Immutable flattened tree on one GPU.
+
+    mean, var          [Nn, D] float32 (torch on any device, or numpy), BFS order
+    parent             [Nn] int64, parent[0] = -1, non-decreasing (BFS)
+    node_of_sentence   [n_sent] int64, node holding each sentence id (-1: none)
+    level_weights      per-depth weights (CobwebWrapper.py:153-168)
+    """
+
+    def __init__(self, mean, var, parent, node_of_sentence, level_weights=None, device=None):
+        self.device = _dev(device)
+        L = lib()
+        mean = torch.as_tensor(mean, dtype=torch.float32).to(self.device).contiguous()
+        var = torch.as_tensor(var, dtype=torch.float32).to(self.device).contiguous()
+        if mean.shape != var.shape or mean.dim() != 2:
+            raise ValueError("mean and var must both be [n_nodes, dim]")
+        parent = np.ascontiguousarray(np.asarray(parent, dtype=np.int64))
+        nos = np.ascontiguousarray(np.asarray(node_of_sentence, dtype=np.int64))
+        w = np.ascontiguousarray(np.asarray(
+            DEFAULT_LEVEL_WEIGHTS if level_weights is None else level_weights, dtype=np.float64))
+        self.n_nodes, self.dim = mean.shape
+        self.n_sent = int(nos.size)
+        self.level_weights = [float(x) for x in w]
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(L.cwq_index_create(self.device.index, self.n_nodes, self.dim, _ptr(mean), _ptr(var),
+                                     parent.ctypes.data_as(ctypes.c_void_p), nos.ctypes.data_as(ctypes.c_void_p),
+                                     self.n_sent, w.ctypes.data_as(ctypes.c_void_p), w.size,
+                                     _stream(self.device), ctypes.byref(h)))
+        self._h = h
+        self.info = self._info()
+
+    def _info(self):
+        out = np.zeros(8, np.int64)
+        check(lib().cwq_index_info(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        keys = ["n_nodes", "dim", "n_sent", "internal_nodes", "leaf_rows", "isotropic_rows", "max_depth",
+                "device_bytes"]
+        return dict(zip(keys, (int(v) for v in out)))
+
+    def set_timing(self, enable=True):
+        check(lib().cwq_set_timing(self._h, int(bool(enable))))
+
+    def last_timing(self):
+        """Phase times (ms) of the last score_topk call, from HIP events on its stream."""
+        out = np.zeros(5, np.float32)
+        check(lib().cwq_last_timing(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"leaf_scan_ms": float(out[0]), "internal_ms": float(out[1]), "merge_ms": float(out[2]),
+                "call_ms": float(out[3]), "leaf_scan_launches": int(out[4])}
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().cwq_index_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- queries ----
+    def _queries(self, q):
+        q = torch.as_tensor(q, dtype=torch.float32)
+        if q.dim() == 1:
+            q = q[None, :]
+        if q.dim() != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be [nq, {self.dim}]")
+        return q.to(self.device).contiguous()
+
+    def score_topk(self, q, k):
+        """Top-k sentence ids/scores per query ("Cobweb Fast", A6)."""
+        q = self._queries(q)
+        nq = q.shape[0]
+        ids = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+        scores = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib().cwq_score_topk(self._h, _ptr(q), nq, int(k), _ptr(ids), _ptr(scores),
+                                       _stream(self.device)))
+        return ids, scores
+
+    def rank_scores(self, q):
+        """All sentence scores (A8), [nq, n_sent]."""
+        q = self._queries(q)
+        out = torch.empty((q.shape[0], self.n_sent), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib().cwq_rank_scores(self._h, _ptr(q), q.shape[0], _ptr(out), _stream(self.device)))
+        return out
+
+    def node_logprob(self, q, full=False):
+        """Per-node log-likelihood in BFS order: lp' (full=False) or log_prob (full=True)."""
+        q = self._queries(q)
+        out = torch.empty((q.shape[0], self.n_nodes), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib().cwq_node_logprob(self._h, _ptr(q), q.shape[0], int(bool(full)), _ptr(out),
+                                         _stream(self.device)))
+        return out
+
+    def categorize(self, q, k, max_nodes=100000):
+        """Best-first categorize ("Cobweb Basic", A4): retrieved BFS node ids in pop
+        order [nq, k], number found [nq], log_prob call count [nq]."""
+        q = self._queries(q)
+        nq = q.shape[0]
+        nodes = torch.full((nq, k), -1, dtype=torch.int64, device=self.device)
+        found = torch.empty(nq, dtype=torch.int32, device=self.device)
+        calls = torch.empty(nq, dtype=torch.int64, device=self.device)
+        mx = int(min(max_nodes, 2 ** 62)) if max_nodes != float("inf") else 2 ** 62
+        with torch.cuda.device(self.device):
+            check(lib().cwq_categorize(self._h, _ptr(q), nq, int(k), mx, _ptr(nodes), _ptr(found), _ptr(calls),
+                                       _stream(self.device)))
+        return nodes, found, calls
+
+
+def welford_groups(X, order, group_ptr):
+    """Sequential-Welford stats per row group on the GPU (libcwq cwq_welford_groups).
+    X [n, D] float32 cuda; order, group_ptr int64 cuda.  Returns (count, mean, meanSq)."""
+    n, D = X.shape
+    G = group_ptr.numel() - 1
+    count = torch.empty(G, dtype=torch.float32, device=X.device)
+    mean = torch.empty((G, D), dtype=torch.float32, device=X.device)
+    meanSq = torch.empty((G, D), dtype=torch.float32, device=X.device)
+    for g0 in range(0, G, 65535):
+        g1 = min(G, g0 + 65535)
+        with torch.cuda.device(X.device):
+            check(lib().cwq_welford_groups(_ptr(X), n, D, _ptr(order), ctypes.c_void_p(group_ptr[g0:].data_ptr()),
+                                           g1 - g0, ctypes.c_void_p(count[g0:].data_ptr()),
+                                           ctypes.c_void_p(mean[g0:].data_ptr()),
+                                           ctypes.c_void_p(meanSq[g0:].data_ptr()), _stream(X.device)))
+    return count, mean, meanSq

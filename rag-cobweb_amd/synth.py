@@ -1,0 +1,83 @@
+"""Synthetic trees for the 1M-10M configurations.
+
+The reference cannot build trees at these sizes (ifit is O(N^2 D) on Gaussian
+data), so the benchmark trees are synthesised on the GPU with the statistics the
+reference's own inserts would accumulate:
+
+* flat-synth: root + N singleton leaves -- what the reference ifit builds for
+  isotropic N(0, I) data (root fan-out = N).  Leaf: count 1,
+  mean = x, meanSq = 0 (var == prior_var exactly).  Root: sequential Welford over
+  X in index order (CobwebTorchNode.increment_counts, :57-68) -- computed by the
+  libcwq `cwq_welford_groups` kernel in the same fp32 op order.
+* two-level synth: root -> clusters -> leaves (cluster stats by the same Welford
+  over each cluster's members in index order); exercises paths of length 3.
+
+Outputs are the BFS-ordered arrays `CobwebIndex` takes.
+"""
+import torch
+
+from .index import welford_groups
+from .tree import PRIOR_VAR
+
+
+def synthetic_corpus(n, dim, seed=0, device="cuda"):
+    """X ~ N(0, I) float32, generated on the device with a seeded generator."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return torch.randn((n, dim), generator=g, device=device, dtype=torch.float32)
+
+
+def synthetic_queries(X, nq, seed=1, frac_perturbed=0.5, sigma=0.1):
+    """Half fresh N(0, I), half corpus points + sigma*N(0, I) (targets = their ids)."""
+    g = torch.Generator(device=X.device)
+    g.manual_seed(seed)
+    n_pert = int(nq * frac_perturbed)
+    targets = torch.randint(0, X.shape[0], (n_pert,), generator=g, device=X.device)
+    pert = X[targets] + sigma * torch.randn((n_pert, X.shape[1]), generator=g, device=X.device)
+    fresh = torch.randn((nq - n_pert, X.shape[1]), generator=g, device=X.device)
+    return torch.cat([pert, fresh]).contiguous(), targets
+
+
+def _var_of(count, meanSq):
+    # CobwebTorchTree.compute_var: meanSq / count + prior_var (fp32 division then add)
+    return meanSq / count[:, None] + float(PRIOR_VAR)
+
+
+def flat_synth(X):
+    """root + N leaves.  Returns dict(mean, var, parent, node_of_sentence) with the
+    BFS order [root, leaf 0, ..., leaf N-1]."""
+    N, D = X.shape
+    order = torch.arange(N, device=X.device, dtype=torch.int64)
+    gptr = torch.tensor([0, N], device=X.device, dtype=torch.int64)
+    cnt, mu, m2 = welford_groups(X, order, gptr)
+    mean = torch.cat([mu, X])
+    var = torch.cat([_var_of(cnt, m2), torch.full((N, D), float(PRIOR_VAR), device=X.device)])
+    parent = torch.zeros(N + 1, dtype=torch.int64)
+    parent[0] = -1
+    nos = torch.arange(1, N + 1, dtype=torch.int64)
+    return dict(mean=mean, var=var, parent=parent.numpy(), node_of_sentence=nos.numpy(),
+                root=(cnt, mu, m2))
+
+
+def two_level_synth(X, labels):
+    """root -> one node per non-empty cluster (ascending label) -> its members
+    (ascending index).  BFS: [root, clusters..., leaves of cluster 0, ...]."""
+    N, D = X.shape
+    dev = X.device
+    labels = labels.to(dev)
+    uniq, inv, counts = torch.unique(labels, sorted=True, return_inverse=True, return_counts=True)
+    G = uniq.numel()
+    order = torch.argsort(inv * N + torch.arange(N, device=dev))          # by cluster, then index
+    gptr = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+    gptr[1:] = torch.cumsum(counts, 0)
+    c_cnt, c_mu, c_m2 = welford_groups(X, order, gptr)
+    r_cnt, r_mu, r_m2 = welford_groups(X, torch.arange(N, device=dev), torch.tensor([0, N], device=dev))
+    mean = torch.cat([r_mu, c_mu, X[order]])
+    var = torch.cat([_var_of(r_cnt, r_m2), _var_of(c_cnt, c_m2),
+                     torch.full((N, D), float(PRIOR_VAR), device=dev)])
+    parent = torch.cat([torch.tensor([-1]), torch.zeros(G, dtype=torch.int64),
+                        1 + torch.repeat_interleave(torch.arange(G), counts.cpu())])
+    node_of_sentence = torch.empty(N, dtype=torch.int64)
+    node_of_sentence[order.cpu()] = torch.arange(1 + G, 1 + G + N)
+    return dict(mean=mean, var=var, parent=parent.numpy(), node_of_sentence=node_of_sentence.numpy(),
+                n_clusters=G)

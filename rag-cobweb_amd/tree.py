@@ -1,0 +1,162 @@
+"""Host-side concept tree: node statistics, the reference JSON format and the
+BFS flattening that feeds the device index.
+
+Mirrors the data model of CobwebTorchNode (src/cobweb/CobwebTorchNode.py:31-55)
+and CobwebTorchTree (src/cobweb/CobwebTorchTree.py:23-121): each node keeps
+count, mean and meanSq (Welford M2) in float32, children in list order and the
+sentence ids it holds.  Arrays here are numpy float32; the query path never
+touches them after `flatten()` hands them to libcwq.
+"""
+import json
+import math
+from collections import deque
+
+import numpy as np
+
+F32 = np.float32
+# CobwebTorchTree.py:35-40: prior_var = 1 / (2 * e * pi_tensor), computed in fp32
+PRIOR_VAR = F32(1.0) / (F32(2 * math.e) * F32(math.pi))
+
+
+class Node:
+    __slots__ = ("count", "mean", "meanSq", "children", "parent", "sentence_id")
+
+    def __init__(self, dim):
+        self.count = F32(0.0)
+        self.mean = np.zeros(dim, F32)
+        self.meanSq = np.zeros(dim, F32)
+        self.children = []
+        self.parent = None
+        self.sentence_id = []
+
+    def increment_counts(self, x):
+        """Welford insert, CobwebTorchNode.py:57-68 (fp32, same op order)."""
+        self.count = F32(self.count + F32(1))
+        delta = x - self.mean
+        self.mean = self.mean + delta / self.count
+        self.meanSq = self.meanSq + delta * (x - self.mean)
+
+
+class CobwebTree:
+    """Tree container with the reference's defaults (CobwebTorchTree.py:23-41):
+    use_info=True, acuity_cutoff=False, use_kl=True, prior_var=1/(2*e*pi)."""
+
+    def __init__(self, shape, prior_var=None):
+        self.shape = tuple(int(s) for s in shape)
+        self.dim = self.shape[0]
+        self.use_info, self.acuity_cutoff, self.use_kl, self.alpha = True, False, True, 1e-8
+        self.prior_var = PRIOR_VAR if prior_var is None else F32(prior_var)
+        self.root = Node(self.dim)
+
+    def compute_var(self, meanSq, count):
+        """CobwebTorchTree.py:336-342 with acuity_cutoff=False."""
+        return meanSq / count + self.prior_var
+
+    # ---- reference JSON (CobwebTorchTree.dump_json / load_json, :67-121) ----
+    def dump_json(self):
+        head = {"use_info": self.use_info, "acuity_cutoff": self.acuity_cutoff, "use_kl": self.use_kl,
+                "shape": list(self.shape), "alpha": self.alpha, "prior_var": float(self.prior_var)}
+
+        def node_dict(n):
+            return {"count": float(n.count), "mean": n.mean.tolist(), "meanSq": n.meanSq.tolist(),
+                    "sentence_id": list(n.sentence_id), "children": [node_dict(c) for c in n.children]}
+
+        # iterative to survive deep trees
+        out = dict(head)
+        out["root"] = node_dict(self.root) if self._depth() < 500 else self._iter_dict()
+        return json.dumps(out)
+
+    def _depth(self):
+        d, q = 0, deque([(self.root, 0)])
+        while q:
+            n, k = q.popleft()
+            d = max(d, k)
+            q.extend((c, k + 1) for c in n.children)
+        return d
+
+    def _iter_dict(self):
+        def shell(n):
+            return {"count": float(n.count), "mean": n.mean.tolist(), "meanSq": n.meanSq.tolist(),
+                    "sentence_id": list(n.sentence_id), "children": []}
+        root = shell(self.root)
+        stack = [(self.root, root)]
+        while stack:
+            n, d = stack.pop()
+            for c in n.children:
+                cd = shell(c)
+                d["children"].append(cd)
+                stack.append((c, cd))
+        return root
+
+    @classmethod
+    def from_json(cls, json_string):
+        """Rebuild a tree the way CobwebTorchTree.load_json (:94-121) does, including
+        its LIFO traversal: every node's children list comes back reversed."""
+        data = json.loads(json_string) if isinstance(json_string, str) else json_string
+        shape = data["shape"] if isinstance(data["shape"], (list, tuple)) else [data["shape"]]
+        t = cls(shape, prior_var=data.get("prior_var"))
+        t.use_info, t.acuity_cutoff, t.use_kl = data["use_info"], data["acuity_cutoff"], data["use_kl"]
+        t.alpha = data.get("alpha", 1e-8)
+
+        def mk(d):
+            n = Node(t.dim)
+            n.count = F32(d["count"])
+            n.mean = np.asarray(d["mean"], F32)
+            n.meanSq = np.asarray(d["meanSq"], F32)
+            n.sentence_id = list(d.get("sentence_id") or [])
+            return n
+
+        t.root = mk(data["root"])
+        queue = [(t.root, c) for c in data["root"]["children"]]
+        while queue:
+            parent, cd = queue.pop()
+            n = mk(cd)
+            n.parent = parent
+            parent.children.append(n)
+            queue.extend((n, c) for c in cd["children"])
+        return t
+
+    @classmethod
+    def from_arrays(cls, parent, count, mean, meanSq, sid_ptr, sid_list, prior_var=None):
+        """BFS-ordered node arrays -> tree (children in BFS order)."""
+        t = cls((mean.shape[1],), prior_var)
+        nodes = []
+        for i in range(len(parent)):
+            n = Node(t.dim)
+            n.count = F32(count[i])
+            n.mean = np.asarray(mean[i], F32)
+            n.meanSq = np.asarray(meanSq[i], F32)
+            n.sentence_id = [int(s) for s in sid_list[sid_ptr[i]:sid_ptr[i + 1]]]
+            if parent[i] >= 0:
+                n.parent = nodes[parent[i]]
+                n.parent.children.append(n)
+            nodes.append(n)
+        t.root = nodes[0]
+        return t
+
+    # ---- flattening (CobwebWrapper.build_prediction_index :107-203) ----
+    def flatten(self, n_sentences):
+        """BFS order (children in list order).  Returns (nodes, parent, mean, var,
+        node_of_sentence, max_depth); var = compute_var, prior_var for empty nodes."""
+        nodes, parent, depth = [], [], []
+        q = deque([(self.root, -1, 0)])
+        while q:
+            n, p, d = q.popleft()
+            idx = len(nodes)
+            nodes.append(n)
+            parent.append(p)
+            depth.append(d)
+            q.extend((c, idx, d + 1) for c in n.children)
+        Nn = len(nodes)
+        mean = np.empty((Nn, self.dim), F32)
+        var = np.empty((Nn, self.dim), F32)
+        node_of_sentence = np.full(n_sentences, -1, np.int64)
+        max_depth = 0
+        for i, n in enumerate(nodes):
+            mean[i] = n.mean
+            var[i] = self.compute_var(n.meanSq, n.count) if n.count > 0 else self.prior_var
+            for s in n.sentence_id or []:
+                if s < n_sentences:
+                    node_of_sentence[s] = i
+                    max_depth = max(max_depth, depth[i] + 1)
+        return nodes, np.asarray(parent, np.int64), mean, var, node_of_sentence, max_depth

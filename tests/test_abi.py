@@ -1,0 +1,76 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports every symbol
+include/cobweb_query.h declares; host tree / JSON logic.  No GPU compute here."""
+import ctypes
+import gzip
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, load_golden
+
+HEADER = os.path.join(ROOT, "include", "cobweb_query.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cwq_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol(pkg):
+    syms = header_symbols()
+    assert len(syms) >= 9
+    L = pkg.lib()
+    for s in syms:
+        assert hasattr(L, s), s
+        assert s in pkg._lib.SIGNATURES, f"{s} has no ctypes signature"
+    assert L.cwq_version() >= 100
+
+
+def test_error_path_without_gpu_compute(pkg):
+    """Argument validation happens before any device work."""
+    L = pkg.lib()
+    h = ctypes.c_void_p()
+    rc = L.cwq_index_create(0, 0, 4, None, None, None, None, 0, None, 0, None, ctypes.byref(h))
+    assert rc == pkg._lib.CWQ_ERR_ARG
+    assert b"empty" in L.cwq_last_error()
+    assert L.cwq_index_destroy(None) == 0
+
+
+def test_tree_json_roundtrip(pkg):
+    """The reference JSON loads (children reversed, as CobwebTorchTree.load_json does)
+    and a second load restores the original BFS order exactly."""
+    path = os.path.join(GOLDEN, "g1_hier_d32_tree.json.gz")
+    if not os.path.exists(path):
+        pytest.skip("fixture missing")
+    g = load_golden("g1_hier_d32")
+    with gzip.open(path, "rt") as f:
+        js = f.read()
+    t1 = pkg.CobwebTree.from_json(js)
+    t2 = pkg.CobwebTree.from_json(t1.dump_json())
+    nodes, parent, mean, var, nos, depth = t2.flatten(int(g["n_sent"]))
+    np.testing.assert_array_equal(parent, g["parent"])
+    np.testing.assert_array_equal(mean, g["mean"])
+    np.testing.assert_array_equal(np.array([n.count for n in nodes], np.float32), g["count"])
+    # single load: same nodes, reversed sibling order; every sentence keeps its path statistics
+    n1, p1, m1, v1, nos1, _ = t1.flatten(int(g["n_sent"]))
+    assert len(n1) == len(nodes)
+    np.testing.assert_array_equal(m1[nos1], mean[nos])
+
+
+def test_flatten_matches_oracle(pkg):
+    from oracle import cobweb_oracle as O
+    g = load_golden("g4_twolevel_d48")
+    t = pkg.CobwebTree.from_arrays(g["parent"], g["count"], g["mean"], g["meanSq"], g["sid_ptr"], g["sid_list"])
+    nodes, parent, mean, var, nos, _ = t.flatten(int(g["n_sent"]))
+    ref = O.flatten_tree(O.tree_from_arrays(g["parent"], g["count"], g["mean"], g["meanSq"], g["sid_ptr"],
+                                            g["sid_list"]), int(g["n_sent"]))
+    np.testing.assert_array_equal(var, ref.vars)
+    np.testing.assert_array_equal(parent, ref.parent)
+    assert [p[-1] for p in ref.paths] == list(nos)
+
+
+def test_prior_var_matches_reference_bits(pkg):
+    g = load_golden("g1_hier_d32")
+    assert np.float32(pkg.PRIOR_VAR).tobytes() == np.float32(g["prior_var"]).tobytes()
