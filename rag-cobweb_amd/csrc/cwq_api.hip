@@ -403,9 +403,9 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   a.ld = ix->ld_int;
   a.nrows = ix->NI;
   a.nrows_pad = (int)round_up(ix->NI, kWave);
-  a.n_qblocks = (int)((c.nq + 4 * tq - 1) / (4 * tq));
+  a.n_qblocks = (int)((c.nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
   const int nslab = pick_nslab(ix, ix->NI, a.n_qblocks);
-  a.rows_per_slab = (int)round_up((a.nrows_pad + nslab - 1) / nslab, kWave);
+  a.rows_per_slab = (int)round_up((a.nrows_pad + nslab - 1) / nslab, scan_rows_per_tile(kl));
   const int nslab2 = (a.nrows_pad + a.rows_per_slab - 1) / a.rows_per_slab;
   a.out = c.S_int;
   a.ldo = ix->NI;
@@ -421,7 +421,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
 int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
                   float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s) {
   const int tq = scan_tq(kl);
-  const int nqb = (int)((c.nq + 4 * tq - 1) / (4 * tq));
+  const int nqb = (int)((c.nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
   struct Seg {
     bool iso;
     int n;
@@ -435,12 +435,14 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
     ns[i] = 0;
     rps[i] = 0;
     if (segs[i].n == 0) continue;
+    const int tile = scan_rows_per_tile(kl);
     const int npad = (int)round_up(segs[i].n, kWave);
     const int n = pick_nslab(ix, segs[i].n, nqb);
-    rps[i] = (int)round_up((npad + n - 1) / n, kWave);
+    rps[i] = (int)round_up((npad + n - 1) / n, tile);   // slabs hold whole tiles: no row scanned twice
     ns[i] = (npad + rps[i] - 1) / rps[i];
   }
-  const int nslab_total = ns[0] + ns[1];
+  const int lps = scan_lists_per_slab(kl);
+  const int nslab_total = (ns[0] + ns[1]) * lps;
   if (nslab_total_out) *nslab_total_out = nslab_total;
   int slab_off = 0;
   for (int i = 0; i < 2; ++i) {
@@ -466,7 +468,7 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
     a.slab_off = slab_off;
     a.K = K;
     HIPCHK(launch_scan(segs[i].iso, epi, cat, kl, c.X, segs[i].A, segs[i].B, a, ns[i], s));
-    slab_off += ns[i];
+    slab_off += ns[i] * lps;
   }
   return CWQ_OK;
 }
@@ -515,18 +517,16 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));
   // partial-list entries per query (upper bound over both segments)
   const int tq = scan_tq(kl);
-  const int64_t nq_est = std::min<int64_t>(nq, 1 << 20);
-  const int nqb_est = (int)((nq_est + 4 * tq - 1) / (4 * tq));
-  const int max_slabs = pick_nslab(ix, ix->NL_iso, std::max(1, nqb_est / 64)) +
-                        pick_nslab(ix, ix->NL_an, std::max(1, nqb_est / 64)) + 2;
+  const int nqb_est = (int)((nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8 : (size_t)max_slabs * K * 12 + K * 12;
   const int64_t cq = chunk_queries(ix, nq, extra);
   int rc;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
-    const int nqb = (int)((nqc + 4 * tq - 1) / (4 * tq));
-    const int slabs = pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2;
+    const int nqb = (int)((nqc + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+    const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
     size_t need = chunk_bytes(ix, nq_pad) + 16 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
                     : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12);
@@ -662,12 +662,14 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   const int64_t cap_list = 1 + (int64_t)ix->NI + R;
   const int kl = 64, tq = scan_tq(kl);
   int rc;
-  const int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + 64 * 12 * 64);
+  const int nqb_est = (int)((nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
+  const int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + (size_t)max_slabs * R * 12 + R * 12);
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
-    const int nqb = (int)((nqc + 4 * tq - 1) / (4 * tq));
-    const int slabs = pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2;
+    const int nqb = (int)((nqc + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+    const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 8) + 16 * 256;
     if ((rc = ix->reserve(need))) return rc;

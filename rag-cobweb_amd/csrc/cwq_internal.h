@@ -8,7 +8,7 @@ namespace cwq {
 
 constexpr int kWave = 64;        // CDNA wavefront
 constexpr int kWavesPerWG = 4;   // 256-thread workgroups
-constexpr int kDChunk = 16;      // dimensions held in registers per step (D padded to this)
+constexpr int kDChunk = 32;      // D is padded to a multiple of this (largest compute chunk)
 
 // Per leaf-class row constants (one float4 load per lane in the epilogue).
 struct RowMeta {
@@ -93,7 +93,11 @@ hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_
 // The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
 hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
                        const ScanArgs& a, int nslab, hipStream_t s);
-int scan_tq(int kl);   // queries per wave for a list width
+int scan_tq(int kl);             // queries per wave for a list width
+int scan_rows_per_tile(int kl);  // rows per wave per tile (64 * rows per lane)
+int scan_queries_per_block(int kl);  // queries per workgroup
+int scan_dchunk(int kl);
+int scan_lists_per_slab(int kl);  // partial top-k lists a workgroup writes per query         // dims per compute phase (D is padded to a multiple of 32)
 
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
