@@ -373,13 +373,33 @@ struct Chunk {
   float *S_int = nullptr, *P = nullptr, *BF = nullptr, *LPF = nullptr;   // [nq_pad][NI]
 };
 
-// Choose the slab split of a segment so that the grid has ~8 waves of workgroups.
-int pick_nslab(const cwq_index* ix, int nrows, int n_qblocks) {
+// Query blocks of a launch; a multiple of 8 under the XCD-aware mapping (the
+// extra blocks exit at once).
+int n_qblocks_for(int64_t nq, int kl) {
+  const int qpb = scan_queries_per_block(kl);
+  const int n = (int)((nq + qpb - 1) / qpb);
+  return scan_xcd_map() ? (int)round_up(n, 8) : n;
+}
+
+// Choose the slab split of a segment: enough workgroups for >= ~5 waves of the
+// resident grid, with the last wave as full as possible (tail balance).
+int pick_nslab(const cwq_index* ix, int nrows, int n_qblocks, int kl = 16) {
   if (nrows <= 0) return 0;
-  const int target = std::max(1, 8 * 4 * ix->cus);
   const int max_slab = (int)std::max<int64_t>(1, round_up(nrows, kWave) / 256);
-  int n = (target + n_qblocks - 1) / n_qblocks;
-  return std::max(1, std::min(n, max_slab));
+  const int64_t slots = (int64_t)ix->cus * scan_wgs_per_cu(kl);
+  int best = 1;
+  double best_fill = -1.0;
+  for (int r = 5; r <= 10; ++r) {
+    const int n = (int)std::max<int64_t>(1, std::min<int64_t>(max_slab, r * slots / std::max(1, n_qblocks)));
+    const int64_t wgs = (int64_t)n * n_qblocks;
+    const int64_t rounds = (wgs + slots - 1) / slots;
+    const double fill = (double)wgs / (double)(rounds * slots);
+    if (fill >= best_fill - 1e-9) {
+      best_fill = fill;
+      best = n;
+    }
+  }
+  return best;
 }
 
 ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
@@ -392,6 +412,7 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
   a.flags = ix->row_flags;
   a.P = c.P ? c.P : ix->dummy;
   a.ldP = std::max(ix->NI, 1);
+  a.xcd_map = scan_xcd_map();
   return a;
 }
 
@@ -403,7 +424,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   a.ld = ix->ld_int;
   a.nrows = ix->NI;
   a.nrows_pad = (int)round_up(ix->NI, kWave);
-  a.n_qblocks = (int)((c.nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  a.n_qblocks = n_qblocks_for(c.nq, kl);
   const int nslab = pick_nslab(ix, ix->NI, a.n_qblocks);
   a.rows_per_slab = (int)round_up((a.nrows_pad + nslab - 1) / nslab, scan_rows_per_tile(kl));
   const int nslab2 = (a.nrows_pad + a.rows_per_slab - 1) / a.rows_per_slab;
@@ -421,7 +442,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
 int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
                   float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s) {
   const int tq = scan_tq(kl);
-  const int nqb = (int)((c.nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  const int nqb = n_qblocks_for(c.nq, kl);
   struct Seg {
     bool iso;
     int n;
@@ -517,7 +538,7 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));
   // partial-list entries per query (upper bound over both segments)
   const int tq = scan_tq(kl);
-  const int nqb_est = (int)((nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  const int nqb_est = n_qblocks_for(nq, kl);
   const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8 : (size_t)max_slabs * K * 12 + K * 12;
   const int64_t cq = chunk_queries(ix, nq, extra);
@@ -525,7 +546,7 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
-    const int nqb = (int)((nqc + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+    const int nqb = n_qblocks_for(nqc, kl);
     const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
     size_t need = chunk_bytes(ix, nq_pad) + 16 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
@@ -662,13 +683,13 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   const int64_t cap_list = 1 + (int64_t)ix->NI + R;
   const int kl = 64, tq = scan_tq(kl);
   int rc;
-  const int nqb_est = (int)((nq + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+  const int nqb_est = n_qblocks_for(nq, kl);
   const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
   const int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + (size_t)max_slabs * R * 12 + R * 12);
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
-    const int nqb = (int)((nqc + scan_queries_per_block(kl) - 1) / scan_queries_per_block(kl));
+    const int nqb = n_qblocks_for(nqc, kl);
     const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 8) + 16 * 256;

@@ -8,6 +8,7 @@ namespace cwq {
 
 constexpr int kWave = 64;        // CDNA wavefront
 constexpr int kWavesPerWG = 4;   // 256-thread workgroups
+constexpr int kXQ = 16;         // queries per scalar-load group (queries per wave)
 constexpr int kDChunk = 32;      // D is padded to a multiple of this (largest compute chunk)
 
 // Per leaf-class row constants (one float4 load per lane in the epilogue).
@@ -32,7 +33,8 @@ struct ScanArgs {
   int nrows;           // valid rows in the segment
   int nrows_pad;       // rows rounded up to 64
   int rows_per_slab;   // rows per workgroup (multiple of 64)
-  int n_qblocks;       // query blocks of (4 * TQ) queries
+  int n_qblocks;       // query blocks (a multiple of 8 when xcd_map)
+  int xcd_map;         // XCD-aware block -> (slab, query block) mapping
   int seg_base;        // global leaf-row id of segment row 0
   const RowMeta* meta; // [nrows]
   const int* par;      // [nrows] internal-node id of the parent (-1: none)
@@ -93,11 +95,13 @@ hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_
 // The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
 hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
                        const ScanArgs& a, int nslab, hipStream_t s);
-int scan_tq(int kl);             // queries per wave for a list width
-int scan_rows_per_tile(int kl);  // rows per wave per tile (64 * rows per lane)
+int scan_tq(int kl);                 // queries per wave for a list width
+int scan_rows_per_tile(int kl);      // rows per workgroup step (64 * rows per lane [* 4 if shared queries])
 int scan_queries_per_block(int kl);  // queries per workgroup
-int scan_dchunk(int kl);
-int scan_lists_per_slab(int kl);  // partial top-k lists a workgroup writes per query         // dims per compute phase (D is padded to a multiple of 32)
+int scan_dchunk(int kl);             // dims per compute phase (D is padded to a multiple of 32)
+int scan_lists_per_slab(int kl);     // partial top-k lists a workgroup writes per query
+int scan_xcd_map();                  // XCD-aware block mapping (CWQ_XCD_MAP, default 1)
+int scan_wgs_per_cu(int kl);         // resident workgroups per CU (occupancy query, cached)
 
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,

@@ -15,7 +15,8 @@ import cobweb_pkg  # noqa: E402
 
 pkg = cobweb_pkg.load()
 N, D, Q, k = (int(v) for v in (sys.argv[1:5] if len(sys.argv) >= 5 else (1_000_000, 768, 10_000, 10)))
-cfgs = [int(c) for c in (sys.argv[5].split(",") if len(sys.argv) > 5 else "0,1,2,3".split(","))]
+# variants: "scan_cfg[:xcd_map]" (CWQ_SCAN_CFG, CWQ_XCD_MAP)
+cfgs = sys.argv[5].split(",") if len(sys.argv) > 5 else ["0:1", "0:0", "1:1", "3:1"]
 X = pkg.synth.synthetic_corpus(N, D, seed=0)
 t = pkg.synth.flat_synth(X)
 ix = pkg.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"])
@@ -25,7 +26,9 @@ ix.set_timing(True)
 res, ref = {c: [] for c in cfgs}, None
 for rnd in range(3):
     for c in cfgs:
-        os.environ["CWQ_SCAN_CFG"] = str(c)
+        sc_, _, xm = c.partition(":")
+        os.environ["CWQ_SCAN_CFG"] = sc_
+        os.environ["CWQ_XCD_MAP"] = xm or "1"
         ids, sc = ix.score_topk(Qs, k)
         tm = ix.last_timing()
         res[c].append(tm["leaf_scan_ms"])
