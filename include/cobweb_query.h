@@ -145,6 +145,34 @@ int cwq_last_timing(cwq_index* idx, float* out5);
 int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order, const int64_t* group_ptr,
                        int64_t n_groups, float* count, float* mean, float* meanSq, void* stream);
 
+/*
+ * Incremental fit (ifit) support: category-utility scoring on the GPU (add path,
+ * CobwebTorchTree.cobweb, CobwebTorchTree.py:143-233).  Node statistics live in a
+ * caller-owned device pool: count[cap], mean[cap*dim], meanSq[cap*dim] (slot = row).
+ *
+ * cwq_fit_kl: out[j] = compute_score(cand_j, ref_j) = KL(cand || ref)
+ *   (CobwebTorchTree.py:344-364, use_info=True, use_kl=True) for jobs[4*j..4*j+3] =
+ *   {cand_type, n1, n2, ref_type}:
+ *     cand_type 0: node n1                    (CobwebTorchNode.mean_var, :211-212)
+ *               1: node n1 with x inserted    (mean_var_insert, :214-222)
+ *               2: new leaf from x            (mean_var_new, :204-209)
+ *               3: merge(n1, n2) with x       (mean_var_merge, :224-239)
+ *     ref_type  0: parent p_slot; 1: parent with x inserted.
+ *   x, jobs, out: device.  Asynchronous on `stream`.
+ */
+int cwq_fit_kl(const float* count, const float* mean, const float* meanSq, int32_t dim, const float* x,
+               float prior_var, int32_t p_slot, const int32_t* jobs, int32_t n_jobs, float* out, void* stream);
+
+/*
+ * cwq_fit_node_op: one node update in the pool, same fp32 op order as the reference:
+ *   op 0 increment_counts(dst, x)           (CobwebTorchNode.py:57-68)
+ *   op 1 update_counts_from_node(dst, src)  (:70-85; merge and the copy constructor)
+ *   op 2 zero(dst)                          (a fresh node)
+ *   op 3 *flag = is_exact_match(dst, x)     (:652-666, torch.isclose defaults)
+ */
+int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_t dim, int32_t dst, int32_t src,
+                    const float* x, int32_t* flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,254 @@
+"""Incremental fit (ifit) with the category-utility scoring on the GPU.
+
+`TreeFitter.ifit(x)` is CobwebTorchTree.cobweb (CobwebTorchTree.py:143-233): the
+host walks the tree and picks the operation (best / new / merge / split, fringe
+split at a leaf) exactly as the reference does; every D-length computation runs in
+libcwq on a device pool of node statistics:
+
+* per tree level ONE `cwq_fit_kl` launch returns KL(c || P+x), KL(c+x || P+x) for
+  every child c and KL(new || P+x) -- the terms of two_best_children,
+  pu_for_insert and pu_for_new_child (CobwebTorchNode.py:374-515); a second launch
+  returns the merge / split terms (:550-650) when those operations apply;
+* node updates (increment_counts, update_counts_from_node, is_exact_match) are
+  `cwq_fit_node_op` launches.
+
+The scalar combinations (p(c) weights, sums over children, the descending sort by
+(gain, count, random()), the operation choice by (pu, random(), name)) follow the
+reference's float32 op order; `random()` is drawn from Python's global `random`
+module in the same order as the reference, so a run seeded like the reference makes
+the same tie-breaks.  Counts are kept on the host as well (exact small integers).
+"""
+import ctypes
+import random as _random_mod
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+from .tree import Node
+
+F32 = np.float32
+_ADD, _COMBINE, _ZERO, _EXACT = 0, 1, 2, 3
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _seqsum(terms):
+    """Python `score = 0.0; score += t` over float32 terms: sequential fp32 sum."""
+    if len(terms) == 0:
+        return F32(0.0)
+    return F32(np.add.accumulate(np.asarray(terms, F32), dtype=F32)[-1])
+
+
+class TreeFitter:
+    def __init__(self, tree, device=None, rng=None):
+        self.tree = tree
+        self.D = tree.dim
+        self.pv = F32(tree.prior_var)
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rng = rng if rng is not None else _random_mod   # the reference draws from the global random()
+        self.cap, self.used, self.free = 0, 0, []
+        self.count = self.mean = self.meanSq = None
+        self._flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._owned = []
+        self._grow(max(64, self._n_nodes() * 2))
+        stack = [tree.root]
+        while stack:       # upload the existing tree
+            n = stack.pop()
+            self._attach(n)
+            stack.extend(n.children)
+
+    # ---- device pool ----
+    def _n_nodes(self):
+        n, stack = 0, [self.tree.root]
+        while stack:
+            x = stack.pop()
+            n += 1
+            stack.extend(x.children)
+        return n
+
+    def _grow(self, cap):
+        cnt = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        mean = torch.zeros((cap, self.D), dtype=torch.float32, device=self.dev)
+        m2 = torch.zeros((cap, self.D), dtype=torch.float32, device=self.dev)
+        if self.cap:
+            cnt[:self.cap] = self.count
+            mean[:self.cap] = self.mean
+            m2[:self.cap] = self.meanSq
+        self.count, self.mean, self.meanSq, self.cap = cnt, mean, m2, cap
+
+    def _new_slot(self):
+        if self.free:
+            s = self.free.pop()
+        else:
+            if self.used == self.cap:
+                self._grow(self.cap * 2)
+            s = self.used
+            self.used += 1
+        self._op(_ZERO, s)
+        return s
+
+    def _attach(self, n):
+        n.slot = self._new_slot()
+        self._owned.append(n)
+        if n.count != 0:
+            self.count[n.slot] = float(n.count)
+            self.mean[n.slot] = torch.from_numpy(np.asarray(n.mean, F32)).to(self.dev)
+            self.meanSq[n.slot] = torch.from_numpy(np.asarray(n.meanSq, F32)).to(self.dev)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _op(self, op, dst, src=-1, x=None):
+        check(lib().cwq_fit_node_op(op, _p(self.count), _p(self.mean), _p(self.meanSq), self.D, dst, src,
+                                    _p(x) if x is not None else None, _p(self._flag), self._stream()))
+
+    def _kl(self, p_slot, x, jobs):
+        jobs = np.ascontiguousarray(np.asarray(jobs, np.int32).reshape(-1, 4))
+        jt = torch.from_numpy(jobs).to(self.dev)
+        out = torch.empty(len(jobs), dtype=torch.float32, device=self.dev)
+        check(lib().cwq_fit_kl(_p(self.count), _p(self.mean), _p(self.meanSq), self.D, _p(x), float(self.pv),
+                               int(p_slot), _p(jt), len(jobs), _p(out), self._stream()))
+        return out.cpu().numpy()
+
+    def _new_node(self):
+        n = Node(self.D)
+        n.slot = self._new_slot()
+        self._owned.append(n)
+        return n
+
+    def _increment(self, n, x):
+        self._op(_ADD, n.slot, x=x)
+        n.count = F32(n.count + F32(1))
+
+    def _combine(self, dst, src):
+        self._op(_COMBINE, dst.slot, src.slot)
+        dst.count = F32(dst.count + src.count)
+
+    def _exact_match(self, n, x):
+        self._op(_EXACT, n.slot, x=x)
+        return bool(self._flag.item())
+
+    # ---- CobwebTorchTree.cobweb ----
+    def ifit(self, x_np):
+        x = torch.as_tensor(np.asarray(x_np, F32)).to(self.dev)
+        t = self.tree
+        cur = t.root
+        while cur is not None:
+            if not cur.children and (cur.count == 0 or self._exact_match(cur, x)):
+                self._increment(cur, x)
+                break
+            if not cur.children:                                   # fringe split :190-204
+                new = self._new_node()
+                new.parent = cur.parent
+                self._combine(new, cur)                            # copy constructor
+                cur.parent = new
+                new.children.append(cur)
+                if new.parent is not None:
+                    new.parent.children.remove(cur)
+                    new.parent.children.append(new)
+                else:
+                    t.root = new
+                self._increment(new, x)
+                cur = self._create_child(new, x)
+                break
+            action, b1, b2 = self._best_operation(cur, x)
+            if action == "best":
+                self._increment(cur, x)
+                cur = b1
+            elif action == "new":
+                self._increment(cur, x)
+                cur = self._create_child(cur, x)
+                break
+            elif action == "merge":                                # CobwebTorchNode.py:517-548
+                self._increment(cur, x)
+                nc = self._new_node()
+                nc.parent = cur
+                self._combine(nc, b1)
+                self._combine(nc, b2)
+                b1.parent = nc
+                b2.parent = nc
+                nc.children += [b1, b2]
+                cur.children.remove(b1)
+                cur.children.remove(b2)
+                cur.children.append(nc)
+                cur = nc
+            else:                                                  # split :593-609
+                cur.children.remove(b1)
+                for c in b1.children:
+                    c.parent = cur
+                    cur.children.append(c)
+                self.free.append(b1.slot)
+                b1.slot = -1
+        return cur
+
+    def _create_child(self, parent, x):
+        ch = self._new_node()
+        ch.parent = parent
+        self._increment(ch, x)
+        parent.children.append(ch)
+        return ch
+
+    def _best_operation(self, cur, x):
+        """two_best_children + get_best_operation (CobwebTorchNode.py:287-420)."""
+        ch = cur.children
+        b = len(ch)
+        jobs = []
+        for c in ch:
+            jobs += [1, c.slot, -1, 1, 0, c.slot, -1, 1]
+        jobs += [2, -1, -1, 1]
+        out = self._kl(cur.slot, x, jobs)
+        U, T, knew = out[0:2 * b:2], out[1:2 * b:2], out[2 * b]
+        nc = np.array([c.count for c in ch], F32)
+        nP1 = F32(cur.count + F32(1))
+        p1 = (nc + F32(1)) / nP1
+        p2 = nc / nP1
+        gain = p1 * U - p2 * T
+        rel = [(gain[i], nc[i], self.rng.random(), i) for i in range(b)]
+        rel.sort(key=lambda r: (r[0], r[1], r[2]), reverse=True)
+        i1 = rel[0][3]
+        i2 = rel[1][3] if b > 1 else None
+        b1, b2 = ch[i1], (ch[i2] if i2 is not None else None)
+        t_all = p2 * T
+        t_ins = t_all.copy()
+        t_ins[i1] = p1[i1] * U[i1]
+        pu_best = F32(_seqsum(t_ins) / F32(b))
+        pu_new = F32(F32(_seqsum(t_all) + F32(F32(F32(1.0) / nP1) * knew)) / F32(b + 1))
+        ops = [(pu_best, self.rng.random(), "best"), (pu_new, self.rng.random(), "new")]
+        extra = []
+        do_merge = b > 2 and b2 is not None
+        do_split = len(b1.children) > 0
+        if do_merge:
+            extra += [3, b1.slot, b2.slot, 1]
+        split_nodes = []
+        if do_split:
+            split_nodes = [c for c in ch if c is not b1] + list(b1.children)
+            for c in split_nodes:
+                extra += [0, c.slot, -1, 0]
+        if extra:
+            out2 = self._kl(cur.slot, x, extra)
+            if do_merge:
+                keep = [i for i in range(b) if i != i1 and i != i2]
+                pm = F32(F32(F32(b1.count + b2.count) + F32(1)) / nP1)
+                pu_merge = F32(F32(_seqsum(t_all[keep]) + F32(pm * out2[0])) / F32(b - 1))
+                ops.append((pu_merge, self.rng.random(), "merge"))
+            if do_split:
+                ks = out2[1:] if do_merge else out2
+                terms = np.array([c.count for c in split_nodes], F32) / F32(cur.count) * ks
+                pu_split = F32(_seqsum(terms) / F32(b - 1 + len(b1.children)))
+                ops.append((pu_split, self.rng.random(), "split"))
+        ops.sort(reverse=True)
+        return ops[0][2], b1, b2
+
+    # ---- results back to the host tree ----
+    def sync_to_host(self):
+        cnt = self.count.cpu().numpy()
+        mean = self.mean.cpu().numpy()
+        m2 = self.meanSq.cpu().numpy()
+        for n in self._owned:
+            if n.slot >= 0:
+                n.count = F32(cnt[n.slot])
+                n.mean = mean[n.slot].copy()
+                n.meanSq = m2[n.slot].copy()

@@ -19,7 +19,7 @@ PRIOR_VAR = F32(1.0) / (F32(2 * math.e) * F32(math.pi))
 
 
 class Node:
-    __slots__ = ("count", "mean", "meanSq", "children", "parent", "sentence_id")
+    __slots__ = ("count", "mean", "meanSq", "children", "parent", "sentence_id", "slot")
 
     def __init__(self, dim):
         self.count = F32(0.0)
@@ -28,6 +28,7 @@ class Node:
         self.children = []
         self.parent = None
         self.sentence_id = []
+        self.slot = -1          # row in the device stats pool while a TreeFitter owns the tree
 
     def increment_counts(self, x):
         """Welford insert, CobwebTorchNode.py:57-68 (fp32, same op order)."""

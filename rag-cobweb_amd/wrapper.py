@@ -77,22 +77,25 @@ class CobwebWrapper:
             new_embeddings = new_vectors
             if isinstance(new_embeddings, list):
                 new_embeddings = np.asarray(new_embeddings, dtype=np.float32)
-            if new_embeddings.shape[1] != self.tree.shape[0]:
+            if self.tree is not None and new_embeddings.shape[1] != self.tree.shape[0]:
                 print(f"[Warning] Provided vector dim {new_embeddings.shape[1]} != tree dim "
                       f"{self.tree.shape[0]}, re-encoding...")
                 new_embeddings = np.asarray(self.encode_func(new_sentences), dtype=np.float32)
         from .fit import TreeFitter
+        X = np.asarray(new_embeddings.detach().cpu().numpy() if torch.is_tensor(new_embeddings)
+                       else new_embeddings, dtype=np.float32)
+        if self.tree is None:
+            self.tree = CobwebTree(X.shape[1:])
         fitter = TreeFitter(self.tree, device=self.device)
         start = len(self.sentences)
-        X = torch.as_tensor(np.asarray(new_embeddings if not torch.is_tensor(new_embeddings)
-                                       else new_embeddings.cpu().numpy(), dtype=np.float32))
         for i, sent in enumerate(new_sentences):
             self.sentences.append(sent)
-            leaf = fitter.ifit(X[i].numpy())
+            leaf = fitter.ifit(X[i])
             if leaf.sentence_id is None:
                 leaf.sentence_id = []
             leaf.sentence_id.append(start + i)
             self.sentence_to_node[start + i] = leaf
+        fitter.sync_to_host()
         self._invalidate_prediction_index()
 
     # --------------------------------------------------------------- index build

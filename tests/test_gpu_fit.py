@@ -1,0 +1,71 @@
+"""GPU ifit (add path, CU scoring on libcwq) against trees built by the reference's
+own ifit (golden G1, G5): identical structure, sentence placement and counts; and the
+drop-in CobwebWrapper end to end (construct from embeddings -> query)."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def bfs(root):
+    out, q, h = [], [root], 0
+    while h < len(q):
+        n = q[h]
+        h += 1
+        out.append(n)
+        q.extend(n.children)
+    return out
+
+
+@pytest.mark.parametrize("name", ["g1_hier_d32", "g5_hier_d384"])
+def test_gpu_ifit_reproduces_reference_tree(pkg, name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = load_golden(name)
+    random.seed(0)   # gen_golden.py seeds the reference the same way
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(len(g["X"]))], corpus_embeddings=g["X"])
+    nodes = bfs(w.tree.root)
+    pos = {id(n): i for i, n in enumerate(nodes)}
+    parent = np.array([-1 if n.parent is None else pos[id(n.parent)] for n in nodes])
+    np.testing.assert_array_equal(parent, g["parent"])
+    np.testing.assert_array_equal([s for n in nodes for s in n.sentence_id], g["sid_list"])
+    np.testing.assert_array_equal(np.array([n.count for n in nodes], np.float32), g["count"])
+    np.testing.assert_allclose(np.stack([n.mean for n in nodes]), g["mean"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np.stack([n.meanSq for n in nodes]), g["meanSq"], rtol=1e-4, atol=1e-4)
+    # the drop-in answers like the reference
+    k = int(g["k"])
+    for qi in range(6):
+        got = w.cobweb_predict_fast(g["Xq"][qi], k, return_ids=True)
+        ref = g["fast_ids"][qi]
+        rs = g["rank_scores"][qi]
+        for a, b in zip(got, ref):
+            if a != b:
+                assert abs(rs[a] - rs[b]) <= 1e-5 * abs(rs[b])
+        sent = w.cobweb_predict_fast(g["Xq"][qi], k)
+        assert sent == [f"s{i}" for i in got]
+        basic = w.cobweb_predict(g["Xq"][qi], k, return_ids=True)
+        exp = [s for nid in g["cat_nodes"][qi] for s in
+               sorted(g["sid_list"][g["sid_ptr"][nid]:g["sid_ptr"][nid + 1]])]
+        assert basic == exp
+    with pytest.raises(IndexError):
+        w.cobweb_predict(g["Xq"][0], int(g["n_leaf_nodes"]) + 1)
+
+
+def test_wrapper_json_roundtrip_and_add(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = load_golden("g1_hier_d32")
+    random.seed(0)
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(200)], corpus_embeddings=g["X"][:200])
+    w.add_sentences([f"s{i}" for i in range(200, 300)], g["X"][200:])   # incremental add, same stream
+    w2 = pkg.CobwebWrapper.load_json(w.dump_json())
+    assert len(w2) == 300
+    for qi in range(4):
+        a = w.cobweb_predict_fast(g["Xq"][qi], 10, return_ids=True)
+        b = w2.cobweb_predict_fast(g["Xq"][qi], 10, return_ids=True)
+        assert a == b
