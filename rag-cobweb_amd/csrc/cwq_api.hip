@@ -14,7 +14,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -93,8 +95,15 @@ struct cwq_index {
   int* row_of_sent = nullptr;
   int* node_src = nullptr;
   float* dummy = nullptr;
+  // bf16-MFMA filter operands for the isotropic rows (cwq_mfma.hip): row-major
+  // fp32 (exact rerank) and bf16 (GEMM) copies padded to whole 128-row tiles, norms
+  int64_t ld_f = 0;
+  float *iso_Mf = nullptr, *iso_n2 = nullptr, *iso_n1 = nullptr, *iso_c = nullptr;   // iso_c: centre [D]
+  uint16_t* iso_Mb = nullptr;
+  int64_t stats[4] = {0, 0, 0, 0};   // cwq_last_stats
   // timing (cwq_set_timing)
   bool timing = false;
+  int filter = -1;   // cwq_set_filter
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float t_ms[5] = {0, 0, 0, 0, 0};
   // workspace
@@ -295,6 +304,17 @@ extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const 
   HIPCHK(launch_gather_T(mean, var, dim, d_rows, ix->NL_iso, 0, ix->iso_M, ix->ld_iso, DP, s));
   HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 1, ix->an_A, ix->ld_an, DP, s));
   HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 2, ix->an_B, ix->ld_an, DP, s));
+  if (ix->NL_iso > 0) {
+    ix->ld_f = round_up(ix->NL_iso, kFiltTile);
+    if ((rc = ix->alloc(&ix->iso_Mf, (size_t)DP * ix->ld_f))) return rc;
+    if ((rc = ix->alloc(&ix->iso_Mb, (size_t)DP * ix->ld_f))) return rc;
+    if ((rc = ix->alloc(&ix->iso_n2, ix->ld_f))) return rc;
+    if ((rc = ix->alloc(&ix->iso_n1, ix->ld_f))) return rc;
+    if ((rc = ix->alloc(&ix->iso_c, dim))) return rc;
+    HIPCHK(hipMemcpyAsync(ix->iso_c, mean, (size_t)dim * 4, hipMemcpyDeviceToDevice, s));   // root mean
+    HIPCHK(launch_rows_prep(mean, dim, d_rows, ix->NL_iso, ix->iso_c, DP, ix->ld_f, ix->iso_Mf, ix->iso_Mb,
+                            ix->iso_n2, ix->iso_n1, s));
+  }
 
   if ((rc = ix->alloc(&ix->logdet_int, ix->NI))) return rc;
   if ((rc = ix->alloc(&ix->logdet_row, ix->NL))) return rc;
@@ -439,8 +459,11 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
 }
 
 // One scan over both leaf-row segments.
+// seg_mask: bit 0 = isotropic segment, bit 1 = anisotropic; TOPK lists start at
+// slab_off0 (slots before it are filled by the caller).
 int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
-                  float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s) {
+                  float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s,
+                  int seg_mask = 3, int slab_off0 = 0) {
   const int tq = scan_tq(kl);
   const int nqb = n_qblocks_for(c.nq, kl);
   struct Seg {
@@ -455,6 +478,7 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
   for (int i = 0; i < 2; ++i) {
     ns[i] = 0;
     rps[i] = 0;
+    if (!((seg_mask >> i) & 1)) segs[i].n = 0;
     if (segs[i].n == 0) continue;
     const int tile = scan_rows_per_tile(kl);
     const int npad = (int)round_up(segs[i].n, kWave);
@@ -463,9 +487,9 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
     ns[i] = (npad + rps[i] - 1) / rps[i];
   }
   const int lps = scan_lists_per_slab(kl);
-  const int nslab_total = (ns[0] + ns[1]) * lps;
+  const int nslab_total = slab_off0 + (ns[0] + ns[1]) * lps;
   if (nslab_total_out) *nslab_total_out = nslab_total;
-  int slab_off = 0;
+  int slab_off = slab_off0;
   for (int i = 0; i < 2; ++i) {
     if (segs[i].n == 0) continue;
     ScanArgs a = base_args(ix, c);
@@ -523,34 +547,103 @@ int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
 
 }  // namespace
 
-extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
-                              void* stream) {
-  if (!ix || (!q && nq > 0) || (!ids && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
-  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
-  if (nq == 0) return CWQ_OK;
-  std::lock_guard<std::mutex> lk(ix->mu);
-  DevGuard dg(ix->device);
-  hipStream_t s = (hipStream_t)stream;
-  for (float& t : ix->t_ms) t = 0.f;
+namespace {
+
+constexpr int kFiltMinRows = 16384;   // automatic mode: below this the exact scan is as fast
+constexpr int kFiltMaxK = 32;         // the certificate needs K' = 64 >= 2k candidates
+
+bool use_filter(const cwq_index* ix, int k) {
+  if (k > kFiltMaxK || ix->NL_iso == 0 || !ix->iso_Mb) return false;
+  int mode = ix->filter;
+  if (mode < 0) {
+    const char* e = getenv("CWQ_FILTER");
+    if (e && *e) mode = atoi(e) ? 1 : 0;
+  }
+  if (mode < 0) return ix->NL_iso >= kFiltMinRows;
+  return mode == 1;
+}
+
+// Error-bound constants of the approximate keys (cwq_mfma.hip header): bf16 rounding
+// of both operands (2 * 2^-8 + 2^-16) plus fp32 accumulation over DP terms, each
+// small term doubled for margin.
+void filter_consts(const cwq_index* ix, GemmArgs& g) {
+  g.eta = (float)(std::ldexp(1.0, -7) + std::ldexp(1.0, -15) + (ix->DP + 64) * std::ldexp(1.0, -23));
+  g.eta_n = (float)std::ldexp(1.0, -20);
+  g.slack = (float)std::ldexp(1.0, -16);
+}
+
+int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                    hipStream_t s, bool allow_filter);
+
+// Queries whose certificate failed: exact scan, results scattered back in place.
+int rerun_exact(cwq_index* ix, const float* q, const std::vector<int64_t>& qi, int32_t k, int64_t* ids, float* scores,
+                hipStream_t s) {
+  const int64_t n = (int64_t)qi.size();
+  float* tq = nullptr;
+  float* ts = nullptr;
+  int64_t* tid = nullptr;
+  const size_t D = (size_t)ix->D;
+  if (hipMalloc(&tq, n * D * 4) != hipSuccess || hipMalloc(&tid, n * k * 8) != hipSuccess ||
+      (scores && hipMalloc(&ts, n * k * 4) != hipSuccess)) {
+    (void)hipFree(tq);
+    (void)hipFree(tid);
+    return fail(CWQ_ERR_OOM, "fallback buffers");
+  }
+  int rc = CWQ_OK;
+  for (int64_t i = 0; i < n && rc == CWQ_OK; ++i)
+    if (hipMemcpyAsync(tq + i * D, q + qi[i] * D, D * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      rc = fail(CWQ_ERR_HIP, "fallback gather");
+  if (rc == CWQ_OK) rc = score_topk_impl(ix, tq, n, k, tid, ts, s, false);
+  for (int64_t i = 0; i < n && rc == CWQ_OK; ++i) {
+    if (hipMemcpyAsync(ids + qi[i] * k, tid + i * k, (size_t)k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        (scores && hipMemcpyAsync(scores + qi[i] * k, ts + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s) !=
+                       hipSuccess))
+      rc = fail(CWQ_ERR_HIP, "fallback scatter");
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && rc == CWQ_OK) rc = fail(CWQ_ERR_HIP, "fallback sync");
+  (void)hipFree(tq);
+  (void)hipFree(tid);
+  if (ts) (void)hipFree(ts);
+  return rc;
+}
+
+int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                    hipStream_t s, bool allow_filter) {
   const bool general = k > 64;
+  const bool filt = !general && allow_filter && use_filter(ix, k);
   const int kl = k <= 16 ? 16 : 64;
   const int K = std::min<int>(k, 64);
+  const int Kp = kFiltCand;
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));
-  // partial-list entries per query (upper bound over both segments)
-  const int tq = scan_tq(kl);
+  // partial-list entries per query (upper bound over both segments; one list for the filter)
   const int nqb_est = n_qblocks_for(nq, kl);
-  const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
-  const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8 : (size_t)max_slabs * K * 12 + K * 12;
+  auto n_slabs = [&](int nqb) {
+    return filt ? 1 + (pick_nslab(ix, ix->NL_an, nqb) + 1) * scan_lists_per_slab(kl)
+                : (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
+  };
+  const size_t filt_q = filt ? (size_t)ix->DP * 2 + 8 + (size_t)Kp * 8 + 4 + 4 * 256 : 0;
+  const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
+                               : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
   const int64_t cq = chunk_queries(ix, nq, extra);
+  // approximate-key buffer: a sub-chunk of queries x all isotropic rows (<= 4 GiB)
+  int64_t qs_max = 0;
+  size_t u_bytes = 0;
+  if (filt) {
+    qs_max = ((int64_t)1 << 30) / ix->ld_f / kFiltTile * kFiltTile;
+    qs_max = std::max<int64_t>(kFiltTile, std::min<int64_t>(qs_max, round_up(cq, kFiltTile)));
+    u_bytes = ((size_t)qs_max * ix->ld_f + 2048) * 4;
+  }
+  int64_t n_fallback = 0;
+  std::vector<int64_t> redo;
   int rc;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
     const int nqb = n_qblocks_for(nqc, kl);
-    const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
-    size_t need = chunk_bytes(ix, nq_pad) + 16 * 256;
+    const int slabs = n_slabs(nqb);
+    size_t need = chunk_bytes(ix, nq_pad) + 32 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
-                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12);
+                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12 + filt_q) + u_bytes;
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
@@ -567,11 +660,60 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
       float* oaux = b.take<float>((size_t)nq_pad * K);
       int* orow = b.take<int>((size_t)nq_pad * K);
       int nst = 0;
-      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s))) return rc;
+      int* okf = nullptr;
+      if (filt) {
+        // isotropic rows: MFMA filter -> K' candidates -> exact rerank into list slot 0;
+        // anisotropic rows: exact scan into slots 1..
+        uint16_t* Xb = b.take<uint16_t>((size_t)nq_pad * ix->DP);
+        float* xn2 = b.take<float>(nq_pad);
+        float* xn1 = b.take<float>(nq_pad);
+        float* cu = b.take<float>((size_t)nq_pad * Kp);
+        int* crow = b.take<int>((size_t)nq_pad * Kp);
+        okf = b.take<int>(nq_pad);
+        float* u = b.take<float>(u_bytes / 4);
+        HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DP, nq_pad, Xb, xn2, xn1, s));
+        GemmArgs g;
+        memset(&g, 0, sizeof(g));
+        g.DP = ix->DP;
+        g.nrows = ix->NL_iso;
+        g.ldu = ix->ld_f;
+        g.rn2 = ix->iso_n2;
+        g.rn1 = ix->iso_n1;
+        g.meta = ix->row_meta;
+        g.par = ix->row_par;
+        g.flags = ix->row_flags;
+        g.ldP = std::max(ix->NI, 1);
+        filter_consts(ix, g);
+        for (int64_t qs = 0; qs < nqc; qs += qs_max) {
+          const int nqs = (int)std::min<int64_t>(qs_max, nqc - qs);
+          g.nq = nqs;
+          g.n_qt = (nqs + kFiltTile - 1) / kFiltTile;
+          g.xn2 = xn2 + qs;
+          g.xn1 = xn1 + qs;
+          g.P = c.P ? c.P + qs * g.ldP : ix->dummy;
+          HIPCHK(launch_approx_gemm(Xb + qs * ix->DP, ix->iso_Mb, u, g, (int)(ix->ld_f / kFiltTile), s));
+          HIPCHK(launch_select(u, ix->ld_f, nqs, ix->NL_iso, Kp, cu + qs * Kp, crow + qs * Kp, s));
+        }
+        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
+          return rc;
+        HIPCHK(launch_rerank(c.X, ix->iso_Mf, ix->DP, nqc, Kp, K, cu, crow, ix->row_meta, ix->row_par,
+                             c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
+                             s));
+      } else {
+        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s)))
+          return rc;
+      }
       if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
       HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
       HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
                            scores ? scores + q0 * k : nullptr, s));
+      if (filt) {
+        std::vector<int> okh(nqc);
+        HIPCHK(hipMemcpyAsync(okh.data(), okf, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int i = 0; i < nqc; ++i)
+          if (!okh[i]) redo.push_back(q0 + i);
+      }
     } else {
       float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
       float* skey = b.take<float>((size_t)nq_pad * n_pow2);
@@ -587,18 +729,55 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
     if (ix->timing) {
       HIPCHK(hipEventRecord(ix->ev[3], s));
       HIPCHK(hipEventSynchronize(ix->ev[3]));
-      float a = 0, b = 0, c2 = 0, d = 0;
+      float a = 0, b2 = 0, c2 = 0, d = 0;
       HIPCHK(hipEventElapsedTime(&a, ix->ev[1], ix->ev[2]));
-      HIPCHK(hipEventElapsedTime(&b, ix->ev[0], ix->ev[1]));
+      HIPCHK(hipEventElapsedTime(&b2, ix->ev[0], ix->ev[1]));
       HIPCHK(hipEventElapsedTime(&c2, ix->ev[2], ix->ev[3]));
       HIPCHK(hipEventElapsedTime(&d, ix->ev[0], ix->ev[3]));
       ix->t_ms[0] += a;
-      ix->t_ms[1] += b;
+      ix->t_ms[1] += b2;
       ix->t_ms[2] += c2;
       ix->t_ms[3] += d;
-      ix->t_ms[4] += (ix->NL_iso > 0) + (ix->NL_an > 0);
+      ix->t_ms[4] += filt ? 1 : (ix->NL_iso > 0) + (ix->NL_an > 0);
     }
   }
+  if (!redo.empty()) {
+    n_fallback = (int64_t)redo.size();
+    if ((rc = rerun_exact(ix, q, redo, k, ids, scores, s))) return rc;
+  }
+  if (allow_filter) {
+    ix->stats[0] = filt ? nq : 0;
+    ix->stats[1] = n_fallback;
+    ix->stats[2] = filt ? 1 : 0;
+    ix->stats[3] = filt ? Kp : 0;
+  }
+  return CWQ_OK;
+}
+
+}  // namespace
+
+extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                              void* stream) {
+  if (!ix || (!q && nq > 0) || (!ids && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  for (float& t : ix->t_ms) t = 0.f;
+  for (int64_t& t : ix->stats) t = 0;
+  return score_topk_impl(ix, q, nq, k, ids, scores, (hipStream_t)stream, true);
+}
+
+extern "C" int cwq_set_filter(cwq_index* ix, int mode) {
+  if (!ix) return fail(CWQ_ERR_ARG, "NULL index");
+  if (mode < -1 || mode > 1) return fail(CWQ_ERR_ARG, "mode must be -1, 0 or 1");
+  ix->filter = mode;
+  return CWQ_OK;
+}
+
+extern "C" int cwq_last_stats(cwq_index* ix, int64_t* out) {
+  if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
+  for (int i = 0; i < 4; ++i) out[i] = ix->stats[i];
   return CWQ_OK;
 }
 

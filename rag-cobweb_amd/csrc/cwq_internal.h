@@ -122,4 +122,33 @@ hipError_t launch_simulate(const SimArgs& a, hipStream_t s);
 hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, const int64_t* gptr, int64_t n_groups,
                                  float* count, float* mean, float* meanSq, hipStream_t s);
 
+// bf16-MFMA candidate filter (cwq_mfma.hip)
+struct GemmArgs {
+  int DP, nq, nrows;
+  int n_qt;                     // query tiles of 128
+  int64_t ldu;                  // u row stride
+  const float* xn2;             // [nq] |x|^2
+  const float* xn1;             // [nq] |x|
+  const float* rn2;             // [rows] |mu|^2
+  const float* rn1;             // [rows] |mu|
+  const RowMeta* meta;
+  const int* par;
+  const int* flags;
+  const float* P;               // [nq][ldP] (launch-local query rows)
+  int64_t ldP;
+  float eta, eta_n, slack;      // error-bound constants (cwq_mfma.hip header)
+};
+constexpr int kFiltTile = 128;  // GEMM tile (queries and rows); operand arrays are padded to it
+constexpr int kFiltCand = 64;   // candidates per query (K')
+hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
+                            int64_t ld, float* Mf, void* Mb, float* n2, float* n1, hipStream_t s);
+hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DP, int64_t nq_pad, void* Xb,
+                             float* n2, float* n1, hipStream_t s);
+hipError_t launch_approx_gemm(const void* Xb, const void* Mb, float* u, const GemmArgs& a, int n_rt, hipStream_t s);
+hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
+hipError_t launch_rerank(const float* X, const float* Mf, int DP, int nq, int Kp, int K, const float* cu,
+                         const int* crow, const RowMeta* meta, const int* par, const float* P, int64_t ldP,
+                         int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag,
+                         hipStream_t s);
+
 }  // namespace cwq

@@ -84,6 +84,17 @@ class CobwebIndex:
         return {"leaf_scan_ms": float(out[0]), "internal_ms": float(out[1]), "merge_ms": float(out[2]),
                 "call_ms": float(out[3]), "leaf_scan_launches": int(out[4])}
 
+    def set_filter(self, mode):
+        """Isotropic-row strategy of score_topk: -1 automatic, 0 exact fp32 scan,
+        1 bf16-MFMA candidate filter + exact rerank (k <= 32).  Results are identical."""
+        check(lib().cwq_set_filter(self._h, int(mode)))
+
+    def last_stats(self):
+        out = np.zeros(4, np.int64)
+        check(lib().cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"filter_queries": int(out[0]), "fallback_queries": int(out[1]), "filter_used": bool(out[2]),
+                "candidates": int(out[3])}
+
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
             lib().cwq_index_destroy(self._h)

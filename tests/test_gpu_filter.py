@@ -1,0 +1,129 @@
+"""bf16-MFMA candidate filter + exact rerank (cwq_mfma.hip): the filter changes how
+the isotropic rows are searched, never the answer.  Every case compares the filter
+(cwq_set_filter 1) with the exact fp32 scan (mode 0): ids AND scores bit-identical,
+plus the reference goldens through the filter, mixed isotropic/anisotropic rows,
+boundary ties that defeat the certificate (exact fallback), and data with a large
+common offset or scale."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from test_gpu_parity import HIER, index_from_golden, rel_err, topk_equiv, RTOL
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg
+
+
+def flat_index(pkg, X):
+    fs = pkg.synth.flat_synth(X)
+    return pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device="cuda:0")
+
+
+def both(ix, Q, k):
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, k)
+    assert not ix.last_stats()["filter_used"]
+    ix.set_filter(1)
+    ids1, s1 = ix.score_topk(Q, k)
+    st = ix.last_stats()
+    ix.set_filter(-1)
+    return ids0.cpu(), s0.cpu(), ids1.cpu(), s1.cpu(), st
+
+
+@pytest.mark.parametrize("N,D,k", [(20000, 96, 10), (30000, 768, 10), (5000, 64, 1), (5000, 64, 32),
+                                   (1000, 32, 16), (100, 32, 10), (40, 32, 32), (3000, 200, 7)])
+def test_filter_equals_exact_scan(gpu, N, D, k):
+    X = gpu.synth.synthetic_corpus(N, D, seed=N + D)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=k)
+    ids0, s0, ids1, s1, st = both(ix, Q, k)
+    assert st["filter_used"] and st["filter_queries"] == 300
+    assert torch.equal(ids0, ids1)
+    assert torch.equal(s0, s1)
+    assert st["fallback_queries"] <= 15, st
+
+
+@pytest.mark.parametrize("name", HIER)
+def test_goldens_through_filter(gpu, name):
+    g = load_golden(name)
+    ix = index_from_golden(gpu, g)
+    ix.set_filter(1)
+    k = int(g["k"])
+    ids, scores = ix.score_topk(g["Xq"], k)
+    assert ix.last_stats()["filter_used"]
+    ids, scores = ids.cpu().numpy(), scores.cpu().numpy()
+    for qi in range(len(g["Xq"])):
+        ref = g["rank_scores"][qi].astype(np.float64)
+        topk_equiv(ids[qi], g["fast_ids"][qi], ref)
+        assert rel_err(scores[qi], ref[ids[qi]]) < RTOL
+
+
+def test_mixed_iso_aniso_rows(gpu):
+    """Leaves with per-dimension variances (count >= 2 leaves) go through the exact
+    scan and are merged with the filtered isotropic rows."""
+    X = gpu.synth.synthetic_corpus(6000, 64, seed=3)
+    fs = gpu.synth.flat_synth(X)
+    var = fs["var"].clone()
+    g = torch.Generator(device=X.device)
+    g.manual_seed(5)
+    an = torch.randperm(6000, generator=g, device=X.device)[:700] + 1
+    var[an] = var[an] * (0.5 + torch.rand((700, 64), generator=g, device=X.device))
+    ix = gpu.index.CobwebIndex(fs["mean"], var, fs["parent"], fs["node_of_sentence"], device="cuda:0")
+    assert ix.info["isotropic_rows"] == 5300
+    Q, _ = gpu.synth.synthetic_queries(X, 200, seed=9)
+    for k in (5, 20):
+        ids0, s0, ids1, s1, st = both(ix, Q, k)
+        assert st["filter_used"]
+        assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
+def test_boundary_ties_fall_back(gpu):
+    """200 identical leaves around every query: the top-k boundary is a tie wider
+    than K' = 64, the certificate cannot hold and every query is re-run exactly."""
+    X = gpu.synth.synthetic_corpus(5000, 48, seed=11)
+    X[1000:1200] = X[1000]
+    ix = flat_index(gpu, X)
+    Q = X[1000].repeat(50, 1) + 0.01 * gpu.synth.synthetic_corpus(50, 48, seed=12)
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert st["fallback_queries"] == 50, st
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
+@pytest.mark.parametrize("shift,scale", [(50.0, 1.0), (0.0, 100.0), (0.0, 0.01), (-3.0, 7.0)])
+def test_offset_and_scale(gpu, shift, scale):
+    X = gpu.synth.synthetic_corpus(8000, 128, seed=21) * scale + shift
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, 200, seed=22, sigma=0.1 * scale)
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    assert st["fallback_queries"] <= 10, st
+
+
+def test_hierarchical_two_level(gpu):
+    X = gpu.synth.synthetic_corpus(12000, 96, seed=31)
+    g = torch.Generator(device=X.device)
+    g.manual_seed(32)
+    labels = torch.randint(0, 40, (12000,), generator=g, device=X.device)
+    ts = gpu.synth.two_level_synth(X, labels)
+    ix = gpu.index.CobwebIndex(ts["mean"], ts["var"], ts["parent"], ts["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 256, seed=33)
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert st["filter_used"]
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
+def test_auto_mode_threshold(gpu):
+    X = gpu.synth.synthetic_corpus(20000, 32, seed=41)
+    ix = flat_index(gpu, X)
+    Q = X[:8].contiguous()
+    ix.score_topk(Q, 10)
+    assert ix.last_stats()["filter_used"]          # >= 16384 iso rows, k <= 32
+    ix.score_topk(Q, 40)
+    assert not ix.last_stats()["filter_used"]      # k > 32: exact scan
