@@ -136,14 +136,15 @@ int cwq_last_timing(cwq_index* idx, float* out5);
  * Isotropic-row strategy of cwq_score_topk (no reference counterpart: an execution
  * choice; results are identical either way).
  *   mode -1: automatic (default; env CWQ_FILTER=0/1 overrides): the bf16-MFMA
- *            candidate filter + exact rerank when k <= 32 and the index holds
+ *            candidate filter + exact rerank when k <= 64 and the index holds
  *            >= 16384 isotropic rows, the exact fp32 scan otherwise
- *   mode  0: always the exact fp32 scan      mode 1: the filter whenever k <= 32
- * cwq_last_stats(out4): [queries served by the filter, of which re-run by the exact
- * scan because their certificate failed, filter used (0/1), candidates per query].
+ *   mode  0: always the exact fp32 scan      mode 1: the filter whenever k <= 64
+ * cwq_last_stats(out6): [queries served by the filter, of which re-run by the exact
+ * scan (candidate list overflow / no threshold), filter used (0/1), mean candidate
+ * records per query, mean exact reranks per query, threshold-sample rows].
  */
 int cwq_set_filter(cwq_index* idx, int mode);
-int cwq_last_stats(cwq_index* idx, int64_t* out4);
+int cwq_last_stats(cwq_index* idx, int64_t* out6);
 
 /*
  * Sequential Welford statistics of row groups (synthetic-tree builder).

@@ -96,11 +96,18 @@ struct cwq_index {
   int* node_src = nullptr;
   float* dummy = nullptr;
   // bf16-MFMA filter operands for the isotropic rows (cwq_mfma.hip): row-major
-  // fp32 (exact rerank) and bf16 (GEMM) copies padded to whole 128-row tiles, norms
+  // fp32 (exact rerank, DP wide) and bf16 hi-part (GEMM, DPB wide) copies padded to
+  // whole 256-row tiles, per-row / per-tile bound constants, the threshold sample
   int64_t ld_f = 0;
-  float *iso_Mf = nullptr, *iso_n2 = nullptr, *iso_n1 = nullptr, *iso_c = nullptr;   // iso_c: centre [D]
+  int DPB = 0;
+  float *iso_Mf = nullptr, *iso_c = nullptr;   // iso_c: centre [D] (root mean)
   uint16_t* iso_Mb = nullptr;
-  int64_t stats[4] = {0, 0, 0, 0};   // cwq_last_stats
+  RowF* iso_rf = nullptr;
+  TileF* iso_tf = nullptr;
+  int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
+  int* samp_rows = nullptr;
+  uint16_t* iso_Sb = nullptr;
+  int64_t stats[6] = {0, 0, 0, 0, 0, 0};   // cwq_last_stats
   // timing (cwq_set_timing)
   bool timing = false;
   int filter = -1;   // cwq_set_filter
@@ -148,6 +155,125 @@ struct cwq_index {
 
 extern "C" int cwq_version(void) { return 100; }
 extern "C" const char* cwq_last_error(void) { return g_err.c_str(); }
+
+namespace {
+
+// Error-bound constants of the filter (cwq_mfma.hip header): fp32 accumulation of the
+// MFMA products (2x the textbook (n-1)u, n = DPB + 64), norm/centring rounding, and the
+// relative slack that covers the fp32 evaluation of both the bounds and the exact keys.
+struct FiltConsts {
+  double gamma, eps_n, slack;
+};
+FiltConsts filt_consts(int DPB) {
+  return {(DPB + 64) * std::ldexp(1.0, -23), std::ldexp(1.0, -20), std::ldexp(1.0, -16)};
+}
+
+float round_up_f(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+// bf16 operands, fp32 rerank copy, per-row and per-tile bound constants, and the
+// strided threshold sample of the isotropic rows.
+int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const std::vector<RowMeta>& meta,
+                 const std::vector<int>& row_par, const std::vector<int>& row_flags, hipStream_t s) {
+  int rc;
+  const int DP = ix->DP, D = ix->D, NLi = ix->NL_iso;
+  ix->DPB = (int)round_up(D, 64);
+  const int DPB = ix->DPB;
+  ix->ld_f = round_up(NLi, kFgTile);
+  const int64_t ld = ix->ld_f;
+  float *n2 = nullptr, *nlo = nullptr, *nhi = nullptr;
+  if ((rc = ix->alloc(&ix->iso_Mf, (size_t)DP * ld))) return rc;
+  if ((rc = ix->alloc(&ix->iso_Mb, (size_t)DPB * ld))) return rc;
+  if ((rc = ix->alloc(&n2, ld))) return rc;
+  if ((rc = ix->alloc(&nlo, ld))) return rc;
+  if ((rc = ix->alloc(&nhi, ld))) return rc;
+  if ((rc = ix->alloc(&ix->iso_c, D))) return rc;
+  HIPCHK(hipMemcpyAsync(ix->iso_c, mean, (size_t)D * 4, hipMemcpyDeviceToDevice, s));   // root mean
+  HIPCHK(launch_rows_prep(mean, D, d_rows, NLi, ix->iso_c, DP, DPB, ld, ix->iso_Mf, ix->iso_Mb, n2, nlo, nhi, s));
+  std::vector<float> hn2(ld), hlo(ld), hhi(ld);
+  HIPCHK(hipMemcpyAsync(hn2.data(), n2, ld * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hlo.data(), nlo, ld * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hhi.data(), nhi, ld * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const FiltConsts fc = filt_consts(DPB);
+  std::vector<RowF> rf(ld);
+  std::vector<double> gr(ld, 0.0);
+  for (int64_t r = 0; r < ld; ++r) {
+    RowF& f = rf[r];
+    const bool usable = r < NLi && (row_flags[r] & FLAG_HAS_SENT);
+    if (!usable) {
+      f = RowF{-INFINITY, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+      continue;
+    }
+    const RowMeta& m = meta[r];
+    const double hs = -0.5 * (double)m.cw * (double)m.iv, hl = -0.5 * (double)m.cw * (double)m.logdet;
+    const double g = (double)m.cw * (double)m.iv;
+    f.beta = round_up_f((double)hlo[r] + fc.gamma * (double)hhi[r]);
+    f.delta = round_up_f((double)hhi[r] + (double)hlo[r]);
+    f.rn2 = hn2[r];
+    f.hs = (float)hs;
+    f.hl = (float)hl;
+    f.invL = m.invL;
+    f.par = row_par[r];
+    gr[r] = g;
+    if (g > 0.0 && std::isfinite(g) && std::isfinite(hl)) {
+      const double rn2 = hn2[r];
+      double R = hl / g - 0.5 * rn2 + 0.5 * fc.eps_n * rn2 + fc.slack * (std::fabs(hl) / g + 1.5 * rn2);
+      R += 4.0 * fc.gamma * (std::fabs(R) + std::fabs(hl) / g + rn2);
+      f.R0 = round_up_f(R);
+    } else {
+      f.R0 = 0.f;   // only ever on non-uniform tiles
+    }
+  }
+  const int n_rt = (int)(ld / kFgTile);
+  std::vector<TileF> tf(n_rt);
+  for (int t = 0; t < n_rt; ++t) {
+    TileF& T = tf[t];
+    T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, 0.f, 0.f};
+    bool first = true;
+    for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
+      if (rf[r].par < -1) continue;
+      const double g = gr[r];
+      if (!(g > 0.0) || !std::isfinite(g) || !std::isfinite(rf[r].R0)) T.uniform = 0;
+      if (first) {
+        T.par = rf[r].par;
+        T.invL = rf[r].invL;
+        T.g = (float)g;
+        first = false;
+      } else if (rf[r].par != T.par || rf[r].invL != T.invL || (float)g != T.g) {
+        T.uniform = 0;
+      }
+      T.beta_max = std::max(T.beta_max, rf[r].beta);
+      T.delta_max = std::max(T.delta_max, rf[r].delta);
+    }
+  }
+  if ((rc = ix->upload(&ix->iso_rf, rf, s))) return rc;
+  if ((rc = ix->upload(&ix->iso_tf, tf, s))) return rc;
+  // threshold sample: ~NL_iso/32 rows at a fixed stride, 256 <= S <= 32768
+  int S = (int)std::min<int64_t>(32768, std::max<int64_t>(kFgTile, NLi / 32 / kFgTile * kFgTile));
+  const int stride = std::max(1, NLi / S);
+  std::vector<int> srow(round_up(S, kFgTile), -1);
+  int ns = 0;
+  for (int j = 0; j < S; ++j) {
+    const int64_t r = (int64_t)j * stride;
+    if (r < NLi) {
+      srow[j] = (int)r;
+      ns = j + 1;
+    }
+  }
+  ix->n_samp = ns;
+  ix->ld_s = (int)srow.size();
+  if ((rc = ix->upload(&ix->samp_rows, srow, s))) return rc;
+  if ((rc = ix->alloc(&ix->iso_Sb, (size_t)DPB * ix->ld_s))) return rc;
+  HIPCHK(launch_gather_bf16_rows(ix->iso_Mb, DPB, ix->samp_rows, ix->ld_s, ix->iso_Sb, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return CWQ_OK;
+}
+
+}  // namespace
 
 extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var,
                                 const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
@@ -304,18 +430,6 @@ extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const 
   HIPCHK(launch_gather_T(mean, var, dim, d_rows, ix->NL_iso, 0, ix->iso_M, ix->ld_iso, DP, s));
   HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 1, ix->an_A, ix->ld_an, DP, s));
   HIPCHK(launch_gather_T(mean, var, dim, d_rows + ix->NL_iso, ix->NL_an, 2, ix->an_B, ix->ld_an, DP, s));
-  if (ix->NL_iso > 0) {
-    ix->ld_f = round_up(ix->NL_iso, kFiltTile);
-    if ((rc = ix->alloc(&ix->iso_Mf, (size_t)DP * ix->ld_f))) return rc;
-    if ((rc = ix->alloc(&ix->iso_Mb, (size_t)DP * ix->ld_f))) return rc;
-    if ((rc = ix->alloc(&ix->iso_n2, ix->ld_f))) return rc;
-    if ((rc = ix->alloc(&ix->iso_n1, ix->ld_f))) return rc;
-    if ((rc = ix->alloc(&ix->iso_c, dim))) return rc;
-    HIPCHK(hipMemcpyAsync(ix->iso_c, mean, (size_t)dim * 4, hipMemcpyDeviceToDevice, s));   // root mean
-    HIPCHK(launch_rows_prep(mean, dim, d_rows, ix->NL_iso, ix->iso_c, DP, ix->ld_f, ix->iso_Mf, ix->iso_Mb,
-                            ix->iso_n2, ix->iso_n1, s));
-  }
-
   if ((rc = ix->alloc(&ix->logdet_int, ix->NI))) return rc;
   if ((rc = ix->alloc(&ix->logdet_row, ix->NL))) return rc;
   HIPCHK(launch_logdet(var, dim, d_int_nodes, ix->NI, ix->logdet_int, s));
@@ -335,6 +449,7 @@ extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const 
     meta[r].iv = ivh[r];
   }
   if ((rc = ix->upload(&ix->row_meta, meta, s))) return rc;
+  if (ix->NL_iso > 0 && (rc = build_filter(ix.get(), mean, d_rows, meta, row_par, row_flags, s))) return rc;
   if ((rc = ix->upload(&ix->row_par, row_par, s))) return rc;
   if ((rc = ix->upload(&ix->row_flags, row_flags, s))) return rc;
   if ((rc = ix->upload(&ix->row_bfs, row_bfs, s))) return rc;
@@ -539,7 +654,7 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
 // Query-chunk size that keeps the per-chunk workspace within ~2 GiB (min 128).
 int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
   const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
-  const size_t budget = (size_t)2 << 30;
+  const size_t budget = (size_t)8 << 30;
   int64_t c = (int64_t)std::max<size_t>(kQPad, budget / std::max<size_t>(per_q, 1));
   c = std::max<int64_t>(kQPad, c / kQPad * kQPad);
   return std::min(nq, c);
@@ -550,7 +665,9 @@ int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
 namespace {
 
 constexpr int kFiltMinRows = 16384;   // automatic mode: below this the exact scan is as fast
-constexpr int kFiltMaxK = 32;         // the certificate needs K' = 64 >= 2k candidates
+constexpr int kFiltMaxK = 64;         // the filter serves the list-based top-k path (k <= 64)
+constexpr int kFgRecPerQ = 1024;      // candidate-record slots per query (append buffer)
+constexpr int kFgDirPerQ = 1024;      // direct-record slots per query (tiles past kFgCap)
 
 bool use_filter(const cwq_index* ix, int k) {
   if (k > kFiltMaxK || ix->NL_iso == 0 || !ix->iso_Mb) return false;
@@ -563,13 +680,11 @@ bool use_filter(const cwq_index* ix, int k) {
   return mode == 1;
 }
 
-// Error-bound constants of the approximate keys (cwq_mfma.hip header): bf16 rounding
-// of both operands (2 * 2^-8 + 2^-16) plus fp32 accumulation over DP terms, each
-// small term doubled for margin.
-void filter_consts(const cwq_index* ix, GemmArgs& g) {
-  g.eta = (float)(std::ldexp(1.0, -7) + std::ldexp(1.0, -15) + (ix->DP + 64) * std::ldexp(1.0, -23));
-  g.eta_n = (float)std::ldexp(1.0, -20);
-  g.slack = (float)std::ldexp(1.0, -16);
+// fgemm launch geometry: query groups over the 8 XCDs (each keeps its query panel in
+// L2), row groups for the remaining factor.
+void fg_groups(int n_qt, int& qg, int& rg) {
+  qg = n_qt >= 8 ? 8 : n_qt >= 4 ? 4 : n_qt >= 2 ? 2 : 1;
+  rg = 8 / qg;
 }
 
 int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
@@ -613,7 +728,6 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const bool filt = !general && allow_filter && use_filter(ix, k);
   const int kl = k <= 16 ? 16 : 64;
   const int K = std::min<int>(k, 64);
-  const int Kp = kFiltCand;
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));
   // partial-list entries per query (upper bound over both segments; one list for the filter)
   const int nqb_est = n_qblocks_for(nq, kl);
@@ -621,19 +735,17 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     return filt ? 1 + (pick_nslab(ix, ix->NL_an, nqb) + 1) * scan_lists_per_slab(kl)
                 : (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
   };
-  const size_t filt_q = filt ? (size_t)ix->DP * 2 + 8 + (size_t)Kp * 8 + 4 + 4 * 256 : 0;
+  const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
+  const int n_rts = filt ? ix->ld_s / kFgTile : 0;
+  // per query: bf16 query, info, sample bounds, threshold list, candidate lists, flags, records
+  const size_t filt_q = filt ? (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
+                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64
+                             : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
-  const int64_t cq = chunk_queries(ix, nq, extra);
-  // approximate-key buffer: a sub-chunk of queries x all isotropic rows (<= 4 GiB)
-  int64_t qs_max = 0;
-  size_t u_bytes = 0;
-  if (filt) {
-    qs_max = ((int64_t)1 << 30) / ix->ld_f / kFiltTile * kFiltTile;
-    qs_max = std::max<int64_t>(kFiltTile, std::min<int64_t>(qs_max, round_up(cq, kFiltTile)));
-    u_bytes = ((size_t)qs_max * ix->ld_f + 2048) * 4;
-  }
-  int64_t n_fallback = 0;
+  int64_t cq = chunk_queries(ix, nq, extra);
+  if (filt && cq < nq) cq = std::max<int64_t>(kFgTile, cq / kFgTile * kFgTile);   // whole query tiles
+  int64_t n_fallback = 0, cand_sum = 0, exact_sum = 0;
   std::vector<int64_t> redo;
   int rc;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
@@ -641,9 +753,10 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     const int64_t nq_pad = round_up(nqc, kQPad);
     const int nqb = n_qblocks_for(nqc, kl);
     const int slabs = n_slabs(nqb);
-    size_t need = chunk_bytes(ix, nq_pad) + 32 * 256;
+    const int64_t nqf = round_up(nqc, kFgTile);
+    size_t need = chunk_bytes(ix, nq_pad) + 64 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
-                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12 + filt_q) + u_bytes;
+                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) + (size_t)nqf * filt_q + 4096 * 4;
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
@@ -661,44 +774,81 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       int* orow = b.take<int>((size_t)nq_pad * K);
       int nst = 0;
       int* okf = nullptr;
+      int *qcnt_d = nullptr, *nex_d = nullptr;
       if (filt) {
-        // isotropic rows: MFMA filter -> K' candidates -> exact rerank into list slot 0;
-        // anisotropic rows: exact scan into slots 1..
-        uint16_t* Xb = b.take<uint16_t>((size_t)nq_pad * ix->DP);
-        float* xn2 = b.take<float>(nq_pad);
-        float* xn1 = b.take<float>(nq_pad);
-        float* cu = b.take<float>((size_t)nq_pad * Kp);
-        int* crow = b.take<int>((size_t)nq_pad * Kp);
-        okf = b.take<int>(nq_pad);
-        float* u = b.take<float>(u_bytes / 4);
-        HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DP, nq_pad, Xb, xn2, xn1, s));
-        GemmArgs g;
+        // isotropic rows: sample bounds -> thresholds -> MFMA filter -> candidates ->
+        // exact rerank into list slot 0; anisotropic rows: exact scan into slots 1..
+        const FiltConsts fc = filt_consts(ix->DPB);
+        const int n_qt = (int)(nqf / kFgTile);
+        uint16_t* Xb = b.take<uint16_t>((size_t)nqf * ix->DPB);
+        float4* qinfo = b.take<float4>(nqf);
+        float* lb = b.take<float>((size_t)nqf * ix->ld_s + 4096);
+        float* tl = b.take<float>((size_t)nqf * 64);
+        int* tr = b.take<int>((size_t)nqf * 64);
+        int* qcnt = b.take<int>(nqf);
+        int* qover = b.take<int>(nqf);
+        okf = b.take<int>(nqf);
+        int* nex = b.take<int>(nqf);
+        int* crow = b.take<int>((size_t)nqf * kFgCapQ);
+        float* cu = b.take<float>((size_t)nqf * kFgCapQ);
+        float* cl = b.take<float>((size_t)nqf * kFgCapQ);
+        const int64_t rec_cap = round_up((int64_t)nqf * kFgRecPerQ, kFgChunk);
+        int4* rec = b.take<int4>((size_t)rec_cap);
+        int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
+        int* gctr = b.take<int>(64);
+        const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
+        int4* rec_dir = b.take<int4>((size_t)dir_cap);
+        HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
+        FgArgs g;
         memset(&g, 0, sizeof(g));
-        g.DP = ix->DP;
-        g.nrows = ix->NL_iso;
-        g.ldu = ix->ld_f;
-        g.rn2 = ix->iso_n2;
-        g.rn1 = ix->iso_n1;
-        g.meta = ix->row_meta;
-        g.par = ix->row_par;
-        g.flags = ix->row_flags;
+        g.DPB = ix->DPB;
+        g.nq = nqc;
+        g.n_qt = n_qt;
+        fg_groups(n_qt, g.qgroups, g.rgroups);
+        g.qinfo = qinfo;
+        g.rf = ix->iso_rf;
+        g.tf = ix->iso_tf;
+        g.P = c.P ? c.P : ix->dummy;
         g.ldP = std::max(ix->NI, 1);
-        filter_consts(ix, g);
-        for (int64_t qs = 0; qs < nqc; qs += qs_max) {
-          const int nqs = (int)std::min<int64_t>(qs_max, nqc - qs);
-          g.nq = nqs;
-          g.n_qt = (nqs + kFiltTile - 1) / kFiltTile;
-          g.xn2 = xn2 + qs;
-          g.xn1 = xn1 + qs;
-          g.P = c.P ? c.P + qs * g.ldP : ix->dummy;
-          HIPCHK(launch_approx_gemm(Xb + qs * ix->DP, ix->iso_Mb, u, g, (int)(ix->ld_f / kFiltTile), s));
-          HIPCHK(launch_select(u, ix->ld_f, nqs, ix->NL_iso, Kp, cu + qs * Kp, crow + qs * Kp, s));
-        }
+        g.gamma = (float)fc.gamma;
+        g.eps_n = (float)fc.eps_n;
+        g.slack = (float)fc.slack;
+        // 1. sample pass -> T[q] = K-th largest lower bound over the sample rows
+        g.mode = 1;
+        g.n_rt = n_rts;
+        g.nrows = ix->ld_s;
+        g.rowmap = ix->samp_rows;
+        g.lb = lb;
+        g.ldlb = ix->ld_s;
+        HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
+        HIPCHK(launch_select(lb, ix->ld_s, nqc, ix->ld_s, K, tl, tr, s));
+        // 2. filter pass -> per-tile candidate records
+        g.mode = 0;
+        g.n_rt = n_rt;
+        g.nrows = ix->NL_iso;
+        g.rowmap = nullptr;
+        g.T = tl + (K - 1);
+        g.ldT = 64;
+        g.rec = rec;
+        g.rec_cap = rec_cap;
+        g.gctr = gctr;
+        g.chunk_fill = chunk_fill;
+        g.qover = qover;
+        g.rec_dir = rec_dir;
+        g.dir_cap = dir_cap;
+        HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)nqf * 4, s));
+        HIPCHK(hipMemsetAsync(qover, 0, (size_t)nqf * 4, s));
+        HIPCHK(hipMemsetAsync(gctr, 0, 8, s));
+        HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
+        // 3. per-query candidate lists, 4. exact rerank
+        HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl, s));
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;
-        HIPCHK(launch_rerank(c.X, ix->iso_Mf, ix->DP, nqc, Kp, K, cu, crow, ix->row_meta, ix->row_par,
-                             c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
-                             s));
+        HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
+                            ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow,
+                            (int64_t)nst * K, okf, nex, s));
+        qcnt_d = qcnt;
+        nex_d = nex;
       } else {
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s)))
           return rc;
@@ -708,11 +858,16 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
                            scores ? scores + q0 * k : nullptr, s));
       if (filt) {
-        std::vector<int> okh(nqc);
+        std::vector<int> okh(nqc), cnth(nqc), nexh(nqc);
         HIPCHK(hipMemcpyAsync(okh.data(), okf, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(cnth.data(), qcnt_d, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(nexh.data(), nex_d, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        for (int i = 0; i < nqc; ++i)
+        for (int i = 0; i < nqc; ++i) {
           if (!okh[i]) redo.push_back(q0 + i);
+          cand_sum += cnth[i];
+          exact_sum += nexh[i];
+        }
       }
     } else {
       float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
@@ -749,7 +904,9 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     ix->stats[0] = filt ? nq : 0;
     ix->stats[1] = n_fallback;
     ix->stats[2] = filt ? 1 : 0;
-    ix->stats[3] = filt ? Kp : 0;
+    ix->stats[3] = filt && nq > 0 ? (cand_sum + nq / 2) / nq : 0;
+    ix->stats[4] = filt && nq > 0 ? (exact_sum + nq / 2) / nq : 0;
+    ix->stats[5] = filt ? ix->n_samp : 0;
   }
   return CWQ_OK;
 }
@@ -777,7 +934,7 @@ extern "C" int cwq_set_filter(cwq_index* ix, int mode) {
 
 extern "C" int cwq_last_stats(cwq_index* ix, int64_t* out) {
   if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
-  for (int i = 0; i < 4; ++i) out[i] = ix->stats[i];
+  for (int i = 0; i < 6; ++i) out[i] = ix->stats[i];
   return CWQ_OK;
 }
 

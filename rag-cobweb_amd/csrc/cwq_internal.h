@@ -123,32 +123,67 @@ hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, co
                                  float* count, float* mean, float* meanSq, hipStream_t s);
 
 // bf16-MFMA candidate filter (cwq_mfma.hip)
-struct GemmArgs {
-  int DP, nq, nrows;
-  int n_qt;                     // query tiles of 128
-  int64_t ldu;                  // u row stride
-  const float* xn2;             // [nq] |x|^2
-  const float* xn1;             // [nq] |x|
-  const float* rn2;             // [rows] |mu|^2
-  const float* rn1;             // [rows] |mu|
-  const RowMeta* meta;
-  const int* par;
-  const int* flags;
-  const float* P;               // [nq][ldP] (launch-local query rows)
-  int64_t ldP;
-  float eta, eta_n, slack;      // error-bound constants (cwq_mfma.hip header)
+constexpr int kFgTile = 256;      // fgemm tile edge (queries and rows); operands are padded to it
+constexpr int kFgCap = 512;       // candidate records per tile (LDS staging)
+constexpr int kFgChunk = 2048;    // record slots a workgroup claims at a time
+constexpr int kFgCapQ = 4096;     // candidate records per query
+
+// Per filter row (isotropic leaf-class row) constants, 32 B.
+struct RowF {
+  float R0;      // pretest row term on uniform tiles (-inf: never a candidate)
+  float beta;    // |mu_lo| + gamma |mu_hi|
+  float delta;   // |mu_hi| + |mu_lo|
+  float rn2;     // |mu - c|^2
+  float hs;      // -cw*iv/2
+  float hl;      // -cw*logdet/2
+  float invL;    // 1/path length
+  int par;       // internal id of the parent (-1: none), -2: unusable row (no sentence / padding)
 };
-constexpr int kFiltTile = 128;  // GEMM tile (queries and rows); operand arrays are padded to it
-constexpr int kFiltCand = 64;   // candidates per query (K')
+// Per row tile: "uniform" when every usable row shares parent, path length and g = cw*iv > 0.
+struct TileF {
+  int uniform;
+  int par;
+  float invL;
+  float g;
+  float beta_max, delta_max;
+  float pad0, pad1;
+};
+struct FgArgs {
+  int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
+  int qgroups, rgroups;                   // XCD split (qgroups * rgroups == 8)
+  const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
+  const float* T;                         // thresholds, T[q * ldT]
+  int64_t ldT;
+  const RowF* rf;
+  const TileF* tf;
+  const int* rowmap;                      // sample pass: operand row -> filter row (-1 pad)
+  const float* P;                         // [nq][ldP] path prefixes of internal nodes
+  int64_t ldP;
+  float gamma, eps_n, slack;              // error-bound constants (cwq_mfma.hip header)
+  float* lb;                              // sample: [nq_pad][ldlb]
+  int64_t ldlb;
+  int4* rec;                              // filter: appended records {q, row, u, l}
+  int64_t rec_cap;                        // record slots (a multiple of kFgChunk)
+  int* gctr;                              // [0] chunks claimed, [1] direct records (zeroed before the launch)
+  int4* rec_dir;                          // direct records (a tile with more than kFgCap)
+  int dir_cap;
+  int* chunk_fill;                        // valid records per claimed chunk
+  int* qover;                             // queries whose records were lost (re-run exactly)
+};
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
-                            int64_t ld, float* Mf, void* Mb, float* n2, float* n1, hipStream_t s);
-hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DP, int64_t nq_pad, void* Xb,
-                             float* n2, float* n1, hipStream_t s);
-hipError_t launch_approx_gemm(const void* Xb, const void* Mb, float* u, const GemmArgs& a, int n_rt, hipStream_t s);
+                            int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,
+                            hipStream_t s);
+hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int64_t n, void* Sb, hipStream_t s);
+hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
+                             float4* qinfo, hipStream_t s);
+hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s);
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
-hipError_t launch_rerank(const float* X, const float* Mf, int DP, int nq, int Kp, int K, const float* cu,
-                         const int* crow, const RowMeta* meta, const int* par, const float* P, int64_t ldP,
-                         int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag,
-                         hipStream_t s);
+hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
+                         int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
+hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
+                        const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
+                        int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
+                        float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
+                        hipStream_t s);
 
 }  // namespace cwq

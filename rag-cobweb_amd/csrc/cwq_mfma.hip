@@ -1,22 +1,37 @@
 // libcwq: bf16-MFMA candidate filter + exact fp32 rerank for isotropic rows
-// ("Cobweb Fast", A6).  Results are EXACT (identical keys to the fp32 scan):
+// ("Cobweb Fast", A6; CobwebWrapper.py:210-265).  Results are EXACT: the final
+// keys are the scan kernel's fp32 arithmetic, op for op.
 //
-//   1. approx_gemm: S~ = |x|^2 + |mu|^2 - 2 x.mu with x.mu on v_mfma_f32_32x32x16_bf16
-//      (bf16 operands, fp32 accumulate); writes an UPPER BOUND of every key,
-//        u = key~ + e(q, r),   e = 0.5*cw*iv*(2*eta*|x||mu| + ...)    (see bound_slack)
-//      since |x.mu - (x.mu)~| <= eta * sum_d |x_d mu_d| <= eta |x| |mu| (Cauchy-Schwarz),
-//      eta = 2*2^-8 + 2^-16 + D*2^-24 (bf16 rounding of both operands + fp32 sums);
-//   2. select: per query the K' = 64 rows with the largest u;
-//   3. rerank: exact fp32 keys of those rows, op for op the scan kernel's (so the
-//      keys are bit-identical), top-k, and the certificate u_(K') < tau_k: every row
-//      outside the set has key <= u <= u_(K') < tau_k.  Queries without the
-//      certificate are flagged and re-run by the exact scan.
+// Key of an isotropic row r for query x:
+//   key = pi + hl + hs * S,   S = |x - mu|^2 = |x'|^2 + |mu'|^2 - 2 x'.mu'
+//   (x' = x - c, mu' = mu - c, c = root mean; pi = P[q][parent] / L; hs = -cw*iv/2 < 0,
+//   hl = -cw*logdet/2).  The bf16 MFMA computes x_hi.mu_hi (x_hi = bf16(x'),
+//   x_lo = x' - x_hi exactly, same for mu); since
+//     x'.mu' - x_hi.mu_hi = x_hi.mu_lo + x_lo.mu_hi + x_lo.mu_lo,
+//   |error| <= a*b + c*d + c*b  (a=|x_hi|, c=|x_lo|, d=|mu_hi|, b=|mu_lo|, Cauchy-Schwarz),
+//   plus fp32 accumulation gamma*a*d.  That gives rigorous bounds l <= key_fp32 <= u.
 //
-// CDNA4 mapping of the GEMM: 256-thread workgroups, 128 queries x 128 rows per
-// workgroup, 2x2 waves each owning 64x64 = 2x2 tiles of 32x32 (four 16-register
-// accumulators), K staged 32 deep through LDS (double buffer, 80-B padded rows:
-// conflict-free ds_read_b128 fragment reads), queries fastest in the grid so the
-// co-running workgroups share each row tile in L2.
+// Pipeline per query chunk:
+//   1. sample pass: fgemm over a strided sample of S rows, dense lower bounds l;
+//      T[q] = k-th largest l  (<= the true k-th key: those k rows have key >= l);
+//   2. filter pass: fgemm over all rows; each (q, r) with u >= T[q] is a candidate
+//      (every true top-k row has u >= key >= tau_k >= T).  The epilogue does NOT
+//      materialise u: the accumulator starts at R_r - Qv_q so that acc >= 0 is a
+//      conservative pretest of u >= T (2 VALU/element, no stores); survivors get the
+//      rigorous u/l and go to a per-tile record list (LDS, then one coalesced flush);
+//   3. bucket: records -> per-query candidate lists;
+//   4. final (one wave per query): T2 = k-th largest l among the candidates
+//      (<= tau_k), exact fp32 keys of the candidates with u >= T2, exact top-k.
+//   Queries whose lists overflow (or have no usable threshold) are flagged and re-run
+//   by the exact scan, so the result never depends on the filter's statistics.
+//
+// CDNA4 mapping of fgemm: persistent, one 512-thread workgroup per CU, 256 queries x
+// 256 rows per tile, 8 waves as 2 (queries) x 4 (rows), each 128 x 64 = 4 x 2
+// v_mfma_f32_32x32x16_bf16 accumulators; K staged 64 deep by global_load_lds (16 B per
+// lane) into two LDS buffers (128 KiB), XOR-swizzled 16-B chunks (conflict-free
+// ds_read_b128), next stage (or the next tile's first stage) in flight during the
+// MFMAs.  Tiles are split over the 8 XCDs by query group so each XCD keeps its query
+// panel in L2 while all XCDs stream the same row panels (Infinity-Cache sharing).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -28,8 +43,9 @@
 namespace cwq {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
 
 #define CWQ_INF __builtin_inff()
 
@@ -37,195 +53,459 @@ __device__ __forceinline__ float rl_f2(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// |v| rounded up a little (norms are used as bounds)
+__device__ __forceinline__ float up(double v) { return (float)(v * (1.0 + 0x1p-20)); }
+
 // ---------------------------------------------------------------------------
-// Row / query preparation: row-major fp32 copy (rerank), bf16 copy (GEMM), norms.
-// The GEMM operands are centred on c (the root mean): |x-mu|^2 is unchanged while
-// the bf16 error, ~|x-c||mu-c| instead of |x||mu|, tracks the spread of the data
-// rather than its offset.  (The fp32 rounding of the centring is covered by eta_n.)
+// Row / query preparation
 // ---------------------------------------------------------------------------
+// Rows: fp32 row-major copy (exact rerank, DP wide), bf16 hi part of the centred row
+// (DPB wide, zero padded), |mu'|^2, |mu_lo|, |mu_hi|.  One wave per row.
 __global__ void rows_prep_kernel(const float* __restrict__ mean, int D, const int64_t* __restrict__ nodes, int64_t n,
-                                 const float* __restrict__ c, int DP, int64_t ld, float* Mf, __bf16* Mb, float* n2,
-                                 float* n1) {
+                                 const float* __restrict__ c, int DP, int DPB, int64_t ld, float* Mf, __bf16* Mb,
+                                 float* n2, float* nlo, float* nhi) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
   if (r >= ld) return;
-  double s = 0.0;
-  for (int d = lane; d < DP; d += kWave) {
-    const float v = (r < n && d < D) ? mean[nodes[r] * (int64_t)D + d] : 0.f;
-    const float vc = (r < n && d < D) ? v - c[d] : 0.f;
-    Mf[r * DP + d] = v;
-    Mb[r * DP + d] = (__bf16)vc;
+  double s = 0.0, slo = 0.0, shi = 0.0;
+  const int W = DP > DPB ? DP : DPB;
+  for (int d = lane; d < W; d += kWave) {
+    const bool ok = r < n && d < D;
+    const float v = ok ? mean[nodes[r] * (int64_t)D + d] : 0.f;
+    const float vc = ok ? v - c[d] : 0.f;
+    const __bf16 h = (__bf16)vc;
+    const float hf = (float)h;
+    const float lo = vc - hf;   // exact
+    if (d < DP) Mf[r * DP + d] = v;
+    if (d < DPB) Mb[r * DPB + d] = h;
     s += (double)vc * (double)vc;
+    slo += (double)lo * (double)lo;
+    shi += (double)hf * (double)hf;
   }
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+    shi += __shfl_xor(shi, off, 64);
+  }
   if (lane == 0) {
     n2[r] = (float)s;
-    n1[r] = (float)sqrt(s);
+    nlo[r] = up(sqrt(slo));
+    nhi[r] = up(sqrt(shi));
   }
 }
 
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
-                            int64_t ld, float* Mf, void* Mb, float* n2, float* n1, hipStream_t s) {
+                            int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,
+                            hipStream_t s) {
   if (ld <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, D, nodes, n, c, DP, ld,
-                     Mf, (__bf16*)Mb, n2, n1);
+  hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, D, nodes, n, c, DP, DPB,
+                     ld, Mf, (__bf16*)Mb, n2, nlo, nhi);
   return hipGetLastError();
 }
 
-__global__ void query_prep_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c, int DP,
-                                  int64_t nq_pad, __bf16* Xb, float* n2, float* n1) {
+// Copy the sample rows (bf16) into a compact operand: Sb[j] = Mb[srow[j]] (zero if srow < 0).
+__global__ void gather_bf16_rows_kernel(const __bf16* __restrict__ Mb, int DPB, const int* __restrict__ srow,
+                                        int64_t n, __bf16* Sb) {
+  const int64_t j = blockIdx.x;
+  const int r = srow[j];
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i* src = reinterpret_cast<const v4i*>(Mb + (size_t)(r < 0 ? 0 : r) * DPB);
+  v4i* dst = reinterpret_cast<v4i*>(Sb + (size_t)j * DPB);
+  for (int i = threadIdx.x; i < DPB / 8; i += blockDim.x) dst[i] = r < 0 ? v4i{0, 0, 0, 0} : src[i];
+}
+
+hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int64_t n, void* Sb, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_bf16_rows_kernel, dim3((unsigned)n), dim3(64), 0, s, (const __bf16*)Mb, DPB, srow, n,
+                     (__bf16*)Sb);
+  return hipGetLastError();
+}
+
+// Queries: bf16 hi part of the centred query, and {|x'|^2, |x_hi|, |x_lo|}.
+__global__ void query_prep_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c,
+                                  int DPB, int64_t nq_pad, __bf16* Xb, float4* qinfo) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
   if (r >= nq_pad) return;
-  double s = 0.0;
-  for (int d = lane; d < DP; d += kWave) {
+  double s = 0.0, slo = 0.0, shi = 0.0;
+  for (int d = lane; d < DPB; d += kWave) {
     const float v = (r < nq && d < D) ? q[r * D + d] - c[d] : 0.f;
-    Xb[r * DP + d] = (__bf16)v;
+    const __bf16 h = (__bf16)v;
+    const float hf = (float)h;
+    const float lo = v - hf;
+    Xb[r * DPB + d] = h;
     s += (double)v * (double)v;
+    slo += (double)lo * (double)lo;
+    shi += (double)hf * (double)hf;
   }
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) {
-    n2[r] = (float)s;
-    n1[r] = (float)sqrt(s);
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+    shi += __shfl_xor(shi, off, 64);
   }
+  if (lane == 0) qinfo[r] = make_float4((float)s, up(sqrt(shi)), up(sqrt(slo)), 0.f);
 }
 
-hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DP, int64_t nq_pad, void* Xb,
-                             float* n2, float* n1, hipStream_t s) {
-  hipLaunchKernelGGL(query_prep_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DP, nq_pad,
-                     (__bf16*)Xb, n2, n1);
+hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
+                             float4* qinfo, hipStream_t s) {
+  hipLaunchKernelGGL(query_prep_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DPB, nq_pad,
+                     (__bf16*)Xb, qinfo);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// 1. approximate-key GEMM (bf16 MFMA) -> upper bounds u[q][r]
+// fgemm: bf16-MFMA bounds over (query tile x row tile), persistent
 // ---------------------------------------------------------------------------
-constexpr int GB = 128;        // queries and rows per workgroup tile
-constexpr int GK = 32;         // K depth per LDS stage
-constexpr int GLD = GK + 8;    // padded LDS row (80 B): conflict-free ds_read_b128
+constexpr int FT = kFgTile;       // 256 queries and rows per tile
+constexpr int FK = 64;            // K per LDS stage
+constexpr int FSTAGE = 2 * FT * FK * 2;   // bytes of one stage (A + B images) = 64 KiB
+constexpr int OFF_QV = 2 * FSTAGE;        // float  [FT]   pretest query terms
+constexpr int OFF_QI = OFF_QV + FT * 4;   // float4 [FT]   {|x'|^2, a, c, T}
+constexpr int OFF_PI = OFF_QI + FT * 16;  // float  [FT]   pi of the tile's parent
+constexpr int OFF_REC = OFF_PI + FT * 4;  // int4   [kFgCap] record staging
+constexpr int OFF_CNT = OFF_REC + kFgCap * 16;   // int[4]: count, chunk, fill, base1/n1/base2 scratch
+constexpr int FLDS = OFF_CNT + 32;
 
+// Rigorous bounds l <= key_fp32 <= u from an approximate dot product (error eextra on
+// top of the bf16 split terms).
+__device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, const RowF& rf, float pi, float eps_n,
+                                          float slack, float& u, float& l) {
+  const float n2 = qi.x + rf.rn2;
+  const float S = fmaf(-2.f, dot, n2);
+  const float key = pi + fmaf(rf.hs, S, rf.hl);
+  const float ES = 2.f * fmaf(qi.y, rf.beta, fmaf(qi.z, rf.delta, eextra)) + eps_n * n2;
+  const float ahs = fabsf(rf.hs);
+  const float err = fmaf(ahs, ES, slack * (fabsf(pi) + fabsf(rf.hl) + 3.f * ahs * n2));
+  u = key + err;
+  l = key - err;
+}
 
-// u[q][r] = key~(q, r) + e(q, r) >= key(q, r)   (q local to the launch's query block)
-__global__ __launch_bounds__(256) void approx_gemm_kernel(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb,
-                                                          float* __restrict__ u, const GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][GB][GLD];
-  __shared__ __attribute__((aligned(16))) __bf16 Ms[2][GB][GLD];
-  __shared__ float sxn2[GB], sxn1[GB];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wq = wave >> 1, wr = wave & 1;
-  const int qt = blockIdx.x % a.n_qt;
-  const int rt = blockIdx.x / a.n_qt;
-  const int q0 = qt * GB, r0 = rt * GB;
-  if (tid < GB) {
-    const int q = min(q0 + tid, a.nq - 1);
-    sxn2[tid] = a.xn2[q];
-    sxn1[tid] = a.xn1[q];
-  }
+__device__ __forceinline__ void fg_decode(const FgArgs& a, int xcd, int i, int& qt, int& rt) {
+  const int qg = xcd % a.qgroups, rg = xcd / a.qgroups;
+  const int nqt_g = (a.n_qt + a.qgroups - 1) / a.qgroups;
+  const int nrt_g = (a.n_rt + a.rgroups - 1) / a.rgroups;
+  const int q_lo = qg * nqt_g, r_lo = rg * nrt_g;
+  const int nq_l = max(0, min(nqt_g, a.n_qt - q_lo));
+  qt = q_lo + i % max(nq_l, 1);
+  rt = r_lo + i / max(nq_l, 1);
+}
 
-  // staging: thread -> (tile row, 16-element half); operands are padded to whole tiles
-  const int srow = tid >> 1, shalf = (tid & 1) * 16;
-  const __bf16* xg = Xb + (size_t)(q0 + srow) * a.DP + shalf;
-  const __bf16* mg = Mb + (size_t)(r0 + srow) * a.DP + shalf;
-  typedef int v4i __attribute__((ext_vector_type(4)));
-  v4i xr0, xr1, mr0, mr1;
-  auto gload = [&](int k0) {
-    xr0 = *reinterpret_cast<const v4i*>(xg + k0);
-    xr1 = *reinterpret_cast<const v4i*>(xg + k0 + 8);
-    mr0 = *reinterpret_cast<const v4i*>(mg + k0);
-    mr1 = *reinterpret_cast<const v4i*>(mg + k0 + 8);
-  };
-  auto swrite = [&](int b) {
-    *reinterpret_cast<v4i*>(&Xs[b][srow][shalf]) = xr0;
-    *reinterpret_cast<v4i*>(&Xs[b][srow][shalf + 8]) = xr1;
-    *reinterpret_cast<v4i*>(&Ms[b][srow][shalf]) = mr0;
-    *reinterpret_cast<v4i*>(&Ms[b][srow][shalf + 8]) = mr1;
-  };
+__device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
+  const int qg = xcd % a.qgroups, rg = xcd / a.qgroups;
+  const int nqt_g = (a.n_qt + a.qgroups - 1) / a.qgroups;
+  const int nrt_g = (a.n_rt + a.rgroups - 1) / a.rgroups;
+  const int nq_l = max(0, min(nqt_g, a.n_qt - qg * nqt_g));
+  const int nr_l = max(0, min(nrt_g, a.n_rt - rg * nrt_g));
+  return nq_l * nr_l;
+}
 
-  f32x16v acc[2][2];
+// one K stage of both operands into an LDS stage buffer (8 glds per wave)
+__device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb, int DPB, int q0,
+                                         int r0, int k0, char* sb, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int nk = a.DP / GK;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  const int fr = lane & 31, fk = (lane >> 5) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int b = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * GK);
-#pragma unroll
-    for (int kk = 0; kk < GK / 16; ++kk) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        af[t] = *reinterpret_cast<const bf16x8*>(&Xs[b][wq * 64 + t * 32 + fr][kk * 16 + fk]);
-        bfr[t] = *reinterpret_cast<const bf16x8*>(&Ms[b][wr * 64 + t * 32 + fr][kk * 16 + fk]);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) swrite(b ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue: C[i = query][j = row]; lane: row j = lane&31, query i = (e&3) + 8(e>>2) + 4(lane>>5)
-  //   key~ = P[q][par]*invL + cw*(-0.5*(logdet + iv*S~)),  S~ = |x|^2 + |mu|^2 - 2 x.mu~
-  //   e    = ci*(2 eta |x||mu| + eta_n(|x|^2+|mu|^2))                    (dot-product + norm rounding)
-  //        + slack*(|P invL| + 0.5 cw |logdet| + 3 ci (|x|^2+|mu|^2))   (fp32 evaluation of both keys)
-  //   with ci = 0.5*cw*iv and |S| <= 2(|x|^2+|mu|^2).
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = r0 + wr * 64 + j * 32 + (lane & 31);
-    const bool vrow = r < a.nrows;
-    RowMeta md{0.f, 0.f, 0.f, 0.f};
-    int p = -1, fl = 0;
-    float rn2 = 0.f, rn1 = 0.f;
-    if (vrow) {
-      md = a.meta[r];
-      p = a.par[r];
-      fl = a.flags[r];
-      rn2 = a.rn2[r];
-      rn1 = a.rn1[r];
-    }
-    const bool usable = vrow && (fl & FLAG_HAS_SENT);
-    const float ci = 0.5f * md.cw * md.iv;
-    const float c1 = 2.0f * a.eta * ci * rn1;
-    const float c2 = ci * (a.eta_n + 3.0f * a.slack);
-    const float c0 = a.slack * 0.5f * md.cw * fabsf(md.logdet);
-    const float hl = -0.5f * md.cw * md.logdet;     // cw * (-0.5 logdet)
-    const float hs = -0.5f * md.cw * md.iv;         // cw * (-0.5 iv)
-    const float* Pp = a.P + (p >= 0 ? p : 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int ql = wq * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const int q = q0 + ql;
-        if (!vrow || q >= a.nq) continue;
-        const float xn2 = sxn2[ql], xn1 = sxn1[ql];
-        const float n2 = xn2 + rn2;
-        const float S = fmaf(-2.0f, acc[i][j][e], n2);
-        const float pi = p >= 0 ? Pp[(size_t)q * a.ldP] * md.invL : 0.f;
-        const float key = pi + fmaf(hs, S, hl);
-        const float err = fmaf(c1, xn1, fmaf(c2, n2, fmaf(a.slack, fabsf(pi), c0)));
-        u[(size_t)q * a.ldu + r] = usable ? key + err : -CWQ_INF;
-      }
-    }
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 32 + i * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const __bf16* ga = Xb + (size_t)(q0 + row) * DPB + k0 + c * 8;
+    const __bf16* gb = Mb + (size_t)(r0 + row) * DPB + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(sb + (wave * 32 + i * 8) * 128), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)gb, (lds_void*)(sb + FT * 128 + (wave * 32 + i * 8) * 128), 16, 0,
+                                     0);
   }
 }
 
-hipError_t launch_approx_gemm(const void* Xb, const void* Mb, float* u, const GemmArgs& a, int n_rt, hipStream_t s) {
-  dim3 grid((unsigned)(a.n_qt * n_rt)), block(256);
-  hipLaunchKernelGGL(approx_gemm_kernel, grid, block, 0, s, (const __bf16*)Xb, (const __bf16*)Mb, u, a);
+__global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb,
+                                                    const FgArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[FLDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wq = wave & 1, wr = wave >> 1;
+  const int h = lane >> 5, l31 = lane & 31;
+  const int xcd = blockIdx.x & 7;
+  const int lw = blockIdx.x >> 3;
+  const int nw_x = ((int)gridDim.x - xcd + 7) >> 3;
+  const int ntl = fg_count(a, xcd);
+  if (lw >= ntl) return;
+  const int nk = a.DPB / FK;
+  float* s_qv = reinterpret_cast<float*>(smem + OFF_QV);
+  float4* s_qi = reinterpret_cast<float4*>(smem + OFF_QI);
+  float* s_pi = reinterpret_cast<float*>(smem + OFF_PI);
+  int4* s_rec = reinterpret_cast<int4*>(smem + OFF_REC);
+  int* s_cnt = reinterpret_cast<int*>(smem + OFF_CNT);
+  // fragment read offsets (bytes) within an operand image; f(row) is the same for every
+  // 32-row block, so one per-lane value per k-substep
+  const int fsw = (l31 >> 1) & 7;
+  int foff[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) foff[kk] = l31 * 128 + (((2 * kk + h) ^ fsw) << 4);
+
+  int i = lw;
+  int qt, rt;
+  fg_decode(a, xcd, i, qt, rt);
+  fg_stage(Xb, Mb, a.DPB, qt * FT, rt * FT, 0, smem, wave, lane);
+  if (tid == 0) {
+    s_cnt[0] = 0;    // records of the current tile
+    s_cnt[1] = -1;   // owned chunk
+    s_cnt[2] = 0;    // its fill
+  }
+  int cur = 0;
+  f32x16 acc[4][2];
+  for (;;) {
+    const int q0 = qt * FT, r0 = rt * FT;
+    // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
+    TileF tf;
+    if (a.mode == 0) tf = a.tf[rt];
+    else tf.uniform = 0;
+    const bool uni = tf.uniform != 0;
+    if (tid < FT) {
+      const int q = q0 + tid;
+      float4 qi = a.qinfo[q];
+      float T = CWQ_INF;
+      if (q < a.nq && a.mode == 0) T = a.T[(size_t)q * a.ldT];
+      qi.w = T;
+      s_qi[tid] = qi;
+      float pi = 0.f, qv = CWQ_INF;
+      if (uni) {
+        pi = tf.par >= 0 && q < a.nq ? a.P[(size_t)q * a.ldP + tf.par] * tf.invL : 0.f;
+        if (q < a.nq && T > -CWQ_INF) {   // T = +inf / NaN / -inf: never a candidate here
+          const float tpg = (T - pi) / tf.g;
+          float v = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x + tpg - a.slack * fabsf(pi) / tf.g -
+                    qi.y * tf.beta_max - qi.z * tf.delta_max;
+          v -= 4.f * a.gamma * (fabsf(v) + qi.x + fabsf(tpg) + fabsf(pi) / tf.g);
+          qv = v == v ? v : CWQ_INF;
+        }
+      }
+      s_pi[tid] = pi;
+      s_qv[tid] = qv;
+    }
+    float R0[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int r = r0 + wr * 64 + jb * 32 + l31;
+      R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
+    }
+    __syncthreads();   // stage 0 landed, setup visible
+    // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 qv4 = uni ? *reinterpret_cast<const float4*>(s_qv + wq * 128 + ib * 32 + 8 * g + 4 * h)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          acc[ib][jb][4 * g + 0] = R0[jb] - qv4.x;
+          acc[ib][jb][4 * g + 1] = R0[jb] - qv4.y;
+          acc[ib][jb][4 * g + 2] = R0[jb] - qv4.z;
+          acc[ib][jb][4 * g + 3] = R0[jb] - qv4.w;
+        }
+      }
+    // ---- K loop ----
+    const int inext = i + nw_x;
+    int qn = qt, rn = rt;
+    if (inext < ntl) fg_decode(a, xcd, inext, qn, rn);
+    for (int t = 0; t < nk; ++t) {
+      char* sb = smem + cur * FSTAGE;
+      if (t + 1 < nk) fg_stage(Xb, Mb, a.DPB, q0, r0, (t + 1) * FK, smem + (cur ^ 1) * FSTAGE, wave, lane);
+      else if (inext < ntl) fg_stage(Xb, Mb, a.DPB, qn * FT, rn * FT, 0, smem + (cur ^ 1) * FSTAGE, wave, lane);
+      const char* sA = sb + wq * 128 * 128;
+      const char* sB = sb + FT * 128 + wr * 64 * 128;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 af[4], bfr[2];
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) af[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 4096 + foff[kk]);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) bfr[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 4096 + foff[kk]);
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb)
+            acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ib], bfr[jb], acc[ib][jb], 0, 0, 0);
+      }
+      __syncthreads();   // next stage landed; this stage free
+      cur ^= 1;
+    }
+    // ---- epilogue ----
+    // The stage buffer just consumed (cur ^ 1) is free until the next tile's first
+    // K step: 8 KiB per wave of it hold one 32x32 block at a time for the scalar paths.
+    float* wsc = reinterpret_cast<float*>(smem + (cur ^ 1) * FSTAGE) + wave * 2048;
+    bool anyb[4][2];
+    if (a.mode == 0 && uni) {
+      bool any = false;
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          float m = __builtin_fmaxf(acc[ib][jb][0], acc[ib][jb][1]);
+#pragma unroll
+          for (int e = 2; e < 16; e += 2) m = __builtin_fmaxf(m, __builtin_fmaxf(acc[ib][jb][e], acc[ib][jb][e + 1]));
+          anyb[ib][jb] = __ballot(m >= 0.f) != 0;
+          any = any || anyb[ib][jb];
+        }
+      if (!any) goto flush;
+    } else {
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) anyb[ib][jb] = true;
+    }
+    {
+      RowF rf[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int r = r0 + wr * 64 + jb * 32 + l31;
+        const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
+        rf[jb] = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+      }
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          if (!anyb[ib][jb]) continue;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) wsc[e * 64 + lane] = acc[ib][jb][e];
+          const int r = r0 + wr * 64 + jb * 32 + l31;
+          const RowF f = rf[jb];
+          const bool usable = f.par >= -1;
+#pragma unroll 1
+          for (int e = 0; e < 16; ++e) {
+            const float d0 = wsc[e * 64 + lane];
+            const int ql = wq * 128 + ib * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            const int q = q0 + ql;
+            if (a.mode == 1) {
+              float lo = -CWQ_INF;
+              if (usable) {
+                const float4 qi = s_qi[ql];
+                const float pi = (f.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+                float u;
+                fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f, pi, a.eps_n, a.slack, u, lo);
+              }
+              a.lb[(size_t)q * a.ldlb + r] = lo;
+            } else if (usable && q < a.nq && (!uni || d0 >= 0.f)) {
+              const float4 qi = s_qi[ql];
+              float d, ex, pi;
+              if (uni) {
+                const float init = f.R0 - s_qv[ql];
+                d = d0 - init;
+                ex = a.gamma * fabsf(init) + 0x1p-23f * (fabsf(d0) + fabsf(init));
+                pi = s_pi[ql];
+              } else {
+                d = d0;
+                ex = 0x1p-23f * fabsf(d0);
+                pi = f.par >= 0 ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+              }
+              float u, lo;
+              fg_bounds(d, ex, qi, f, pi, a.eps_n, a.slack, u, lo);
+              if (u >= qi.w) {
+                const int4 rv = make_int4(q, r, __float_as_int(u), __float_as_int(lo));
+                const int slot = atomicAdd(&s_cnt[0], 1);
+                if (slot < kFgCap) {
+                  s_rec[slot] = rv;
+                } else {   // dense tile (small or clustered data): straight to the direct region
+                  const int gs = atomicAdd(&a.gctr[1], 1);
+                  if (gs < a.dir_cap) a.rec_dir[gs] = rv;
+                  else a.qover[q] = 1;
+                }
+              }
+            }
+          }
+        }
+    }
+  flush:
+    if (a.mode == 0) {
+      // records -> global append buffer, in chunks of kFgChunk slots owned by this
+      // workgroup (one atomic per chunk, not per tile)
+      __syncthreads();
+      const int cnt = s_cnt[0];
+      const int n = min(cnt, kFgCap);
+      if (tid == 0) {
+        int chunk = s_cnt[1], fill = s_cnt[2];
+        int n1 = chunk >= 0 ? min(n, kFgChunk - fill) : 0;
+        int base1 = chunk * kFgChunk + fill, base2 = 0, lost = 0;
+        fill += n1;
+        if (n > n1) {
+          if (chunk >= 0) a.chunk_fill[chunk] = fill;
+          const int c2 = atomicAdd(a.gctr, 1);
+          if ((int64_t)(c2 + 1) * kFgChunk > a.rec_cap) {   // buffer full: records lost
+            lost = 1;
+            chunk = -1;
+            fill = 0;
+            s_cnt[5] = n1;   // write only the first part
+          } else {
+            chunk = c2;
+            fill = n - n1;
+            base2 = c2 * kFgChunk;
+            s_cnt[5] = n;
+          }
+        } else {
+          s_cnt[5] = n;
+        }
+        s_cnt[1] = chunk;
+        s_cnt[2] = fill;
+        s_cnt[3] = base1;
+        s_cnt[4] = n1;
+        s_cnt[6] = base2;
+        s_cnt[7] = lost;
+      }
+      __syncthreads();
+      const int nw = s_cnt[5], n1 = s_cnt[4];
+      if (tid < nw) a.rec[tid < n1 ? s_cnt[3] + tid : s_cnt[6] + (tid - n1)] = s_rec[tid];
+      if (s_cnt[7] && tid < FT && q0 + tid < a.nq) a.qover[q0 + tid] = 1;   // re-run this tile's queries exactly
+    }
+    i = inext;
+    if (i >= ntl) break;
+    qt = qn;
+    rt = rn;
+    __syncthreads();   // epilogue LDS reads done before the next setup rewrites them
+    if (tid == 0) s_cnt[0] = 0;
+  }
+  if (a.mode == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
+}
+
+hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s) {
+  if (a.DPB % FK != 0 || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
+  if (a.qgroups * a.rgroups != 8) return hipErrorInvalidValue;
+  n_wg = std::max(8, n_wg / 8 * 8);
+  hipLaunchKernelGGL(fgemm_kernel, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// bucket: appended records -> per-query candidate lists
+// ---------------------------------------------------------------------------
+__global__ void bucket_kernel(const int4* __restrict__ rec, const int* __restrict__ gctr,
+                              const int* __restrict__ chunk_fill, int64_t rec_cap, const int4* __restrict__ rec_dir,
+                              int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl) {
+  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int4 r;
+  if (g < rec_cap) {
+    const int chunk = (int)(g / kFgChunk);
+    if (chunk >= gctr[0] || (int)(g % kFgChunk) >= chunk_fill[chunk]) return;
+    r = rec[g];
+  } else {
+    const int64_t d = g - rec_cap;
+    if (d >= min(gctr[1], dir_cap)) return;
+    r = rec_dir[d];
+  }
+  const int q = r.x;
+  const int slot = atomicAdd(&qcnt[q], 1);
+  if (slot < capq) {
+    const size_t o = (size_t)q * capq + slot;
+    crow[o] = r.y;
+    cu[o] = __int_as_float(r.z);
+    cl[o] = __int_as_float(r.w);
+  } else {
+    qover[q] = 1;
+  }
+}
+
+hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
+                         int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s) {
+  const int64_t n = rec_cap + dir_cap;
+  hipLaunchKernelGGL(bucket_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, gctr, chunk_fill, rec_cap,
+                     rec_dir, dir_cap, capq, qcnt, qover, crow, cu, cl);
   return hipGetLastError();
 }
 
@@ -261,7 +541,7 @@ __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float
 }
 
 // ---------------------------------------------------------------------------
-// 2. select: top-K' rows by u per query (workgroup per query, 4 wave lists merged)
+// select: top-Kp values per query of a dense [nq][ld] array (the sample bounds)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u, int64_t ldu, int nrows, int Kp,
                                                      float* cu, int* crow) {
@@ -273,7 +553,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
   float lk = -CWQ_INF;
   int lr = 0x7fffffff;
   // each wave owns a contiguous range of whole 1024-row steps (16 values per lane per step;
-  // the u buffer carries >= 1024 floats of tail slack, masked here)
+  // the buffer carries >= 1024 floats of tail slack, masked here)
   constexpr int STEP = 1024;
   const int per = (int)(((int64_t)nrows + 4 * STEP - 1) / (4 * STEP)) * STEP;
   const int r_lo = wave * per, r_hi = min(nrows, r_lo + per);
@@ -307,23 +587,13 @@ hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp,
 }
 
 // ---------------------------------------------------------------------------
-// 3. rerank: exact keys of the K' candidates (bit-identical to the scan kernel's
-//    ISO arithmetic), exact top-K and the certificate.  One wave per query.
-//    X is the scan's interleaved query layout [q/16][v][q%16][16].
+// final: per query (one wave), T2 = K-th largest l among the candidates, exact keys
+// of the candidates with u >= T2 (bit-identical to the scan kernel's ISO arithmetic),
+// exact top-K into partial-list slot 0.  X is the scan's interleaved query layout
+// [q/16][v][q%16][16].
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X, const float* __restrict__ Mf,
-                                                     int DP, int nq, int Kp, int K, const float* __restrict__ cu,
-                                                     const int* __restrict__ crow, const RowMeta* __restrict__ meta,
-                                                     const int* __restrict__ par, const float* __restrict__ P,
-                                                     int64_t ldP, int seg_base, float* pkey, float* paux, int* prow,
-                                                     int64_t lstride, int* ok_flag) {
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (q >= nq) return;
-  const int row = crow[(size_t)q * 64 + lane];
-  const float uc = cu[(size_t)q * 64 + lane];
-  const bool valid = lane < Kp && uc != -CWQ_INF && row != 0x7fffffff;
-  const int rr = valid ? row : 0;
+__device__ __forceinline__ float exact_iso_key(const float* __restrict__ X, const float* __restrict__ Mf, int DP,
+                                               int q, int rr, const RowMeta& md, float pp, float& lp) {
   const float* __restrict__ mr = Mf + (size_t)rr * DP;
   const int NV16 = DP / 16;
   const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
@@ -347,63 +617,101 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
     }
     acc += part;
   }
-  const RowMeta md = meta[rr];
-  const int p = par[rr];
   const float S = md.iv * acc;
-  const float lp = -0.5f * (md.logdet + 0.f + S);
-  const float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;
-  float key = fmaf(pp, md.invL, md.cw * lp);
-  if (!valid) key = -CWQ_INF;
-  // exact top-K among the candidates
+  lp = -0.5f * (md.logdet + 0.f + S);
+  return fmaf(pp, md.invL, md.cw * lp);
+}
+
+__global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X, const float* __restrict__ Mf, int DP,
+                                                    int nq, int K, int capq, const int* __restrict__ qcnt,
+                                                    const int* __restrict__ qover, const int* __restrict__ crow,
+                                                    const float* __restrict__ cu, const float* __restrict__ cl,
+                                                    const float* __restrict__ T, int64_t ldT,
+                                                    const RowMeta* __restrict__ meta, const int* __restrict__ par,
+                                                    const float* __restrict__ P, int64_t ldP, int seg_base,
+                                                    float* pkey, float* paux, int* prow, int64_t lstride,
+                                                    int* ok_flag, int* n_exact) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (q >= nq) return;
+  const int n = qcnt[q];
+  const float Tq = T[(size_t)q * ldT];
+  bool ok = qover[q] == 0 && n >= K && n <= capq && Tq > -CWQ_INF;
   float lk = -CWQ_INF, la = 0.f;
   int lr = 0x7fffffff;
-  const int rid = seg_base + rr;
-  {
-    const bool c = key != -CWQ_INF;
-    uint64_t mask = __ballot(c);
-    while (mask) {
-      const int j = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const float ck = rl_f2(key, j), ca = rl_f2(lp, j);
-      const int cr = __builtin_amdgcn_readlane(rid, j);
-      const bool prec = lk > ck || (lk == ck && lr < cr);
-      const int pos = __popcll(__ballot(prec));
-      if (pos < K) {
-        const float sk = __int_as_float(__shfl_up(__float_as_int(lk), 1, 64));
-        const float sa = __int_as_float(__shfl_up(__float_as_int(la), 1, 64));
-        const int sr = __shfl_up(lr, 1, 64);
-        if (lane == pos) {
-          lk = ck;
-          la = ca;
-          lr = cr;
-        } else if (lane > pos) {
-          lk = sk;
-          la = sa;
-          lr = sr;
+  int nx = 0;
+  if (ok) {
+    const size_t base = (size_t)q * capq;
+    // pass 1: K-th largest lower bound
+    float tk = -CWQ_INF;
+    int tr = 0x7fffffff;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const float lv = j < n ? cl[base + j] : -CWQ_INF;
+      list64_offer(tk, tr, lane, lv, j, K);
+    }
+    const float T2 = rl_f2(tk, K - 1);
+    // pass 2: exact keys of the survivors
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const bool c = j < n && cu[base + j] >= T2;
+      if (__ballot(c) == 0) continue;
+      float key = -CWQ_INF, lp = 0.f;
+      int rid = 0x7fffffff;
+      if (c) {
+        const int rr = crow[base + j];
+        const RowMeta md = meta[rr];
+        const int p = par[rr];
+        const float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;
+        key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp);
+        rid = seg_base + rr;
+        ++nx;
+      }
+      uint64_t mask = __ballot(c);
+      while (mask) {
+        const int b = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const float ck = rl_f2(key, b), ca = rl_f2(lp, b);
+        const int cr = __builtin_amdgcn_readlane(rid, b);
+        const bool prec = lk > ck || (lk == ck && lr < cr);
+        const int pos = __popcll(__ballot(prec));
+        if (pos < K) {
+          const float sk = __int_as_float(__shfl_up(__float_as_int(lk), 1, 64));
+          const float sa = __int_as_float(__shfl_up(__float_as_int(la), 1, 64));
+          const int sr = __shfl_up(lr, 1, 64);
+          if (lane == pos) {
+            lk = ck;
+            la = ca;
+            lr = cr;
+          } else if (lane > pos) {
+            lk = sk;
+            la = sa;
+            lr = sr;
+          }
         }
       }
     }
   }
-  // certificate: rows outside the candidate set have u <= u_(K') < tau_K
-  const float tau = rl_f2(lk, K - 1);
-  const float ulast = rl_f2(uc, Kp - 1);
-  const bool complete = ulast == -CWQ_INF;   // fewer than K' usable rows: all are candidates
-  const bool ok = complete || ulast < tau;
   if (lane < K) {
     const size_t o = (size_t)q * lstride + lane;
-    pkey[o] = lk;
+    pkey[o] = ok ? lk : -CWQ_INF;
     paux[o] = la;
-    prow[o] = lr;
+    prow[o] = ok ? lr : 0x7fffffff;
   }
-  if (lane == 0) ok_flag[q] = ok ? 1 : 0;
+  for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
+  if (lane == 0) {
+    ok_flag[q] = ok ? 1 : 0;
+    if (n_exact) n_exact[q] = nx;
+  }
 }
 
-hipError_t launch_rerank(const float* X, const float* Mf, int DP, int nq, int Kp, int K, const float* cu,
-                         const int* crow, const RowMeta* meta, const int* par, const float* P, int64_t ldP,
-                         int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, Kp, K, cu, crow,
-                     meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag);
+hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
+                        const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
+                        int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
+                        float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
+                     crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact);
   return hipGetLastError();
 }
 

@@ -86,14 +86,14 @@ class CobwebIndex:
 
     def set_filter(self, mode):
         """Isotropic-row strategy of score_topk: -1 automatic, 0 exact fp32 scan,
-        1 bf16-MFMA candidate filter + exact rerank (k <= 32).  Results are identical."""
+        1 bf16-MFMA candidate filter + exact rerank (k <= 64).  Results are identical."""
         check(lib().cwq_set_filter(self._h, int(mode)))
 
     def last_stats(self):
-        out = np.zeros(4, np.int64)
+        out = np.zeros(6, np.int64)
         check(lib().cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"filter_queries": int(out[0]), "fallback_queries": int(out[1]), "filter_used": bool(out[2]),
-                "candidates": int(out[3])}
+                "candidates": int(out[3]), "exact_reranks": int(out[4]), "sample_rows": int(out[5])}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -2,7 +2,7 @@
 the isotropic rows are searched, never the answer.  Every case compares the filter
 (cwq_set_filter 1) with the exact fp32 scan (mode 0): ids AND scores bit-identical,
 plus the reference goldens through the filter, mixed isotropic/anisotropic rows,
-boundary ties that defeat the certificate (exact fallback), and data with a large
+wide boundary ties, candidate-list overflow (exact fallback), and data with a large
 common offset or scale."""
 import numpy as np
 import pytest
@@ -38,7 +38,8 @@ def both(ix, Q, k):
 
 
 @pytest.mark.parametrize("N,D,k", [(20000, 96, 10), (30000, 768, 10), (5000, 64, 1), (5000, 64, 32),
-                                   (1000, 32, 16), (100, 32, 10), (40, 32, 32), (3000, 200, 7)])
+                                   (1000, 32, 16), (100, 32, 10), (40, 32, 32), (3000, 200, 7),
+                                   (5000, 64, 64)])
 def test_filter_equals_exact_scan(gpu, N, D, k):
     X = gpu.synth.synthetic_corpus(N, D, seed=N + D)
     ix = flat_index(gpu, X)
@@ -84,15 +85,29 @@ def test_mixed_iso_aniso_rows(gpu):
         assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
 
 
-def test_boundary_ties_fall_back(gpu):
-    """200 identical leaves around every query: the top-k boundary is a tie wider
-    than K' = 64, the certificate cannot hold and every query is re-run exactly."""
+def test_boundary_ties(gpu):
+    """200 identical leaves around every query: the top-k boundary is a 200-way tie;
+    every tied row is a candidate and is reranked exactly (ties -> lower row id)."""
     X = gpu.synth.synthetic_corpus(5000, 48, seed=11)
     X[1000:1200] = X[1000]
     ix = flat_index(gpu, X)
     Q = X[1000].repeat(50, 1) + 0.01 * gpu.synth.synthetic_corpus(50, 48, seed=12)
     ids0, s0, ids1, s1, st = both(ix, Q, 10)
-    assert st["fallback_queries"] == 50, st
+    assert st["fallback_queries"] == 0, st
+    assert st["exact_reranks"] >= 200, st
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
+def test_candidate_overflow_falls_back(gpu):
+    """6000 identical leaves next to every query overflow the per-tile record lists and
+    the per-query candidate lists: those queries are re-run by the exact scan."""
+    X = gpu.synth.synthetic_corpus(20000, 64, seed=13)
+    X[2000:8000] = X[2000]
+    ix = flat_index(gpu, X)
+    Q = torch.cat([X[2000].repeat(40, 1) + 0.01 * gpu.synth.synthetic_corpus(40, 64, seed=14),
+                   gpu.synth.synthetic_queries(X, 60, seed=15)[0]])
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert st["fallback_queries"] >= 40, st
     assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
 
 
@@ -124,6 +139,6 @@ def test_auto_mode_threshold(gpu):
     ix = flat_index(gpu, X)
     Q = X[:8].contiguous()
     ix.score_topk(Q, 10)
-    assert ix.last_stats()["filter_used"]          # >= 16384 iso rows, k <= 32
-    ix.score_topk(Q, 40)
-    assert not ix.last_stats()["filter_used"]      # k > 32: exact scan
+    assert ix.last_stats()["filter_used"]          # >= 16384 iso rows, k <= 64
+    ix.score_topk(Q, 70)
+    assert not ix.last_stats()["filter_used"]      # k > 64: exact scan (full ranking path)
