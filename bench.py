@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 import cobweb_pkg  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (no sparsity)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -111,7 +112,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01_fgemm.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,23 +183,35 @@ def main():
     qps = world * Qn * args.steps / dt
 
     # ---- dominant kernel timing (HIP events on the launch stream) ----
+    st = index.last_stats()
     index.set_timing(True)
     tms = []
     for _ in range(3):
         index.score_topk(Q, k)
         tms.append(index.last_timing())
     index.set_timing(False)
-    scan_ms = float(np.mean([t["leaf_scan_ms"] / max(1, t["leaf_scan_launches"]) for t in tms]))
     call_ms = float(np.mean([t["call_ms"] for t in tms]))
     NL = index.info["leaf_rows"]
-    flops_launch = 4.0 * D * NL * Qn                      # 4*Nn*D per query (leaf rows)
-    achieved_tf = flops_launch / (scan_ms * 1e-3) / 1e12
+    if st["filter_used"]:
+        # bf16-MFMA candidate filter (cwq_mfma.hip fgemm): 2*D flops per (query, leaf row)
+        kern_ms = float(np.mean([t["fgemm_ms"] for t in tms]))
+        flops_launch = 2.0 * D * NL * Qn
+        peak, kname, pipe = PEAK_BF16_TFLOPS, "fgemm_kernel (bf16 MFMA filter pass)", "bf16 MFMA dense"
+        phases = {"sample_ms": round(float(np.mean([t["sample_ms"] for t in tms])), 3),
+                  "fgemm_ms": round(kern_ms, 3),
+                  "rerank_ms": round(float(np.mean([t["rerank_ms"] for t in tms])), 3)}
+    else:
+        kern_ms = float(np.mean([t["leaf_scan_ms"] / max(1, t["leaf_scan_launches"]) for t in tms]))
+        flops_launch = 4.0 * D * NL * Qn                  # 4*Nn*D per query (leaf rows)
+        peak, kname, pipe = PEAK_FP32_TFLOPS, "scan_kernel<ISO,TOPK> (exact fp32 leaf scan)", "fp32 VALU"
+        phases = {}
+    achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
     bytes_q = 8.0 * (N + 1) * D + 8.0 * 2 * N + 4.0 * D + 12.0 * k   # SURVEY §8(d) bytes per query
     traffic = None
     if os.path.exists(args.pmc_file):
         try:
             pm = json.load(open(args.pmc_file))
-            if pm.get("workload") == [N, D, Qn, k]:
+            if pm.get("workload") == [N, D, Qn, k] and pm.get("kernel") == kname.split(" ")[0]:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -226,11 +239,13 @@ def main():
                        "corpus": N, "dim": D, "queries_per_gpu": Qn, "k": k, "tree": "flat-synth",
                        "parallelism": f"query-shard x{world}, index broadcast over RCCL" if world > 1
                        else "single GPU"},
-            "roofline": {"bound": "mfma", "pipe": "fp32 VALU (peak = fp32 dense MFMA/vector peak)",
-                         "achieved": round(achieved_tf, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                         "kernel": "scan_kernel<ISO,TOPK> (leaf scan)", "kernel_ms": round(scan_ms, 3),
-                         "call_ms": round(call_ms, 3), "flops_per_launch": flops_launch},
+            "roofline": {"bound": "mfma", "pipe": pipe,
+                         "achieved": round(achieved_tf, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved_tf / peak, 4), "traffic": traffic,
+                         "kernel": kname, "kernel_ms": round(kern_ms, 3),
+                         "call_ms": round(call_ms, 3), "flops_per_launch": flops_launch, "phases_ms": phases},
+            "filter": {k_: st[k_] for k_ in ("filter_used", "fallback_queries", "candidates", "exact_reranks",
+                                              "sample_rows")},
             "hbm_roofline": {"bytes_per_query": bytes_q,
                              "per_query_roof_qps": round(PEAK_HBM_GBS * 1e9 / bytes_q, 1),
                              "frac": round(qps / world * bytes_q / (PEAK_HBM_GBS * 1e9), 3)},

@@ -124,13 +124,15 @@ int cwq_categorize(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_
 /*
  * Device timing of the phases of the last cwq_score_topk call, measured with HIP
  * events recorded on the stream the kernels run on (enable first; timing mode
- * synchronises the stream once per query chunk).
- *   out[0] leaf-row scan (the fused score + top-k kernel)   out[1] internal-node pass
- *   out[2] merge + sentence expansion                      out[3] whole call
- *   (milliseconds; out[4] = number of leaf-scan launches)
+ * synchronises the stream once per query chunk).  Milliseconds:
+ *   out[0] leaf rows (scan, or the whole filter pipeline)   out[1] internal-node pass
+ *   out[2] merge + sentence expansion                        out[3] whole call
+ *   out[4] number of leaf-row launches
+ *   filter pipeline only: out[5] threshold sample pass (fgemm + select)
+ *   out[6] the filter fgemm launches (sum)                  out[7] last bucket + exact rerank
  */
 int cwq_set_timing(cwq_index* idx, int enable);
-int cwq_last_timing(cwq_index* idx, float* out5);
+int cwq_last_timing(cwq_index* idx, float* out8);
 
 /*
  * Isotropic-row strategy of cwq_score_topk (no reference counterpart: an execution

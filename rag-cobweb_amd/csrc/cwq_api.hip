@@ -111,8 +111,8 @@ struct cwq_index {
   // timing (cwq_set_timing)
   bool timing = false;
   int filter = -1;   // cwq_set_filter
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  float t_ms[5] = {0, 0, 0, 0, 0};
+  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  float t_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // workspace
   std::mutex mu;
   void* ws = nullptr;
@@ -180,7 +180,7 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
                  const std::vector<int>& row_par, const std::vector<int>& row_flags, hipStream_t s) {
   int rc;
   const int DP = ix->DP, D = ix->D, NLi = ix->NL_iso;
-  ix->DPB = (int)round_up(D, 64);
+  ix->DPB = (int)std::max<int64_t>(96, round_up(D, 32));   // fgemm: 32-deep stages, >= 3 of them
   const int DPB = ix->DPB;
   ix->ld_f = round_up(NLi, kFgTile);
   const int64_t ld = ix->ld_f;
@@ -682,6 +682,16 @@ bool use_filter(const cwq_index* ix, int k) {
 
 // fgemm launch geometry: query groups over the 8 XCDs (each keeps its query panel in
 // L2), row groups for the remaining factor.
+int fg_phases() {
+  const char* e = getenv("CWQ_FG_PHASES");
+  return e && *e ? atoi(e) : 1;
+}
+
+int fg_order() {   // default: dynamic per-XCD tile claims (measured fastest)
+  const char* e = getenv("CWQ_FG_ORDER");
+  return e && *e ? atoi(e) : 2;
+}
+
 void fg_groups(int n_qt, int& qg, int& rg) {
   qg = n_qt >= 8 ? 8 : n_qt >= 4 ? 4 : n_qt >= 2 ? 2 : 1;
   rg = 8 / qg;
@@ -806,6 +816,9 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.n_qt = n_qt;
         fg_groups(n_qt, g.qgroups, g.rgroups);
         g.qinfo = qinfo;
+        g.order = fg_order();
+        g.dbg = getenv("CWQ_FG_DBG") ? atoi(getenv("CWQ_FG_DBG")) : 0;
+        g.tctr = gctr + 8;
         g.rf = ix->iso_rf;
         g.tf = ix->iso_tf;
         g.P = c.P ? c.P : ix->dummy;
@@ -814,7 +827,9 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.eps_n = (float)fc.eps_n;
         g.slack = (float)fc.slack;
         // 1. sample pass -> T[q] = K-th largest lower bound over the sample rows
+        if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
         g.mode = 1;
+        if (g.order == 2) HIPCHK(hipMemsetAsync(g.tctr, 0, 32, s));
         g.n_rt = n_rts;
         g.nrows = ix->ld_s;
         g.rowmap = ix->samp_rows;
@@ -822,9 +837,10 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.ldlb = ix->ld_s;
         HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
         HIPCHK(launch_select(lb, ix->ld_s, nqc, ix->ld_s, K, tl, tr, s));
-        // 2. filter pass -> per-tile candidate records
+        // 2. filter passes over row-tile phases (1/16, 3/16, 12/16 of the rows); after
+        // each phase the candidates go to per-query lists and T[q] is raised to the K-th
+        // largest candidate lower bound, so later phases emit fewer candidates
         g.mode = 0;
-        g.n_rt = n_rt;
         g.nrows = ix->NL_iso;
         g.rowmap = nullptr;
         g.T = tl + (K - 1);
@@ -838,10 +854,35 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.dir_cap = dir_cap;
         HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)nqf * 4, s));
         HIPCHK(hipMemsetAsync(qover, 0, (size_t)nqf * 4, s));
-        HIPCHK(hipMemsetAsync(gctr, 0, 8, s));
-        HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
-        // 3. per-query candidate lists, 4. exact rerank
-        HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl, s));
+        int cuts[4] = {0, n_rt, n_rt, n_rt};
+        int nph = 1;
+        if (n_rt >= 16 && fg_phases()) {
+          cuts[1] = std::max(1, n_rt / 16);
+          cuts[2] = std::max(cuts[1] + 1, n_rt / 4);
+          cuts[3] = n_rt;
+          nph = 3;
+        }
+        for (int ph = 0; ph < nph; ++ph) {
+          g.rt_off = cuts[ph];
+          g.n_rt = cuts[ph + 1] - cuts[ph];
+          HIPCHK(hipMemsetAsync(gctr, 0, 64, s));
+          if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
+          HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
+          if (ix->timing) {   // per-launch fgemm time (timing mode synchronises)
+            float e = 0, e0 = 0;
+            HIPCHK(hipEventRecord(ix->ev[6], s));
+            HIPCHK(hipEventSynchronize(ix->ev[6]));
+            HIPCHK(hipEventElapsedTime(&e, ix->ev[5], ix->ev[6]));
+            ix->t_ms[6] += e;
+            if (ph == 0) {
+              HIPCHK(hipEventElapsedTime(&e0, ix->ev[4], ix->ev[5]));
+              ix->t_ms[5] += e0;
+            }
+          }
+          HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl,
+                               s));
+          if (ph + 1 < nph) HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, s));
+        }
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
@@ -849,6 +890,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                             (int64_t)nst * K, okf, nex, s));
         qcnt_d = qcnt;
         nex_d = nex;
+        if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
       } else {
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s)))
           return rc;
@@ -894,6 +936,11 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       ix->t_ms[2] += c2;
       ix->t_ms[3] += d;
       ix->t_ms[4] += filt ? 1 : (ix->NL_iso > 0) + (ix->NL_an > 0);
+      if (filt) {
+        float e3 = 0;
+        HIPCHK(hipEventElapsedTime(&e3, ix->ev[6], ix->ev[7]));
+        ix->t_ms[7] += e3;
+      }
     }
   }
   if (!redo.empty()) {
@@ -941,7 +988,7 @@ extern "C" int cwq_last_stats(cwq_index* ix, int64_t* out) {
 extern "C" int cwq_set_timing(cwq_index* ix, int enable) {
   if (!ix) return fail(CWQ_ERR_ARG, "NULL index");
   DevGuard dg(ix->device);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
     if (!ix->ev[i]) HIPCHK(hipEventCreate(&ix->ev[i]));
   ix->timing = enable != 0;
   return CWQ_OK;
@@ -949,7 +996,7 @@ extern "C" int cwq_set_timing(cwq_index* ix, int enable) {
 
 extern "C" int cwq_last_timing(cwq_index* ix, float* out) {
   if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
-  for (int i = 0; i < 5; ++i) out[i] = ix->t_ms[i];
+  for (int i = 0; i < 8; ++i) out[i] = ix->t_ms[i];
   return CWQ_OK;
 }
 

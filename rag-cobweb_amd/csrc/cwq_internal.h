@@ -150,7 +150,11 @@ struct TileF {
 };
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
+  int rt_off;                             // first row tile of this launch (filter phases)
   int qgroups, rgroups;                   // XCD split (qgroups * rgroups == 8)
+  int order;                              // tile order: 0 static q-fastest, 1 static r-fastest, 2 dynamic
+  int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)
+  int dbg;                                // ablation (perf experiments only): 1 no operand loads, 2 no epilogue
   const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
   const float* T;                         // thresholds, T[q * ldT]
   int64_t ldT;
@@ -180,6 +184,8 @@ hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_w
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
+hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
+                          int64_t ldT, hipStream_t s);
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,

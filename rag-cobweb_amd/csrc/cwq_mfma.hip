@@ -157,14 +157,15 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 // fgemm: bf16-MFMA bounds over (query tile x row tile), persistent
 // ---------------------------------------------------------------------------
 constexpr int FT = kFgTile;       // 256 queries and rows per tile
-constexpr int FK = 64;            // K per LDS stage
-constexpr int FSTAGE = 2 * FT * FK * 2;   // bytes of one stage (A + B images) = 64 KiB
-constexpr int OFF_QV = 2 * FSTAGE;        // float  [FT]   pretest query terms
+constexpr int FK = 32;            // K per LDS stage
+constexpr int FNBUF = 4;          // LDS stage ring: 3 stages in flight while one is consumed
+constexpr int FSTAGE = 2 * FT * FK * 2;   // bytes of one stage (A + B images) = 32 KiB
+constexpr int OFF_QV = FNBUF * FSTAGE;    // float  [FT]   pretest query terms
 constexpr int OFF_QI = OFF_QV + FT * 4;   // float4 [FT]   {|x'|^2, a, c, T}
 constexpr int OFF_PI = OFF_QI + FT * 16;  // float  [FT]   pi of the tile's parent
 constexpr int OFF_REC = OFF_PI + FT * 4;  // int4   [kFgCap] record staging
-constexpr int OFF_CNT = OFF_REC + kFgCap * 16;   // int[4]: count, chunk, fill, base1/n1/base2 scratch
-constexpr int FLDS = OFF_CNT + 32;
+constexpr int OFF_CNT = OFF_REC + kFgCap * 16;   // int[16]: count, chunk, fill, flush scratch, claim
+constexpr int FLDS = OFF_CNT + 64;
 
 // Rigorous bounds l <= key_fp32 <= u from an approximate dot product (error eextra on
 // top of the bf16 split terms).
@@ -180,14 +181,23 @@ __device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, co
   l = key - err;
 }
 
+// XCD-local tile i -> (query tile, row tile).  order 0/2: query tiles fastest (the
+// XCD's query panels stay in L2 while row panels stream past, each read by every
+// query tile of the group at about the same time); order 1: row tiles fastest.
 __device__ __forceinline__ void fg_decode(const FgArgs& a, int xcd, int i, int& qt, int& rt) {
   const int qg = xcd % a.qgroups, rg = xcd / a.qgroups;
   const int nqt_g = (a.n_qt + a.qgroups - 1) / a.qgroups;
   const int nrt_g = (a.n_rt + a.rgroups - 1) / a.rgroups;
   const int q_lo = qg * nqt_g, r_lo = rg * nrt_g;
-  const int nq_l = max(0, min(nqt_g, a.n_qt - q_lo));
-  qt = q_lo + i % max(nq_l, 1);
-  rt = r_lo + i / max(nq_l, 1);
+  const int nq_l = max(1, min(nqt_g, a.n_qt - q_lo));
+  const int nr_l = max(1, min(nrt_g, a.n_rt - r_lo));
+  if (a.order == 1) {
+    qt = q_lo + i / nr_l;
+    rt = a.rt_off + r_lo + i % nr_l;
+  } else {
+    qt = q_lo + i % nq_l;
+    rt = a.rt_off + r_lo + i / nq_l;
+  }
 }
 
 __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
@@ -199,17 +209,20 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
   return nq_l * nr_l;
 }
 
-// one K stage of both operands into an LDS stage buffer (8 glds per wave)
+// one K stage (32 deep) of both operands into an LDS stage buffer: 4 glds per wave.
+// Image: [256 rows][64 B] per operand; 16-B chunk c of row r sits at position
+// c ^ ((r >> 2) & 3) (conflict-free ds_read_b128 fragment reads); the LDS side of a
+// glds is lane-linear, so the permutation is applied to the global source address.
 __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb, int DPB, int q0,
                                          int r0, int k0, char* sb, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 32 + i * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3);
     const __bf16* ga = Xb + (size_t)(q0 + row) * DPB + k0 + c * 8;
     const __bf16* gb = Mb + (size_t)(r0 + row) * DPB + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(sb + (wave * 32 + i * 8) * 128), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)gb, (lds_void*)(sb + FT * 128 + (wave * 32 + i * 8) * 128), 16, 0,
+    __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(sb + (wave * 32 + i * 16) * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)gb, (lds_void*)(sb + FT * 64 + (wave * 32 + i * 16) * 64), 16, 0,
                                      0);
   }
 }
@@ -226,30 +239,58 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   const int lw = blockIdx.x >> 3;
   const int nw_x = ((int)gridDim.x - xcd + 7) >> 3;
   const int ntl = fg_count(a, xcd);
-  if (lw >= ntl) return;
+  const bool dyn = a.order == 2;   // tiles claimed from a per-XCD counter (contiguous in-flight window)
+  if (!dyn && lw >= ntl) return;
   const int nk = a.DPB / FK;
   float* s_qv = reinterpret_cast<float*>(smem + OFF_QV);
   float4* s_qi = reinterpret_cast<float4*>(smem + OFF_QI);
   float* s_pi = reinterpret_cast<float*>(smem + OFF_PI);
   int4* s_rec = reinterpret_cast<int4*>(smem + OFF_REC);
   int* s_cnt = reinterpret_cast<int*>(smem + OFF_CNT);
-  // fragment read offsets (bytes) within an operand image; f(row) is the same for every
-  // 32-row block, so one per-lane value per k-substep
-  const int fsw = (l31 >> 1) & 7;
-  int foff[4];
+  // fragment read offsets (bytes) within an operand image; the swizzle term is the
+  // same for every 32-row block, so one per-lane value per k-substep
+  const int fsw = (l31 >> 2) & 3;
+  int foff[2];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) foff[kk] = l31 * 128 + (((2 * kk + h) ^ fsw) << 4);
+  for (int kk = 0; kk < 2; ++kk) foff[kk] = l31 * 64 + (((2 * kk + h) ^ fsw) << 4);
 
+  // stage ring: stages are numbered over this workgroup's whole tile sequence, so the
+  // next tile's first stages are in flight during the current tile's last steps
   int i = lw;
+  if (dyn) {
+    if (tid == 0) s_cnt[8] = atomicAdd(&a.tctr[xcd], 1);
+    __syncthreads();
+    i = s_cnt[8];
+    if (i >= ntl) return;
+  }
+  int next_i = dyn ? ntl : i + nw_x;   // dynamic: claimed at each tile setup
+  int ic_i = i, ic_k = 0, ic_qt, ic_rt, issued = 0, gs = 0;
+  fg_decode(a, xcd, ic_i, ic_qt, ic_rt);
+  // the next tile is resolved lazily: its first stage is issued during the current
+  // tile's K loop, after the setup that claimed it
+  auto issue_next = [&]() {
+    if (ic_i == -2) {
+      ic_i = next_i;
+      if (ic_i < ntl) fg_decode(a, xcd, ic_i, ic_qt, ic_rt);
+    }
+    if (ic_i >= ntl) return;
+    if (!(a.dbg & 1)) fg_stage(Xb, Mb, a.DPB, ic_qt * FT, ic_rt * FT, ic_k * FK, smem + (issued & (FNBUF - 1)) * FSTAGE, wave, lane);
+    ++issued;
+    if (++ic_k == nk) {
+      ic_k = 0;
+      ic_i = -2;
+    }
+  };
+  issue_next();
+  issue_next();
+  issue_next();
   int qt, rt;
   fg_decode(a, xcd, i, qt, rt);
-  fg_stage(Xb, Mb, a.DPB, qt * FT, rt * FT, 0, smem, wave, lane);
   if (tid == 0) {
     s_cnt[0] = 0;    // records of the current tile
     s_cnt[1] = -1;   // owned chunk
     s_cnt[2] = 0;    // its fill
   }
-  int cur = 0;
   f32x16 acc[4][2];
   for (;;) {
     const int q0 = qt * FT, r0 = rt * FT;
@@ -285,7 +326,9 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       const int r = r0 + wr * 64 + jb * 32 + l31;
       R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
     }
+    if (dyn && tid == 0) s_cnt[8] = atomicAdd(&a.tctr[xcd], 1);   // the tile after this one
     __syncthreads();   // stage 0 landed, setup visible
+    if (dyn) next_i = s_cnt[8];
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
@@ -302,36 +345,39 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         }
       }
     // ---- K loop ----
-    const int inext = i + nw_x;
-    int qn = qt, rn = rt;
-    if (inext < ntl) fg_decode(a, xcd, inext, qn, rn);
     for (int t = 0; t < nk; ++t) {
-      char* sb = smem + cur * FSTAGE;
-      if (t + 1 < nk) fg_stage(Xb, Mb, a.DPB, q0, r0, (t + 1) * FK, smem + (cur ^ 1) * FSTAGE, wave, lane);
-      else if (inext < ntl) fg_stage(Xb, Mb, a.DPB, qn * FT, rn * FT, 0, smem + (cur ^ 1) * FSTAGE, wave, lane);
-      const char* sA = sb + wq * 128 * 128;
-      const char* sB = sb + FT * 128 + wr * 64 * 128;
+      issue_next();
+      const char* sb = smem + (gs & (FNBUF - 1)) * FSTAGE;
+      const char* sA = sb + wq * 128 * 64;
+      const char* sB = sb + FT * 64 + wr * 64 * 64;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
+      for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[4], bfr[2];
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) af[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 4096 + foff[kk]);
+        for (int ib = 0; ib < 4; ++ib) af[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 2048 + foff[kk]);
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) bfr[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 4096 + foff[kk]);
+        for (int jb = 0; jb < 2; ++jb) bfr[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 2048 + foff[kk]);
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
           for (int jb = 0; jb < 2; ++jb)
             acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ib], bfr[jb], acc[ib][jb], 0, 0, 0);
       }
-      __syncthreads();   // next stage landed; this stage free
-      cur ^= 1;
+      ++gs;
+      // stage gs must have landed (every wave's share: own vmcnt, then the barrier);
+      // the stages issued after it stay in flight
+      const int n_out = issued - gs - 1;
+      if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
     // ---- epilogue ----
-    // The stage buffer just consumed (cur ^ 1) is free until the next tile's first
-    // K step: 8 KiB per wave of it hold one 32x32 block at a time for the scalar paths.
-    float* wsc = reinterpret_cast<float*>(smem + (cur ^ 1) * FSTAGE) + wave * 2048;
+    // The stage buffer just consumed is free until the next tile's first K step
+    // re-issues it: 4 KiB per wave of it hold one 32x32 block for the scalar paths.
+    float* wsc = reinterpret_cast<float*>(smem + ((gs - 1) & (FNBUF - 1)) * FSTAGE) + wave * 1024;
     bool anyb[4][2];
+    if (a.dbg & 2) goto flush;
     if (a.mode == 0 && uni) {
       bool any = false;
 #pragma unroll
@@ -454,10 +500,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       if (tid < nw) a.rec[tid < n1 ? s_cnt[3] + tid : s_cnt[6] + (tid - n1)] = s_rec[tid];
       if (s_cnt[7] && tid < FT && q0 + tid < a.nq) a.qover[q0 + tid] = 1;   // re-run this tile's queries exactly
     }
-    i = inext;
+    i = next_i;
     if (i >= ntl) break;
-    qt = qn;
-    rt = rn;
+    if (!dyn) next_i = i + nw_x;
+    fg_decode(a, xcd, i, qt, rt);
     __syncthreads();   // epilogue LDS reads done before the next setup rewrites them
     if (tid == 0) s_cnt[0] = 0;
   }
@@ -465,7 +511,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
 }
 
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s) {
-  if (a.DPB % FK != 0 || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
+  if (a.DPB % FK != 0 || a.DPB < 3 * FK || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
   if (a.qgroups * a.rgroups != 8) return hipErrorInvalidValue;
   n_wg = std::max(8, n_wg / 8 * 8);
   hipLaunchKernelGGL(fgemm_kernel, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
@@ -583,6 +629,36 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
 
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s) {
   hipLaunchKernelGGL(select_kernel, dim3((unsigned)nq), dim3(256), 0, s, u, ldu, nrows, Kp, cu, crow);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// tighten: between filter phases, T[q] = max(T[q], K-th largest lower bound among the
+// candidates found so far) -- still <= tau_K (they are K distinct rows).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tighten_kernel(int nq, int K, int capq, const int* __restrict__ qcnt,
+                                                      const int* __restrict__ qover, const float* __restrict__ cl,
+                                                      float* T, int64_t ldT) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (q >= nq) return;
+  const int n = min(qcnt[q], capq);
+  if (qover[q] || n < K) return;
+  const size_t base = (size_t)q * capq;
+  float tk = -CWQ_INF;
+  int tr = 0x7fffffff;
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    const int j = j0 + lane;
+    list64_offer(tk, tr, lane, j < n ? cl[base + j] : -CWQ_INF, j, K);
+  }
+  const float kth = rl_f2(tk, K - 1);
+  if (lane == 0 && kth > T[(size_t)q * ldT]) T[(size_t)q * ldT] = kth;
+}
+
+hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
+                          int64_t ldT, hipStream_t s) {
+  hipLaunchKernelGGL(tighten_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, nq, K, capq, qcnt, qover, cl, T,
+                     ldT);
   return hipGetLastError();
 }
 

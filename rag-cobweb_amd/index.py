@@ -79,10 +79,11 @@ class CobwebIndex:
 
     def last_timing(self):
         """Phase times (ms) of the last score_topk call, from HIP events on its stream."""
-        out = np.zeros(5, np.float32)
+        out = np.zeros(8, np.float32)
         check(lib().cwq_last_timing(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"leaf_scan_ms": float(out[0]), "internal_ms": float(out[1]), "merge_ms": float(out[2]),
-                "call_ms": float(out[3]), "leaf_scan_launches": int(out[4])}
+                "call_ms": float(out[3]), "leaf_scan_launches": int(out[4]), "sample_ms": float(out[5]),
+                "fgemm_ms": float(out[6]), "rerank_ms": float(out[7])}
 
     def set_filter(self, mode):
         """Isotropic-row strategy of score_topk: -1 automatic, 0 exact fp32 scan,

@@ -1,16 +1,15 @@
 #!/bin/bash
-# rocprofv3 PMC passes (one counter group per pass, kernel-trace only; never
-# combined with sys/runtime tracing) over a short bench run.
+# rocprofv3 PMC passes over the filter probe (one counter group per pass,
+# kernel-trace only; never combined with sys/runtime tracing).
+#   bash scripts/pmc.sh "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_WAVES ..."
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
-BENCH="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --recall-queries 0"
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1; echo "list rc=$?"
 i=0
 for set in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- $BENCH \
-      > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- \
+      python3 scripts/filter_probe.py --modes 1 --reps 1 > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($set) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done

@@ -1,9 +1,14 @@
-"""Summarise rocprofv3 output for the hot kernel into profiles/ (JSON).
+"""Summarise rocprofv3 PMC passes for one hot kernel into profiles/ (JSON).
 
-    python scripts/pmc_summary.py gpurun_out/pmc gpurun_out/prof profiles/pmc_r01.json
-Counters are per dispatch of scan_kernel<ISO,TOPK> (the leaf scan).  FETCH_SIZE
-is the L2 memory-side read volume (KB; Infinity-Cache hits included, see
-MI355X_MICROARCH.md §HBM); GRBM_GUI_ACTIVE / 8 XCDs / duration = effective clock."""
+    python scripts/pmc_summary.py gpurun_out/pmc profiles/pmc_r01_fgemm.json [kernel-substring]
+
+Counters are averaged per dispatch over the LONG dispatches of the kernel (the
+filter pass; the much shorter threshold-sample launches of the same kernel are
+excluded by duration).  FETCH_SIZE is the L2 memory-side read volume in KB; on
+gfx950 it reports half the bytes of 16-B-per-lane streaming reads (global_load and
+global_load_lds alike, MI355X_MICROARCH.md §HBM), so bytes = 2 * 1024 * FETCH_SIZE;
+Infinity-Cache hits are counted too.  GRBM_GUI_ACTIVE / 8 XCDs / duration =
+effective clock."""
 import collections
 import csv
 import glob
@@ -11,43 +16,49 @@ import json
 import os
 import sys
 
-pmc_dir, prof_dir, out = sys.argv[1:4]
-HOT = "scan_kernel<true, 2"
+pmc_dir, out = sys.argv[1:3]
+HOT = sys.argv[3] if len(sys.argv) > 3 else "fgemm_kernel"
 agg, durs = collections.defaultdict(list), []
 for d in sorted(glob.glob(os.path.join(pmc_dir, "p*"))):
     f = os.path.join(d, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
+    rows = [r for r in csv.DictReader(open(f)) if HOT in r["Kernel_Name"]]
+    dur = {r["Dispatch_Id"]: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows}
+    if not dur:
+        continue
+    cut = 0.5 * max(dur.values())
     per = collections.defaultdict(lambda: collections.defaultdict(float))
-    for r in csv.DictReader(open(f)):
-        if HOT in r["Kernel_Name"]:
+    for r in rows:
+        if dur[r["Dispatch_Id"]] >= cut:
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    durs += [v for v in dur.values() if v >= cut]
     for disp in per.values():
         for k, v in disp.items():
             agg[k].append(v)
 c = {k: sum(v) / len(v) for k, v in agg.items()}
 dur_ms = sorted(durs)[len(durs) // 2] if durs else None
-res = {"kernel": "scan_kernel<ISO,TOPK,fast> (leaf scan)", "median_dispatch_ms": dur_ms, "counters": c}
+res = {"kernel": HOT, "median_dispatch_ms_profiled": dur_ms, "counters": c}
 if dur_ms and "GRBM_GUI_ACTIVE" in c:
     clk = c["GRBM_GUI_ACTIVE"] / 8 / (dur_ms / 1e3)
     res["effective_clock_ghz"] = round(clk / 1e9, 3)
-    if "SQ_INSTS_VALU" in c:
-        res["valu_pipe_busy"] = round(c["SQ_INSTS_VALU"] * 2 / (1024 * clk * dur_ms / 1e3), 3)
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        # cycles summed over SIMDs (1024 SIMDs)
+        res["mfma_pipe_busy"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * clk * dur_ms / 1e3), 3)
 if "SQ_WAVE_CYCLES" in c:
     w = c["SQ_WAVE_CYCLES"]
     res["wave_cycle_split"] = {k: round(c.get(n, 0) / w, 3) for k, n in
                                [("waiting_on_data", "SQ_WAIT_ANY"), ("issue_stalled", "SQ_WAIT_INST_ANY"),
                                 ("issuing", "SQ_ACTIVE_INST_ANY")]}
+if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_ACTIVE"]:
+    res["lds_bank_conflict_frac"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"], 4)
 if "TCC_HIT_sum" in c:
     res["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
 if "FETCH_SIZE" in c:
-    res["fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
-    res["hbm_bytes_per_launch"] = c["FETCH_SIZE"] * 1024   # upper bound: MALL hits are counted too
-kstats = os.path.join(prof_dir, "run_kernel_stats.csv")
-if os.path.exists(kstats):
-    res["kernel_stats_top"] = [{"name": r["Name"][:100], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                "pct": float(r["Percentage"])} for r in list(csv.DictReader(open(kstats)))[:8]]
-res["workload"] = [1000000, 768, 10000, 10]   # bench.py defaults the passes ran
+    res["fetch_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024        # gfx950 16-B-lane correction
+    res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"]       # upper bound: MALL hits counted
+if "WRITE_SIZE" in c:
+    res["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+res["workload"] = [1000000, 768, 10000, 10]   # filter_probe defaults the passes ran
 json.dump(res, open(out, "w"), indent=1)
-print(json.dumps({k: v for k, v in res.items() if k not in ("counters", "kernel_stats_top")}))
+print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
