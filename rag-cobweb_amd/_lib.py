@@ -9,7 +9,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcwq.so")
+LIB_PATH = os.environ.get("CWQ_LIB") or os.path.join(HERE, "libcwq.so")   # CWQ_LIB: A/B experiments only
 
 CWQ_OK = 0
 CWQ_ERR_ARG = -1

@@ -345,32 +345,35 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         }
       }
     // ---- K loop ----
-    for (int t = 0; t < nk; ++t) {
-      issue_next();
-      const char* sb = smem + (gs & (FNBUF - 1)) * FSTAGE;
+    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+    auto load_frags = [&](bf16x8* fa, bf16x8* fb, const char* sb, int kk) {
       const char* sA = sb + wq * 128 * 64;
       const char* sB = sb + FT * 64 + wr * 64 * 64;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[4], bfr[2];
+      for (int ib = 0; ib < 4; ++ib) fa[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 2048 + foff[kk]);
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) af[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 2048 + foff[kk]);
+      for (int jb = 0; jb < 2; ++jb) fb[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 2048 + foff[kk]);
+    };
+    auto mfma8 = [&](const bf16x8* fa, const bf16x8* fb) {
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) bfr[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 2048 + foff[kk]);
+      for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb)
-            acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ib], bfr[jb], acc[ib][jb], 0, 0, 0);
-      }
+        for (int jb = 0; jb < 2; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ib], fb[jb], acc[ib][jb], 0, 0, 0);
+    };
+    load_frags(fa0, fb0, smem + (gs & (FNBUF - 1)) * FSTAGE, 0);
+    for (int t = 0; t < nk; ++t) {
+      issue_next();
+      load_frags(fa1, fb1, smem + (gs & (FNBUF - 1)) * FSTAGE, 1);
+      mfma8(fa0, fb0);
       ++gs;
-      // stage gs must have landed (every wave's share: own vmcnt, then the barrier);
-      // the stages issued after it stay in flight
       const int n_out = issued - gs - 1;
       if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      load_frags(fa0, fb0, smem + (gs & (FNBUF - 1)) * FSTAGE, 0);
+      mfma8(fa1, fb1);
     }
     // ---- epilogue ----
     // The stage buffer just consumed is free until the next tile's first K step
