@@ -2,13 +2,13 @@
 
     python scripts/pmc_summary.py gpurun_out/pmc profiles/pmc_r01_fgemm.json [kernel-substring]
 
-Counters are averaged per dispatch over the LONG dispatches of the kernel (the
-filter pass; the much shorter threshold-sample launches of the same kernel are
-excluded by duration).  FETCH_SIZE is the L2 memory-side read volume in KB; on
-gfx950 it reports half the bytes of 16-B-per-lane streaming reads (global_load and
-global_load_lds alike, MI355X_MICROARCH.md §HBM), so bytes = 2 * 1024 * FETCH_SIZE;
-Infinity-Cache hits are counted too.  GRBM_GUI_ACTIVE / 8 XCDs / duration =
-effective clock."""
+Counters are summed over the filter launches of one score_topk call (the fgemm
+dispatches come in groups of 1 + PHASES per call: the threshold-sample launch, then
+the filter phases) and averaged over calls.  FETCH_SIZE is the L2 memory-side read
+volume in KB; on gfx950 it reports half the bytes of 16-B-per-lane streaming reads
+(global_load and global_load_lds alike, MI355X_MICROARCH.md §HBM), so bytes =
+2 * 1024 * FETCH_SIZE; Infinity-Cache hits are counted too.  GRBM_GUI_ACTIVE / 8
+XCDs / duration = effective clock."""
 import collections
 import csv
 import glob
@@ -18,27 +18,33 @@ import sys
 
 pmc_dir, out = sys.argv[1:3]
 HOT = sys.argv[3] if len(sys.argv) > 3 else "fgemm_kernel"
+PHASES = int(os.environ.get("PMC_PHASES", "3"))
 agg, durs = collections.defaultdict(list), []
 for d in sorted(glob.glob(os.path.join(pmc_dir, "p*"))):
     f = os.path.join(d, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
     rows = [r for r in csv.DictReader(open(f)) if HOT in r["Kernel_Name"]]
-    dur = {r["Dispatch_Id"]: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows}
-    if not dur:
-        continue
-    cut = 0.5 * max(dur.values())
     per = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur = {}
     for r in rows:
-        if dur[r["Dispatch_Id"]] >= cut:
-            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-    durs += [v for v in dur.values() if v >= cut]
-    for disp in per.values():
-        for k, v in disp.items():
+        did = int(r["Dispatch_Id"])
+        per[did][r["Counter_Name"]] += float(r["Counter_Value"])
+        dur[did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    ids = sorted(per)
+    G = 1 + PHASES
+    for c0 in range(0, len(ids) - G + 1, G):
+        grp = ids[c0 + 1:c0 + G]          # skip the sample launch
+        tot = collections.defaultdict(float)
+        for did in grp:
+            for k, v in per[did].items():
+                tot[k] += v
+        for k, v in tot.items():
             agg[k].append(v)
+        durs.append(sum(dur[did] for did in grp))
 c = {k: sum(v) / len(v) for k, v in agg.items()}
 dur_ms = sorted(durs)[len(durs) // 2] if durs else None
-res = {"kernel": HOT, "median_dispatch_ms_profiled": dur_ms, "counters": c}
+res = {"kernel": HOT, "filter_launches_per_call": PHASES, "median_call_fgemm_ms_profiled": dur_ms, "counters": c}
 if dur_ms and "GRBM_GUI_ACTIVE" in c:
     clk = c["GRBM_GUI_ACTIVE"] / 8 / (dur_ms / 1e3)
     res["effective_clock_ghz"] = round(clk / 1e9, 3)
