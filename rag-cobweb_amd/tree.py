@@ -135,6 +135,84 @@ class CobwebTree:
         t.root = nodes[0]
         return t
 
+    # ---- binary format (F2): BFS node arrays in one .npz, no pickles ----
+    BINARY_VERSION = 1
+
+    def to_arrays(self):
+        """BFS node arrays (children in list order): parent [Nn] int64, count [Nn] f32,
+        mean/meanSq [Nn, D] f32, sid_ptr [Nn+1] int64, sid_list int64."""
+        nodes, parent = [], []
+        q = deque([(self.root, -1)])
+        while q:
+            n, p = q.popleft()
+            idx = len(nodes)
+            nodes.append(n)
+            parent.append(p)
+            q.extend((c, idx) for c in n.children)
+        Nn = len(nodes)
+        count = np.empty(Nn, F32)
+        mean = np.empty((Nn, self.dim), F32)
+        meanSq = np.empty((Nn, self.dim), F32)
+        sid_ptr = np.zeros(Nn + 1, np.int64)
+        sids = []
+        for i, n in enumerate(nodes):
+            count[i], mean[i], meanSq[i] = n.count, n.mean, n.meanSq
+            sids.extend(int(s) for s in (n.sentence_id or []))
+            sid_ptr[i + 1] = len(sids)
+        return {"parent": np.asarray(parent, np.int64), "count": count, "mean": mean, "meanSq": meanSq,
+                "sid_ptr": sid_ptr, "sid_list": np.asarray(sids, np.int64)}
+
+    def save_binary(self, path, extra=None):
+        """Write the tree as BFS arrays + header to an .npz (loadable with
+        allow_pickle=False).  The reference's JSON (dump_json) is ~25x larger and
+        needs a Python node object per concept to read back."""
+        arrs = self.to_arrays()
+        head = {"version": self.BINARY_VERSION, "shape": list(self.shape), "prior_var": float(self.prior_var),
+                "use_info": self.use_info, "acuity_cutoff": self.acuity_cutoff, "use_kl": self.use_kl,
+                "alpha": self.alpha}
+        arrs["header"] = np.frombuffer(json.dumps(head).encode(), np.uint8)
+        for k, v in (extra or {}).items():
+            arrs[k] = v
+        with open(path, "wb") as f:
+            np.savez(f, **arrs)
+
+    @staticmethod
+    def read_binary(path):
+        """(header dict, arrays dict) of a save_binary file."""
+        with np.load(path, allow_pickle=False) as z:
+            arrs = {k: z[k] for k in z.files}
+        head = json.loads(bytes(arrs.pop("header")).decode())
+        if head.get("version") != CobwebTree.BINARY_VERSION:
+            raise ValueError(f"unsupported tree binary version {head.get('version')}")
+        return head, arrs
+
+    @classmethod
+    def load_binary(cls, path):
+        head, a = cls.read_binary(path)
+        t = cls.from_arrays(a["parent"], a["count"], a["mean"], a["meanSq"], a["sid_ptr"], a["sid_list"],
+                            prior_var=head["prior_var"])
+        t.use_info, t.acuity_cutoff, t.use_kl, t.alpha = (head["use_info"], head["acuity_cutoff"], head["use_kl"],
+                                                          head["alpha"])
+        return t
+
+    @staticmethod
+    def arrays_to_index_inputs(head, a, n_sentences=None):
+        """Index inputs straight from binary arrays, without node objects (C3+ scale):
+        (mean, var, parent, node_of_sentence); var = compute_var, prior_var if empty."""
+        pv = F32(head["prior_var"])
+        count = a["count"]
+        var = np.empty_like(a["meanSq"])
+        nz = count > 0
+        var[nz] = a["meanSq"][nz] / count[nz, None] + pv
+        var[~nz] = pv
+        sid_ptr, sid_list = a["sid_ptr"], a["sid_list"]
+        n_sent = int(sid_list.max()) + 1 if n_sentences is None and sid_list.size else int(n_sentences or 0)
+        node_of_sentence = np.full(n_sent, -1, np.int64)
+        owner = np.repeat(np.arange(len(count), dtype=np.int64), np.diff(sid_ptr))
+        keep = sid_list < n_sent
+        node_of_sentence[sid_list[keep]] = owner[keep]
+        return a["mean"], var, a["parent"], node_of_sentence
+
     # ---- flattening (CobwebWrapper.build_prediction_index :107-203) ----
     def flatten(self, n_sentences):
         """BFS order (children in list order).  Returns (nodes, parent, mean, var,

@@ -309,6 +309,27 @@ class CobwebWrapper:
             stack.extend(n.children)
         return w
 
+    def save_binary(self, path):
+        """Binary counterpart of dump_json (F2): the tree's BFS arrays plus the
+        sentences (UTF-8 JSON bytes) in one .npz, readable with allow_pickle=False."""
+        sent = np.frombuffer(json.dumps(list(self.sentences)).encode(), np.uint8)
+        self.tree.save_binary(path, extra={"sentences": sent,
+                                           "max_init_search": np.asarray([self.max_init_search], np.int64)})
+
+    @staticmethod
+    def load_binary(path, encode_func=lambda x: x, device=None):
+        head, a = CobwebTree.read_binary(path)
+        sentences = json.loads(bytes(a.pop("sentences")).decode()) if "sentences" in a else []
+        mis = int(a.pop("max_init_search")[0]) if "max_init_search" in a else MAX_INIT_SEARCH
+        t = CobwebTree.from_arrays(a["parent"], a["count"], a["mean"], a["meanSq"], a["sid_ptr"], a["sid_list"],
+                                   prior_var=head["prior_var"])
+        t.use_info, t.acuity_cutoff, t.use_kl, t.alpha = (head["use_info"], head["acuity_cutoff"], head["use_kl"],
+                                                          head["alpha"])
+        w = CobwebWrapper.from_tree(t, sentences, device=device)
+        w.encode_func = encode_func
+        w.max_init_search = mis
+        return w
+
     @classmethod
     def from_tree(cls, tree, sentences, device=None):
         """Wrap an existing CobwebTree (e.g. CobwebTree.from_arrays / from_json)."""
