@@ -189,6 +189,22 @@ int cwq_fit_kl(const float* count, const float* mean, const float* meanSq, int32
 int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_t dim, int32_t dst, int32_t src,
                     const float* x, int32_t* flag, void* stream);
 
+/*
+ * PCA + ICA whitening transform (F4).  Replaces PCAICAWhiteningModel.transform
+ * (src/whitening/pca_ica.py:30-51), the embedding normalisation of the "PCA + ICA"
+ * benchmark rows and of config C5:
+ *   x_pca = ((X - mean) @ comps^T) / denom,   out = x_pca @ unmix^T   (unmix != NULL)
+ *                                             out = x_pca            (unmix == NULL, is_ica=False)
+ *   X      device [n*d_in] fp32          mean   device [d_in]
+ *   comps  device [d_pca*d_in]           denom  device [d_pca] = sqrt(explained_var + eps),
+ *                                               computed by the caller in fp32 like numpy
+ *   unmix  device [d_out*d_pca] or NULL  work   device [n*d_pca] scratch (when unmix)
+ *   out    device [n*d_out] (or [n*d_pca])
+ * fp32 MFMA GEMMs; results equal numpy's fp32 up to the dot-product summation order.
+ */
+int cwq_whiten(const float* X, int64_t n, int32_t d_in, const float* mean, const float* comps, int32_t d_pca,
+               const float* denom, const float* unmix, int32_t d_out, float* out, float* work, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

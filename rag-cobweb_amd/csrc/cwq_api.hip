@@ -1203,3 +1203,17 @@ extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, c
   HIPCHK(launch_welford_groups(X, dim, order, group_ptr, n_groups, count, mean, meanSq, (hipStream_t)stream));
   return CWQ_OK;
 }
+
+// PCA + ICA whitening transform (F4) -- PCAICAWhiteningModel.transform, src/whitening/pca_ica.py:30-51.
+extern "C" int cwq_whiten(const float* X, int64_t n, int32_t d_in, const float* mean, const float* comps,
+                          int32_t d_pca, const float* denom, const float* unmix, int32_t d_out, float* out,
+                          float* work, void* stream) {
+  if (n < 0 || d_in <= 0 || d_pca <= 0 || (unmix && d_out <= 0)) return fail(CWQ_ERR_ARG, "bad whitening shape");
+  if (n == 0) return CWQ_OK;
+  if (!X || !mean || !comps || !denom || !out || (unmix && !work)) return fail(CWQ_ERR_ARG, "NULL argument");
+  hipStream_t s = (hipStream_t)stream;
+  float* pca = unmix ? work : out;
+  HIPCHK(launch_gemm_nt_f32(X, n, d_in, mean, comps, d_pca, denom, pca, s));
+  if (unmix) HIPCHK(launch_gemm_nt_f32(pca, n, d_pca, nullptr, unmix, d_out, nullptr, out, s));
+  return CWQ_OK;
+}

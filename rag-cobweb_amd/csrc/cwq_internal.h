@@ -192,4 +192,8 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
                         hipStream_t s);
 
+// PCA + ICA whitening (cwq_whiten.hip): C[m][n] = sum_k (A[m][k] - ctr[k]) B[n][k] (/ denom[n])
+hipError_t launch_gemm_nt_f32(const float* A, int64_t M, int K, const float* ctr, const float* B, int N,
+                              const float* denom, float* C, hipStream_t s);
+
 }  // namespace cwq
