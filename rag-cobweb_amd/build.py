@@ -30,7 +30,8 @@ def build_library(force=False, verbose=False):
     if not force and not _stale():
         return OUT
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, *[os.path.join(CSRC, s) for s in SOURCES], "-o", OUT + ".tmp"]
+    extra = os.environ.get("CWQ_HIPCC_FLAGS", "").split()   # A/B experiments only
+    cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, *extra, *[os.path.join(CSRC, s) for s in SOURCES], "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

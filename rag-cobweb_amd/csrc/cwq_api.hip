@@ -252,8 +252,11 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   }
   if ((rc = ix->upload(&ix->iso_rf, rf, s))) return rc;
   if ((rc = ix->upload(&ix->iso_tf, tf, s))) return rc;
-  // threshold sample: ~NL_iso/32 rows at a fixed stride, 256 <= S <= 32768
-  int S = (int)std::min<int64_t>(32768, std::max<int64_t>(kFgTile, NLi / 32 / kFgTile * kFgTile));
+  // threshold sample: ~NL_iso/64 rows at a fixed stride, 256 <= S <= 32768 (the filter
+  // phases tighten T afterwards, so a small sample only costs the first phase)
+  const char* sd = getenv("CWQ_FG_SAMPLE_DIV");
+  const int sdiv = sd && atoi(sd) > 0 ? atoi(sd) : 64;
+  int S = (int)std::min<int64_t>(32768, std::max<int64_t>(kFgTile, NLi / sdiv / kFgTile * kFgTile));
   const int stride = std::max(1, NLi / S);
   std::vector<int> srow(round_up(S, kFgTile), -1);
   int ns = 0;
