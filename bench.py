@@ -35,6 +35,15 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (no spars
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def config_label(N, D):
+    """Which BASELINE.json config a run measures (SURVEY §8 shorthand)."""
+    if (N, D) == (1_000_000, 768):
+        return "BASELINE configs[2], C3"
+    if (N, D) == (10_000_000, 1024):
+        return "BASELINE configs[3], C4 per-GPU shard"
+    return "custom size"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -78,20 +87,13 @@ def cpu_baseline(X_host, root_mean, root_var, Q_host, k, sample, ids_gpu):
             "s_per_query": round(sec, 3)}
 
 
-def recall_at_k(X, Q, ids, targets, k, n_eval):
+def recall_at_k(pkg, X, Q, ids, targets, k, n_eval):
     """recall@k of the Fast ranking vs exact brute force (flat-L2 and flat-IP =
-    the reference's FAISS / Torch Dot baselines, benchmark_utils.py:536-614)."""
+    the reference's FAISS / Torch Dot baselines, benchmark_utils.py:536-614), scored in
+    float64 (harness.brute_force_topk(exact=True))."""
     Qe = Q[:n_eval]
-    gt_l2, gt_ip = [], []
-    xn = (X * X).sum(1)
-    for i in range(0, n_eval, 64):
-        q = Qe[i:i + 64]
-        ip = q @ X.T
-        d2 = xn[None, :] - 2 * ip
-        gt_l2.append(torch.topk(-d2, k, dim=1).indices)
-        gt_ip.append(torch.topk(ip, k, dim=1).indices)
-    gt_l2 = torch.cat(gt_l2).cpu().numpy()
-    gt_ip = torch.cat(gt_ip).cpu().numpy()
+    gt_l2 = pkg.harness.brute_force_topk(X, Qe, k, "l2", exact=True).cpu().numpy()
+    gt_ip = pkg.harness.brute_force_topk(X, Qe, k, "ip", exact=True).cpu().numpy()
     got = ids[:n_eval].cpu().numpy()
     r_l2 = np.mean([len(set(a) & set(b)) / k for a, b in zip(got, gt_l2)])
     r_ip = np.mean([len(set(a) & set(b)) / k for a, b in zip(got, gt_ip)])
@@ -218,7 +220,7 @@ def main():
 
     rec_l2 = rec_ip = rec_tgt = None
     if rank == 0 and args.recall_queries > 0:
-        rec_l2, rec_ip, rec_tgt = recall_at_k(X, Q, ids, targets, k, min(args.recall_queries, Qn))
+        rec_l2, rec_ip, rec_tgt = recall_at_k(pkg, X, Q, ids, targets, k, min(args.recall_queries, Qn))
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -235,7 +237,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"Cobweb Fast top-{k}: synthetic flat-synth tree (root + {N} leaves), "
-                                   f"X~N(0,I) {N}x{D} fp32, {Qn} queries/step/GPU (BASELINE configs[2], C3)",
+                                   f"X~N(0,I) {N}x{D} fp32, {Qn} queries/step/GPU ({config_label(N, D)})",
                        "corpus": N, "dim": D, "queries_per_gpu": Qn, "k": k, "tree": "flat-synth",
                        "parallelism": f"query-shard x{world}, index broadcast over RCCL" if world > 1
                        else "single GPU"},

@@ -101,14 +101,35 @@ def evaluate_retrieval_batch(name, queries, target_keys, retrieve_batch, top_k=1
     return m
 
 
-def brute_force_topk(corpus, queries, k, metric="ip", chunk=1024):
-    """Exact top-k by inner product (FAISS IndexFlatIP / Torch Dot) or L2."""
+def brute_force_topk(corpus, queries, k, metric="ip", chunk=1024, exact=False, row_chunk=1 << 20):
+    """Exact top-k by inner product (FAISS IndexFlatIP / Torch Dot) or L2.
+    exact=True scores in float64 over row chunks with a running top-k (the fp32 GEMM
+    of a library may reorder or split the sums; at 10M x 1024 the fp32 ranking of the
+    GEMM kernel torch picks drifted from the exact one)."""
     corpus = torch.as_tensor(corpus, dtype=torch.float32)
     queries = torch.as_tensor(queries, dtype=torch.float32, device=corpus.device)
-    cn = (corpus * corpus).sum(1) if metric == "l2" else None
-    out = []
-    for i in range(0, queries.shape[0], chunk):
-        ip = queries[i:i + chunk] @ corpus.T
-        s = ip if metric == "ip" else 2 * ip - cn[None, :]
-        out.append(torch.topk(s, k, dim=1).indices)
-    return torch.cat(out)
+    if not exact:
+        cn = (corpus * corpus).sum(1) if metric == "l2" else None
+        out = []
+        for i in range(0, queries.shape[0], chunk):
+            ip = queries[i:i + chunk] @ corpus.T
+            s = ip if metric == "ip" else 2 * ip - cn[None, :]
+            out.append(torch.topk(s, k, dim=1).indices)
+        return torch.cat(out)
+    qd = queries.double()
+    best_s = best_i = None
+    for r0 in range(0, corpus.shape[0], row_chunk):
+        c = corpus[r0:r0 + row_chunk].double()
+        s = qd @ c.T
+        if metric == "l2":
+            s = 2 * s - (c * c).sum(1)[None, :]
+        kk = min(k, s.shape[1])
+        ts, ti = torch.topk(s, kk, dim=1)
+        ti = ti + r0
+        if best_s is None:
+            best_s, best_i = ts, ti
+        else:
+            cs, ci = torch.cat([best_s, ts], 1), torch.cat([best_i, ti], 1)
+            best_s, pos = torch.topk(cs, k, dim=1)
+            best_i = torch.gather(ci, 1, pos)
+    return best_i

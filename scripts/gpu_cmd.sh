@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_whitening.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/whiten_tests.log 2>&1; rc=$?; tail -15 gpurun_out/whiten_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u scripts/whiten_probe.py > gpurun_out/whiten_probe.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/whiten_probe.log; exit $rc
+timeout -k 10 600 python -u bench.py --n 10000000 --dim 1024 --queries 12500 --steps 3 --warmup 1 --no-cpu-baseline --recall-queries 256 > gpurun_out/bench_c4.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/bench_c4.log | tail -1; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/bench.log | tail -1; exit $rc

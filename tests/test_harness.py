@@ -48,3 +48,16 @@ def test_brute_force_matches_numpy(pkg):
     np.testing.assert_array_equal(ip, np.argsort(-(Q @ X.T), 1)[:, :5])
     d = ((Q[:, None, :] - X[None]) ** 2).sum(-1)
     np.testing.assert_array_equal(l2, np.argsort(d, 1)[:, :5])
+
+
+def test_brute_force_exact_chunked(pkg):
+    """The float64 row-chunked path gives the exact ranking, chunk boundaries included."""
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((3001, 48)).astype(np.float32)
+    Q = rng.standard_normal((37, 48)).astype(np.float32)
+    Xd, Qd = X.astype(np.float64), Q.astype(np.float64)
+    for metric in ("ip", "l2"):
+        got = pkg.harness.brute_force_topk(X, Q, 7, metric, exact=True, row_chunk=500).numpy()
+        s = Qd @ Xd.T if metric == "ip" else -((Qd[:, None, :] - Xd[None]) ** 2).sum(-1)
+        ref = np.argsort(-s, axis=1, kind="stable")[:, :7]
+        assert np.array_equal(np.sort(got, 1), np.sort(ref, 1)), metric
