@@ -198,7 +198,8 @@ def main():
         # bf16-MFMA candidate filter (cwq_mfma.hip fgemm): 2*D flops per (query, leaf row)
         kern_ms = float(np.mean([t["fgemm_ms"] for t in tms]))
         flops_launch = 2.0 * D * NL * Qn
-        peak, kname, pipe = PEAK_BF16_TFLOPS, "fgemm_kernel (bf16 MFMA filter pass)", "bf16 MFMA dense"
+        peak, kname, pipe = PEAK_BF16_TFLOPS, "fgemm_kernel<0> (bf16 MFMA filter pass)", "bf16 MFMA dense"
+        launches = 3 if NL >= 16 * 256 else 1   # threshold phases over the row tiles (cwq_api.hip)
         phases = {"sample_ms": round(float(np.mean([t["sample_ms"] for t in tms])), 3),
                   "fgemm_ms": round(kern_ms, 3),
                   "rerank_ms": round(float(np.mean([t["rerank_ms"] for t in tms])), 3)}
@@ -207,6 +208,7 @@ def main():
         flops_launch = 4.0 * D * NL * Qn                  # 4*Nn*D per query (leaf rows)
         peak, kname, pipe = PEAK_FP32_TFLOPS, "scan_kernel<ISO,TOPK> (exact fp32 leaf scan)", "fp32 VALU"
         phases = {}
+        launches = 1
     achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
     bytes_q = 8.0 * (N + 1) * D + 8.0 * 2 * N + 4.0 * D + 12.0 * k   # SURVEY §8(d) bytes per query
     traffic = None
@@ -214,6 +216,7 @@ def main():
         try:
             pm = json.load(open(args.pmc_file))
             if pm.get("workload") == [N, D, Qn, k] and pm.get("kernel") == kname.split(" ")[0]:
+                # per step (the launches of one call), like `achieved`
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -244,8 +247,9 @@ def main():
             "roofline": {"bound": "mfma", "pipe": pipe,
                          "achieved": round(achieved_tf, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved_tf / peak, 4), "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kern_ms, 3),
-                         "call_ms": round(call_ms, 3), "flops_per_launch": flops_launch, "phases_ms": phases},
+                         "kernel": kname, "kernel_ms": round(kern_ms, 3), "launches_per_step": launches,
+                         "avg_launch_ms": round(kern_ms / launches, 3),
+                         "call_ms": round(call_ms, 3), "flops_per_step": flops_launch, "phases_ms": phases},
             "filter": {k_: st[k_] for k_ in ("filter_used", "fallback_queries", "candidates", "exact_reranks",
                                               "sample_rows")},
             "hbm_roofline": {"bytes_per_query": bytes_q,

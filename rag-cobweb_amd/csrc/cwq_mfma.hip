@@ -227,6 +227,9 @@ __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __
   }
 }
 
+// MODE 0: filter pass (records), MODE 1: threshold-sample pass (dense lower bounds);
+// separate instantiations so profiles tell them apart and each drops the other's code.
+template <int MODE>
 __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb,
                                                     const FgArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[FLDS];
@@ -296,14 +299,14 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     const int q0 = qt * FT, r0 = rt * FT;
     // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
     TileF tf;
-    if (a.mode == 0) tf = a.tf[rt];
+    if (MODE == 0) tf = a.tf[rt];
     else tf.uniform = 0;
     const bool uni = tf.uniform != 0;
     if (tid < FT) {
       const int q = q0 + tid;
       float4 qi = a.qinfo[q];
       float T = CWQ_INF;
-      if (q < a.nq && a.mode == 0) T = a.T[(size_t)q * a.ldT];
+      if (q < a.nq && MODE == 0) T = a.T[(size_t)q * a.ldT];
       qi.w = T;
       s_qi[tid] = qi;
       float pi = 0.f, qv = CWQ_INF;
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     float* wsc = reinterpret_cast<float*>(smem + ((gs - 1) & (FNBUF - 1)) * FSTAGE) + wave * 1024;
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
-    if (a.mode == 0 && uni) {
+    if (MODE == 0 && uni) {
       bool any = false;
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib)
@@ -423,7 +426,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             const float d0 = wsc[e * 64 + lane];
             const int ql = wq * 128 + ib * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
             const int q = q0 + ql;
-            if (a.mode == 1) {
+            if (MODE == 1) {
               float lo = -CWQ_INF;
               if (usable) {
                 const float4 qi = s_qi[ql];
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         }
     }
   flush:
-    if (a.mode == 0) {
+    if (MODE == 0) {
       // records -> global append buffer, in chunks of kFgChunk slots owned by this
       // workgroup (one atomic per chunk, not per tile)
       __syncthreads();
@@ -510,14 +513,17 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     __syncthreads();   // epilogue LDS reads done before the next setup rewrites them
     if (tid == 0) s_cnt[0] = 0;
   }
-  if (a.mode == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
+  if (MODE == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
 }
 
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s) {
   if (a.DPB % FK != 0 || a.DPB < 3 * FK || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
   if (a.qgroups * a.rgroups != 8) return hipErrorInvalidValue;
   n_wg = std::max(8, n_wg / 8 * 8);
-  hipLaunchKernelGGL(fgemm_kernel, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
+  if (a.mode == 0)
+    hipLaunchKernelGGL(fgemm_kernel<0>, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
+  else
+    hipLaunchKernelGGL(fgemm_kernel<1>, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
   return hipGetLastError();
 }
 

@@ -2,9 +2,9 @@
 
     python scripts/pmc_summary.py gpurun_out/pmc profiles/pmc_r01_fgemm.json [kernel-substring]
 
-Counters are summed over the filter launches of one score_topk call (the fgemm
-dispatches come in groups of 1 + PHASES per call: the threshold-sample launch, then
-the filter phases) and averaged over calls.  FETCH_SIZE is the L2 memory-side read
+Counters are summed over the filter launches of one score_topk call (fgemm_kernel<0>
+dispatches come in groups of PHASES per call; the threshold-sample pass is the
+separate instantiation fgemm_kernel<1>) and averaged over calls.  FETCH_SIZE is the L2 memory-side read
 volume in KB; on gfx950 it reports half the bytes of 16-B-per-lane streaming reads
 (global_load and global_load_lds alike, MI355X_MICROARCH.md §HBM), so bytes =
 2 * 1024 * FETCH_SIZE; Infinity-Cache hits are counted too.  GRBM_GUI_ACTIVE / 8
@@ -17,14 +17,15 @@ import os
 import sys
 
 pmc_dir, out = sys.argv[1:3]
-HOT = sys.argv[3] if len(sys.argv) > 3 else "fgemm_kernel"
+HOT = sys.argv[3] if len(sys.argv) > 3 else "fgemm_kernel<0>"
 PHASES = int(os.environ.get("PMC_PHASES", "3"))
 agg, durs = collections.defaultdict(list), []
 for d in sorted(glob.glob(os.path.join(pmc_dir, "p*"))):
     f = os.path.join(d, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
-    rows = [r for r in csv.DictReader(open(f)) if HOT in r["Kernel_Name"]]
+    alt = HOT.replace("<0>", "ILi0E").replace("<1>", "ILi1E")   # mangled form in some traces
+    rows = [r for r in csv.DictReader(open(f)) if HOT in r["Kernel_Name"] or alt in r["Kernel_Name"]]
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     for r in rows:
@@ -32,9 +33,9 @@ for d in sorted(glob.glob(os.path.join(pmc_dir, "p*"))):
         per[did][r["Counter_Name"]] += float(r["Counter_Value"])
         dur[did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     ids = sorted(per)
-    G = 1 + PHASES
+    G = PHASES
     for c0 in range(0, len(ids) - G + 1, G):
-        grp = ids[c0 + 1:c0 + G]          # skip the sample launch
+        grp = ids[c0:c0 + G]
         tot = collections.defaultdict(float)
         for did in grp:
             for k, v in per[did].items():
