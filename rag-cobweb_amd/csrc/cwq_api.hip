@@ -104,6 +104,7 @@ struct cwq_index {
   uint16_t* iso_Mb = nullptr;
   RowF* iso_rf = nullptr;
   TileF* iso_tf = nullptr;
+  std::vector<int> tile_uni_prefix;   // prefix counts of uniform row tiles (all_uniform per launch range)
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
   int* samp_rows = nullptr;
   uint16_t* iso_Sb = nullptr;
@@ -252,6 +253,8 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   }
   if ((rc = ix->upload(&ix->iso_rf, rf, s))) return rc;
   if ((rc = ix->upload(&ix->iso_tf, tf, s))) return rc;
+  ix->tile_uni_prefix.assign(n_rt + 1, 0);
+  for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform ? 1 : 0);
   // threshold sample: ~NL_iso/64 rows at a fixed stride, 256 <= S <= 32768 (the filter
   // phases tighten T afterwards, so a small sample only costs the first phase)
   const char* sd = getenv("CWQ_FG_SAMPLE_DIV");
@@ -868,6 +871,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         for (int ph = 0; ph < nph; ++ph) {
           g.rt_off = cuts[ph];
           g.n_rt = cuts[ph + 1] - cuts[ph];
+          g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt;
           HIPCHK(hipMemsetAsync(gctr, 0, 64, s));
           if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
           HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));

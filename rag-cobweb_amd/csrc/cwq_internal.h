@@ -151,6 +151,7 @@ struct TileF {
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
   int rt_off;                             // first row tile of this launch (filter phases)
+  int all_uniform;                        // every row tile of the launch is uniform (TileF)
   int qgroups, rgroups;                   // XCD split (qgroups * rgroups == 8)
   int order;                              // tile order: 0 static q-fastest, 1 static r-fastest, 2 dynamic
   int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)

@@ -229,7 +229,9 @@ __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __
 
 // MODE 0: filter pass (records), MODE 1: threshold-sample pass (dense lower bounds);
 // separate instantiations so profiles tell them apart and each drops the other's code.
-template <int MODE>
+// ALLUNI: every row tile of the launch is uniform (flat trees): the per-element generic
+// bound path is compiled out.
+template <int MODE, bool ALLUNI>
 __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb,
                                                     const FgArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[FLDS];
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     TileF tf;
     if (MODE == 0) tf = a.tf[rt];
     else tf.uniform = 0;
-    const bool uni = tf.uniform != 0;
+    const bool uni = ALLUNI || tf.uniform != 0;
     if (tid < FT) {
       const int q = q0 + tid;
       float4 qi = a.qinfo[q];
@@ -520,10 +522,15 @@ hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_w
   if (a.DPB % FK != 0 || a.DPB < 3 * FK || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
   if (a.qgroups * a.rgroups != 8) return hipErrorInvalidValue;
   n_wg = std::max(8, n_wg / 8 * 8);
-  if (a.mode == 0)
-    hipLaunchKernelGGL(fgemm_kernel<0>, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
+  if (a.mode == 1)
+    hipLaunchKernelGGL((fgemm_kernel<1, false>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
+                       (const __bf16*)Mb, a);
+  else if (a.all_uniform)
+    hipLaunchKernelGGL((fgemm_kernel<0, true>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
+                       (const __bf16*)Mb, a);
   else
-    hipLaunchKernelGGL(fgemm_kernel<1>, dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb, (const __bf16*)Mb, a);
+    hipLaunchKernelGGL((fgemm_kernel<0, false>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
+                       (const __bf16*)Mb, a);
   return hipGetLastError();
 }
 
