@@ -181,7 +181,7 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
                  const std::vector<int>& row_par, const std::vector<int>& row_flags, hipStream_t s) {
   int rc;
   const int DP = ix->DP, D = ix->D, NLi = ix->NL_iso;
-  ix->DPB = (int)std::max<int64_t>(96, round_up(D, 32));   // fgemm: 32-deep stages, >= 3 of them
+  ix->DPB = fgemm_dpb(D);   // whole fgemm stages (cwq_mfma.hip)
   const int DPB = ix->DPB;
   ix->ld_f = round_up(NLi, kFgTile);
   const int64_t ld = ix->ld_f;

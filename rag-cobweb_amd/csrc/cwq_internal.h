@@ -182,6 +182,7 @@ hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int
 hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
                              float4* qinfo, hipStream_t s);
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s);
+int fgemm_dpb(int D);   // padded bf16 operand width the fgemm build needs
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);

@@ -44,6 +44,7 @@ namespace cwq {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -209,6 +210,16 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
   return nq_l * nr_l;
 }
 
+#ifndef FG_M16
+#define FG_M16 1
+#endif
+// 16-B chunk position of logical chunk 0 in row r of a stage image (a permutation of the
+// row's 4 chunks, XORed with the chunk index).  Chosen per MFMA shape so that the
+// ds_read_b128 fragment reads of a wave are bank-conflict free:
+//   32x32x16: lane l reads row l&31, chunk 2kk + (l>>5)      -> f = (r>>2)&3
+//   16x16x32: lane l reads row l&15, chunk l>>4              -> f = (4 - ((r>>2)&3))&3
+__device__ __forceinline__ int fg_swz(int r) { return FG_M16 ? (4 - ((r >> 2) & 3)) & 3 : (r >> 2) & 3; }
+
 // one K stage (32 deep) of both operands into an LDS stage buffer: 4 glds per wave.
 // Image: [256 rows][64 B] per operand; 16-B chunk c of row r sits at position
 // c ^ ((r >> 2) & 3) (conflict-free ds_read_b128 fragment reads); the LDS side of a
@@ -218,7 +229,7 @@ __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = wave * 32 + i * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ ((row >> 2) & 3);
+    const int c = (lane & 3) ^ fg_swz(row);
     const __bf16* ga = Xb + (size_t)(q0 + row) * DPB + k0 + c * 8;
     const __bf16* gb = Mb + (size_t)(r0 + row) * DPB + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(sb + (wave * 32 + i * 16) * 64), 16, 0, 0);
@@ -254,10 +265,15 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   int* s_cnt = reinterpret_cast<int*>(smem + OFF_CNT);
   // fragment read offsets (bytes) within an operand image; the swizzle term is the
   // same for every 32-row block, so one per-lane value per k-substep
-  const int fsw = (l31 >> 2) & 3;
+#if FG_M16
+  const int r16 = lane & 15, c16 = lane >> 4;
+  const int foff16 = r16 * 64 + ((c16 ^ fg_swz(r16)) << 4);
+#else
+  const int fsw = fg_swz(l31);
   int foff[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) foff[kk] = l31 * 64 + (((2 * kk + h) ^ fsw) << 4);
+#endif
 
   // stage ring: stages are numbered over this workgroup's whole tile sequence, so the
   // next tile's first stages are in flight during the current tile's last steps
@@ -296,7 +312,11 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     s_cnt[1] = -1;   // owned chunk
     s_cnt[2] = 0;    // its fill
   }
+#if FG_M16
+  f32x4 acc[8][4];
+#else
   f32x16 acc[4][2];
+#endif
   for (;;) {
     const int q0 = qt * FT, r0 = rt * FT;
     // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
@@ -325,16 +345,77 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       s_pi[tid] = pi;
       s_qv[tid] = qv;
     }
+#if FG_M16
+    float R0[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const int r = r0 + wr * 64 + jb * 16 + r16;
+      R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
+    }
+#else
     float R0[2];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
       const int r = r0 + wr * 64 + jb * 32 + l31;
       R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
     }
+#endif
     if (dyn && tid == 0) s_cnt[8] = atomicAdd(&a.tctr[xcd], 1);   // the tile after this one
     __syncthreads();   // stage 0 landed, setup visible
     if (dyn) next_i = s_cnt[8];
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
+#if FG_M16
+    // 16x16x32 layout: acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
+#pragma unroll
+    for (int ib = 0; ib < 8; ++ib) {
+      const float4 qv4 = uni ? *reinterpret_cast<const float4*>(s_qv + wq * 128 + ib * 16 + 4 * c16)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        acc[ib][jb][0] = R0[jb] - qv4.x;
+        acc[ib][jb][1] = R0[jb] - qv4.y;
+        acc[ib][jb][2] = R0[jb] - qv4.z;
+        acc[ib][jb][3] = R0[jb] - qv4.w;
+      }
+    }
+    // ---- K loop: one 32-deep v_mfma_f32_16x16x32_bf16 substep per stage; the barrier
+    // sits between the two halves of the MFMAs (query blocks 0-3 | 4-7), the next
+    // stage's fragments are read after it, under the second half.  Two fragment sets,
+    // the loop unrolled by two so they alternate without copies.
+    bf16x8 xa0[8], xb0[4], xa1[8], xb1[4];
+    auto load16 = [&](bf16x8* fa, bf16x8* fb, const char* sb) {
+      const char* sA = sb + wq * 128 * 64 + foff16;
+      const char* sB = sb + FT * 64 + wr * 64 * 64 + foff16;
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib) fa[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 1024);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) fb[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 1024);
+    };
+    auto mfma16 = [&](const bf16x8* fa, const bf16x8* fb, int ib0) {
+#pragma unroll
+      for (int ib = ib0; ib < ib0 + 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ib], fb[jb], acc[ib][jb], 0, 0, 0);
+    };
+    auto step16 = [&](const bf16x8* ca, const bf16x8* cb, bf16x8* na, bf16x8* nb) {
+      issue_next();
+      mfma16(ca, cb, 0);
+      ++gs;
+      const int n_out = issued - gs - 1;
+      if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load16(na, nb, smem + (gs & (FNBUF - 1)) * FSTAGE);   // unconditional: keeps lgkmcnt counted
+      mfma16(ca, cb, 4);
+    };
+    load16(xa0, xb0, smem + (gs & (FNBUF - 1)) * FSTAGE);
+    for (int t = 0; t < nk; t += 2) {
+      step16(xa0, xb0, xa1, xb1);
+      step16(xa1, xb1, xa0, xb0);
+    }
+#else
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
@@ -380,10 +461,54 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       load_frags(fa0, fb0, smem + (gs & (FNBUF - 1)) * FSTAGE, 0);
       mfma8(fa1, fb1);
     }
+#endif
     // ---- epilogue ----
     // The stage buffer just consumed is free until the next tile's first K step
     // re-issues it: 4 KiB per wave of it hold one 32x32 block for the scalar paths.
     float* wsc = reinterpret_cast<float*>(smem + ((gs - 1) & (FNBUF - 1)) * FSTAGE) + wave * 1024;
+#if FG_M16
+    // blocks: jb (16 rows) x half (query blocks 0-3 / 4-7): 16 values per lane
+    bool anyb[4][2];
+    if (a.dbg & 2) goto flush;
+    if (MODE == 0 && uni) {
+      bool any = false;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float m = -CWQ_INF;
+#pragma unroll
+          for (int ib = hf * 4; ib < hf * 4 + 4; ++ib)
+            m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fmaxf(acc[ib][jb][0], acc[ib][jb][1]),
+                                                   __builtin_fmaxf(acc[ib][jb][2], acc[ib][jb][3])));
+          anyb[jb][hf] = __ballot(m >= 0.f) != 0;
+          any = any || anyb[jb][hf];
+        }
+      if (!any) goto flush;
+    } else {
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) anyb[jb][0] = anyb[jb][1] = true;
+    }
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      if (!anyb[jb][0] && !anyb[jb][1]) continue;
+      const int r = r0 + wr * 64 + jb * 16 + r16;
+      const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
+      const RowF f = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+      const bool usable = f.par >= -1;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if (!anyb[jb][hf]) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wsc[(k * 4 + j) * 64 + lane] = acc[hf * 4 + k][jb][j];
+#pragma unroll 1
+        for (int e = 0; e < 16; ++e) {
+          const float d0 = wsc[e * 64 + lane];
+          const int ql = wq * 128 + (hf * 4 + (e >> 2)) * 16 + 4 * c16 + (e & 3);
+          const int q = q0 + ql;
+#else
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
     if (MODE == 0 && uni) {
@@ -428,6 +553,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             const float d0 = wsc[e * 64 + lane];
             const int ql = wq * 128 + ib * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
             const int q = q0 + ql;
+#endif
             if (MODE == 1) {
               float lo = -CWQ_INF;
               if (usable) {
@@ -518,8 +644,17 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   if (MODE == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
 }
 
+// Padded bf16 operand width: whole stages, an even number of them for the 16x16x32
+// loop (unrolled by two), at least the ring's prefetch depth.
+int fgemm_dpb(int D) {
+  const int g = FG_M16 ? 2 * FK : FK;
+  const int r = (D + g - 1) / g * g;
+  const int lo = FG_M16 ? 4 * FK : 3 * FK;
+  return r > lo ? r : lo;
+}
+
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s) {
-  if (a.DPB % FK != 0 || a.DPB < 3 * FK || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
+  if (a.DPB != fgemm_dpb(a.DPB) || a.n_qt <= 0 || a.n_rt <= 0) return hipErrorInvalidValue;
   if (a.qgroups * a.rgroups != 8) return hipErrorInvalidValue;
   n_wg = std::max(8, n_wg / 8 * 8);
   if (a.mode == 1)

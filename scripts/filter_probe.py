@@ -24,11 +24,18 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1")
+    ap.add_argument("--clusters", type=int, default=0, help="0: flat tree; G: root -> G random clusters -> leaves")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
-    fs = pkg.synth.flat_synth(X)
+    if args.clusters:
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        labels = torch.randint(0, args.clusters, (args.n,), generator=g, device=dev)
+        fs = pkg.synth.two_level_synth(X, labels)
+    else:
+        fs = pkg.synth.flat_synth(X)
     ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)
     del fs
     Q, _ = pkg.synth.synthetic_queries(X, args.queries, seed=1)
