@@ -560,6 +560,14 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
 // Internal nodes: raw sums -> P (path prefix), BF (bottleneck), LPF (full lp).
 int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   if (ix->NI == 0) return CWQ_OK;
+  const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
+  if (ix->NI <= kWave) {   // a few internal nodes: one wave per query, same arithmetic
+    HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, ix->NI, ix->DP, c.nq, c.S_int, ix->NI, s));
+    for (auto& lv : ix->levels)
+      HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
+                                 dfull, c.P, c.BF, c.LPF, s));
+    return CWQ_OK;
+  }
   ScanArgs a = base_args(ix, c);
   const int kl = 64, tq = scan_tq(kl);
   a.ld = ix->ld_int;
@@ -572,7 +580,6 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   a.out = c.S_int;
   a.ldo = ix->NI;
   HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
-  const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   for (auto& lv : ix->levels)
     HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
                                dfull, c.P, c.BF, c.LPF, s));
@@ -672,8 +679,8 @@ namespace {
 
 constexpr int kFiltMinRows = 16384;   // automatic mode: below this the exact scan is as fast
 constexpr int kFiltMaxK = 64;         // the filter serves the list-based top-k path (k <= 64)
-constexpr int kFgRecPerQ = 1024;      // candidate-record slots per query (append buffer)
-constexpr int kFgDirPerQ = 1024;      // direct-record slots per query (tiles past kFgCap)
+constexpr int kFgRecPerQ = 512;       // candidate-record slots per query (append buffer)
+constexpr int kFgDirPerQ = 256;       // direct-record slots per query (tiles past kFgCap)
 
 bool use_filter(const cwq_index* ix, int k) {
   if (k > kFiltMaxK || ix->NL_iso == 0 || !ix->iso_Mb) return false;
@@ -755,7 +762,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int n_rts = filt ? ix->ld_s / kFgTile : 0;
   // per query: bf16 query, info, sample bounds, threshold list, candidate lists, flags, records
   const size_t filt_q = filt ? (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
-                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64
+                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256
                              : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
@@ -808,7 +815,9 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         int* crow = b.take<int>((size_t)nqf * kFgCapQ);
         float* cu = b.take<float>((size_t)nqf * kFgCapQ);
         float* cl = b.take<float>((size_t)nqf * kFgCapQ);
-        const int64_t rec_cap = round_up((int64_t)nqf * kFgRecPerQ, kFgChunk);
+        // every workgroup holds one partly filled chunk at a time: keep room for two per workgroup
+        const int64_t rec_cap = round_up(std::max<int64_t>((int64_t)nqf * kFgRecPerQ, (int64_t)2 * ix->cus * kFgChunk),
+                                         kFgChunk);
         int4* rec = b.take<int4>((size_t)rec_cap);
         int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
         int* gctr = b.take<int>(64);

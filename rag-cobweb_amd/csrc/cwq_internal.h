@@ -103,6 +103,8 @@ int scan_lists_per_slab(int kl);     // partial top-k lists a workgroup writes p
 int scan_xcd_map();                  // XCD-aware block mapping (CWQ_XCD_MAP, default 1)
 int scan_wgs_per_cu(int kl);         // resident workgroups per CU (occupancy query, cached)
 
+hipError_t launch_int_small(const float* X, const float* A, const float* B, int64_t ld, int NI, int DP, int nq,
+                            float* out, int64_t ldo, hipStream_t s);
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
                                float* LPF, hipStream_t s);
