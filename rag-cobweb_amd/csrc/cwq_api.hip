@@ -848,10 +848,13 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.n_rt = n_rts;
         g.nrows = ix->ld_s;
         g.rowmap = ix->samp_rows;
+        // large samples: lower bounds reduced to maxima over groups of 4 rows in the
+        // kernel (fgemm_kernel<1>); small ones keep one value per row so that K groups exist
         g.lb = lb;
-        g.ldlb = ix->ld_s;
+        g.lbg = (FG_M16 && ix->n_samp >= 64 * K) ? 4 : 1;
+        g.ldlb = ix->ld_s / g.lbg;
         HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
-        HIPCHK(launch_select(lb, ix->ld_s, nqc, ix->ld_s, K, tl, tr, s));
+        HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
         // 2. filter passes over row-tile phases (1/16, 3/16, 12/16 of the rows); after
         // each phase the candidates go to per-query lists and T[q] is raised to the K-th
         // largest candidate lower bound, so later phases emit fewer candidates

@@ -150,6 +150,11 @@ struct TileF {
   float beta_max, delta_max;
   float pad0, pad1;
 };
+// fgemm MFMA shape: 1 = v_mfma_f32_16x16x32_bf16 (default), 0 = 32x32x16 (A/B builds)
+#ifndef FG_M16
+#define FG_M16 1
+#endif
+
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
   int rt_off;                             // first row tile of this launch (filter phases)
@@ -169,6 +174,7 @@ struct FgArgs {
   float gamma, eps_n, slack;              // error-bound constants (cwq_mfma.hip header)
   float* lb;                              // sample: [nq_pad][ldlb]
   int64_t ldlb;
+  int lbg;                                // sample: rows per lower-bound group (1 or 4)
   int4* rec;                              // filter: appended records {q, row, u, l}
   int64_t rec_cap;                        // record slots (a multiple of kFgChunk)
   int* gctr;                              // [0] chunks claimed, [1] direct records (zeroed before the launch)

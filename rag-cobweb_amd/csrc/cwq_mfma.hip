@@ -210,9 +210,6 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
   return nq_l * nr_l;
 }
 
-#ifndef FG_M16
-#define FG_M16 1
-#endif
 #ifndef FG_PRIO
 #define FG_PRIO 0
 #endif
@@ -497,6 +494,42 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // blocks: jb (16 rows) x half (query blocks 0-3 / 4-7): 16 values per lane
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
+    if (MODE == 1 && a.lbg == 4) {
+      // sample pass: lower bounds reduced to row groups of 4 -- rows r16 + 16 jb of this
+      // wave's 64-row block, all in one lane -- before the store.  The K-th largest group
+      // maximum is still <= the K-th largest row lower bound (distinct groups are
+      // distinct rows), and the bounds array and its select shrink 4x.
+      RowF f[4];
+      float pin[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int r = r0 + wr * 64 + jb * 16 + r16;
+        const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
+        f[jb] = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+        pin[jb] = f[jb].invL;
+      }
+      const int g = (r0 + wr * 64) / 4 + r16;
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ql = wq * 128 + ib * 16 + 4 * c16 + j;
+          const int q = q0 + ql;
+          const float4 qi = s_qi[ql];
+          float m = -CWQ_INF;
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb) {
+            if (f[jb].par < -1) continue;
+            const float pi = (f[jb].par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + f[jb].par] * pin[jb] : 0.f;
+            const float d0 = acc[ib][jb][j];
+            float u, lo;
+            fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f[jb], pi, a.eps_n, a.slack, u, lo);
+            m = __builtin_fmaxf(m, lo);
+          }
+          a.lb[(size_t)q * a.ldlb + g] = m;
+        }
+      goto flush;
+    }
     if (MODE == 0 && uni) {
       bool any = false;
 #pragma unroll
