@@ -54,19 +54,24 @@ class CwqError(RuntimeError):
         self.rc = rc
 
 
+def load_library(path):
+    """A configured CDLL for a libcwq build at ``path``."""
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build it with __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
     """Load libcwq.so (once).  Raises ImportError when it is not built."""
     global _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise ImportError(f"{LIB_PATH} is missing: build it with __graft_entry__.build()")
-            L = ctypes.CDLL(LIB_PATH)
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(L, name)
-                fn.restype = res
-                fn.argtypes = args
-            _lib = L
+            _lib = load_library(LIB_PATH)
     return _lib
 
 

@@ -46,7 +46,7 @@ class CobwebIndex:
 
     def __init__(self, mean, var, parent, node_of_sentence, level_weights=None, device=None):
         self.device = _dev(device)
-        L = lib()
+        L = self._L = lib()   # the handle belongs to the library that created it
         mean = torch.as_tensor(mean, dtype=torch.float32).to(self.device).contiguous()
         var = torch.as_tensor(var, dtype=torch.float32).to(self.device).contiguous()
         if mean.shape != var.shape or mean.dim() != 2:
@@ -69,18 +69,18 @@ class CobwebIndex:
 
     def _info(self):
         out = np.zeros(8, np.int64)
-        check(lib().cwq_index_info(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        check(self._L.cwq_index_info(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         keys = ["n_nodes", "dim", "n_sent", "internal_nodes", "leaf_rows", "isotropic_rows", "max_depth",
                 "device_bytes"]
         return dict(zip(keys, (int(v) for v in out)))
 
     def set_timing(self, enable=True):
-        check(lib().cwq_set_timing(self._h, int(bool(enable))))
+        check(self._L.cwq_set_timing(self._h, int(bool(enable))))
 
     def last_timing(self):
         """Phase times (ms) of the last score_topk call, from HIP events on its stream."""
         out = np.zeros(8, np.float32)
-        check(lib().cwq_last_timing(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        check(self._L.cwq_last_timing(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"leaf_scan_ms": float(out[0]), "internal_ms": float(out[1]), "merge_ms": float(out[2]),
                 "call_ms": float(out[3]), "leaf_scan_launches": int(out[4]), "sample_ms": float(out[5]),
                 "fgemm_ms": float(out[6]), "rerank_ms": float(out[7])}
@@ -88,17 +88,17 @@ class CobwebIndex:
     def set_filter(self, mode):
         """Isotropic-row strategy of score_topk: -1 automatic, 0 exact fp32 scan,
         1 bf16-MFMA candidate filter + exact rerank (k <= 64).  Results are identical."""
-        check(lib().cwq_set_filter(self._h, int(mode)))
+        check(self._L.cwq_set_filter(self._h, int(mode)))
 
     def last_stats(self):
         out = np.zeros(6, np.int64)
-        check(lib().cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        check(self._L.cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"filter_queries": int(out[0]), "fallback_queries": int(out[1]), "filter_used": bool(out[2]),
                 "candidates": int(out[3]), "exact_reranks": int(out[4]), "sample_rows": int(out[5])}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
-            lib().cwq_index_destroy(self._h)
+            self._L.cwq_index_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -123,7 +123,7 @@ class CobwebIndex:
         ids = torch.empty((nq, k), dtype=torch.int64, device=self.device)
         scores = torch.empty((nq, k), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
-            check(lib().cwq_score_topk(self._h, _ptr(q), nq, int(k), _ptr(ids), _ptr(scores),
+            check(self._L.cwq_score_topk(self._h, _ptr(q), nq, int(k), _ptr(ids), _ptr(scores),
                                        _stream(self.device)))
         return ids, scores
 
@@ -132,7 +132,7 @@ class CobwebIndex:
         q = self._queries(q)
         out = torch.empty((q.shape[0], self.n_sent), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
-            check(lib().cwq_rank_scores(self._h, _ptr(q), q.shape[0], _ptr(out), _stream(self.device)))
+            check(self._L.cwq_rank_scores(self._h, _ptr(q), q.shape[0], _ptr(out), _stream(self.device)))
         return out
 
     def node_logprob(self, q, full=False):
@@ -140,7 +140,7 @@ class CobwebIndex:
         q = self._queries(q)
         out = torch.empty((q.shape[0], self.n_nodes), dtype=torch.float32, device=self.device)
         with torch.cuda.device(self.device):
-            check(lib().cwq_node_logprob(self._h, _ptr(q), q.shape[0], int(bool(full)), _ptr(out),
+            check(self._L.cwq_node_logprob(self._h, _ptr(q), q.shape[0], int(bool(full)), _ptr(out),
                                          _stream(self.device)))
         return out
 
@@ -154,7 +154,7 @@ class CobwebIndex:
         calls = torch.empty(nq, dtype=torch.int64, device=self.device)
         mx = int(min(max_nodes, 2 ** 62)) if max_nodes != float("inf") else 2 ** 62
         with torch.cuda.device(self.device):
-            check(lib().cwq_categorize(self._h, _ptr(q), nq, int(k), mx, _ptr(nodes), _ptr(found), _ptr(calls),
+            check(self._L.cwq_categorize(self._h, _ptr(q), nq, int(k), mx, _ptr(nodes), _ptr(found), _ptr(calls),
                                        _stream(self.device)))
         return nodes, found, calls
 

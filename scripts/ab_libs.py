@@ -1,0 +1,76 @@
+"""In-process A/B of libcwq builds on the bench workload (flat-synth N x D, Q queries).
+
+Each library gets its own index over the same data; the builds then run in
+interleaved rounds (A B C A B C ...), so clock/DVFS drift hits every arm alike.
+Reports per-arm median call time and median summed fgemm launch time, and checks
+that every arm returns the same ids/scores.  GPU only.
+
+    python scripts/ab_libs.py --libs rag-cobweb_amd/libcwq.so,rag-cobweb_amd/libcwq_b.so
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cobweb_pkg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--queries", type=int, default=10_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=6)
+    args = ap.parse_args()
+    pkg = cobweb_pkg.load()
+    L = pkg._lib
+    dev = torch.device("cuda", 0)
+    X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
+    fs = pkg.synth.flat_synth(X)
+    Q, _ = pkg.synth.synthetic_queries(X, args.queries, seed=1)
+    del X
+    paths = args.libs.split(",")
+    arms = []
+    for p in paths:
+        L._lib = L.load_library(os.path.abspath(p))
+        ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)
+        ix.set_filter(1)
+        ix.score_topk(Q, args.k)
+        arms.append(ix)
+    del fs
+    torch.cuda.empty_cache()
+    call = {p: [] for p in paths}
+    fg = {p: [] for p in paths}
+    ref = None
+    for r in range(args.rounds):
+        for p, ix in zip(paths, arms):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ids, sc = ix.score_topk(Q, args.k)
+            torch.cuda.synchronize()
+            call[p].append((time.perf_counter() - t0) * 1e3)
+            ix.set_timing(True)
+            ix.score_topk(Q, args.k)
+            fg[p].append(ix.last_timing()["fgemm_ms"])
+            ix.set_timing(False)
+            if ref is None:
+                ref = (ids.cpu(), sc.cpu())
+            elif not (torch.equal(ref[0], ids.cpu()) and torch.equal(ref[1], sc.cpu())):
+                print(f"MISMATCH {p} round {r}", flush=True)
+        print(f"round {r}: " + "  ".join(f"{os.path.basename(p)} {call[p][-1]:.2f}/{fg[p][-1]:.3f}" for p in paths),
+              flush=True)
+    base = statistics.median(fg[paths[0]])
+    for p in paths:
+        mc, mf = statistics.median(call[p]), statistics.median(fg[p])
+        print(f"{os.path.basename(p)}: call {mc:.3f} ms ({args.queries / mc * 1e3:.0f} q/s)  fgemm {mf:.3f} ms "
+              f"(x{base / mf:.3f} vs first)  min {min(fg[p]):.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
