@@ -275,6 +275,19 @@ __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __
 #endif
 }
 
+// A tile's TileF (wave-uniform) through the constant address space: scalar loads,
+// counted by lgkmcnt, so they never wait behind the LDS-DMA on the vector counter.
+__device__ __forceinline__ TileF fg_tile_const(const TileF* p, int i) {
+  static_assert(sizeof(TileF) == 32, "TileF is 8 dwords");
+  typedef const __attribute__((address_space(4))) int* cip;
+  const cip src = (cip)(uintptr_t)(p + i);
+  TileF t;
+  int* d = reinterpret_cast<int*>(&t);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = src[k];
+  return t;
+}
+
 // MODE 0: filter pass (records), MODE 1: threshold-sample pass (dense lower bounds);
 // separate instantiations so profiles tell them apart and each drops the other's code.
 // ALLUNI: every row tile of the launch is uniform (flat trees): the per-element generic
@@ -329,7 +342,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   if (dyn) {
     if (tid == 0) s_cnt[8] = atomicAdd(&a.tctr[xcd], 1);
     __syncthreads();
-    i = s_cnt[8];
+    i = __builtin_amdgcn_readfirstlane(s_cnt[8]);
     if (i >= ntl) return;
   }
   int next_i = dyn ? ntl : i + nw_x;   // dynamic: claimed one tile ahead
@@ -390,29 +403,24 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     const int q0 = qt * FT, r0 = rt * FT;
     // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
     TileF tf;
-    if (MODE == 0) tf = a.tf[rt];
+    if (MODE == 0) tf = fg_tile_const(a.tf, rt);
     else tf.uniform = 0;
     const bool uni = ALLUNI || tf.uniform != 0;
+    // all setup loads are issued before any of them is used, so the tile pays one
+    // memory round trip (per-query terms, then per-row terms below)
+    int claimv = 0;   // the tile after this one (when not claimed ahead): in flight with the loads
+    if (dyn && tid == 0 && !claim_pend) {
+      int z;   // opaque zero: a divergent address keeps the atomic optimizer from waiting on the spot
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      claimv = atomicAdd(a.tctr + xcd + z, 1);
+    }
+    const int qs = q0 + tid;
+    float4 qi = make_float4(0.f, 0.f, 0.f, 0.f);
+    float Tq = CWQ_INF, Pq = 0.f;
     if (tid < FT) {
-      const int q = q0 + tid;
-      float4 qi = a.qinfo[q];
-      float T = CWQ_INF;
-      if (q < a.nq && MODE == 0) T = a.T[(size_t)q * a.ldT];
-      qi.w = T;
-      s_qi[tid] = qi;
-      float pi = 0.f, qv = CWQ_INF;
-      if (uni) {
-        pi = tf.par >= 0 && q < a.nq ? a.P[(size_t)q * a.ldP + tf.par] * tf.invL : 0.f;
-        if (q < a.nq && T > -CWQ_INF) {   // T = +inf / NaN / -inf: never a candidate here
-          const float tpg = (T - pi) / tf.g;
-          float v = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x + tpg - a.slack * fabsf(pi) / tf.g -
-                    qi.y * tf.beta_max - qi.z * tf.delta_max;
-          v -= 4.f * a.gamma * (fabsf(v) + qi.x + fabsf(tpg) + fabsf(pi) / tf.g);
-          qv = v == v ? v : CWQ_INF;
-        }
-      }
-      s_pi[tid] = pi;
-      s_qv[tid] = qv;
+      qi = a.qinfo[qs];
+      if (qs < a.nq && MODE == 0) Tq = a.T[(size_t)qs * a.ldT];
+      if (uni && tf.par >= 0 && qs < a.nq) Pq = a.P[(size_t)qs * a.ldP + tf.par];
     }
 #if FG_M16
     float R0[4];
@@ -429,12 +437,30 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
     }
 #endif
+    if (tid < FT) {
+      const float T = Tq;
+      qi.w = T;
+      s_qi[tid] = qi;
+      float pi = 0.f, qv = CWQ_INF;
+      if (uni) {
+        pi = Pq * tf.invL;
+        if (qs < a.nq && T > -CWQ_INF) {   // T = +inf / NaN / -inf: never a candidate here
+          const float tpg = (T - pi) / tf.g;
+          float v = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x + tpg - a.slack * fabsf(pi) / tf.g -
+                    qi.y * tf.beta_max - qi.z * tf.delta_max;
+          v -= 4.f * a.gamma * (fabsf(v) + qi.x + fabsf(tpg) + fabsf(pi) / tf.g);
+          qv = v == v ? v : CWQ_INF;
+        }
+      }
+      s_pi[tid] = pi;
+      s_qv[tid] = qv;
+    }
     // the tile after this one: claimed here for the first tile; afterwards its claim
     // was issued during the previous tile's K loop (its latency hidden there; the
     // return is drained by this barrier's vmcnt(0), which waits for stage 0 anyway)
-    if (dyn && tid == 0) s_cnt[8] = claim_pend ? claim : atomicAdd(&a.tctr[xcd], 1);
+    if (dyn && tid == 0) s_cnt[8] = claim_pend ? claim : claimv;
     __syncthreads();   // stage 0 landed, setup visible
-    if (dyn) next_i = s_cnt[8];
+    if (dyn) next_i = __builtin_amdgcn_readfirstlane(s_cnt[8]);   // uniform: scalar tile loads
     claim_pend = false;
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
 #if FG_M16
