@@ -233,8 +233,9 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   std::vector<TileF> tf(n_rt);
   for (int t = 0; t < n_rt; ++t) {
     TileF& T = tf[t];
-    T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, 0.f, 0.f};
-    bool first = true;
+    T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, -1, 0.f};
+    bool first = true, same_par = true;
+    int plo = INT32_MAX, phi = -1;
     for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
       if (rf[r].par < -1) continue;
       const double g = gr[r];
@@ -244,17 +245,31 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
         T.invL = rf[r].invL;
         T.g = (float)g;
         first = false;
-      } else if (rf[r].par != T.par || rf[r].invL != T.invL || (float)g != T.g) {
+      } else if (rf[r].invL != T.invL || (float)g != T.g) {
         T.uniform = 0;
       }
+      if (rf[r].par != T.par) same_par = false;
+      plo = std::min(plo, rf[r].par);
+      phi = std::max(phi, rf[r].par);
       T.beta_max = std::max(T.beta_max, rf[r].beta);
       T.delta_max = std::max(T.delta_max, rf[r].delta);
+    }
+    T.par_hi = T.par;
+    if (T.uniform && !same_par) {
+      if (plo >= 0 && phi - plo < kFgMaxTileParents && !getenv("CWQ_FG_NO_MULTI")) {
+        T.uniform = 2;
+        T.par = plo;
+        T.par_hi = phi;
+      } else {
+        T.uniform = 0;
+      }
     }
   }
   if ((rc = ix->upload(&ix->iso_rf, rf, s))) return rc;
   if ((rc = ix->upload(&ix->iso_tf, tf, s))) return rc;
   ix->tile_uni_prefix.assign(n_rt + 1, 0);
-  for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform ? 1 : 0);
+  // all_uniform launches (fgemm_kernel<0, true>) need single-parent tiles
+  for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform == 1 ? 1 : 0);
   // threshold sample: ~NL_iso/64 rows at a fixed stride, 256 <= S <= 32768 (the filter
   // phases tighten T afterwards, so a small sample only costs the first phase)
   const char* sd = getenv("CWQ_FG_SAMPLE_DIV");

@@ -142,14 +142,20 @@ struct RowF {
   int par;       // internal id of the parent (-1: none), -2: unusable row (no sentence / padding)
 };
 // Per row tile: "uniform" when every usable row shares parent, path length and g = cw*iv > 0.
+// Row tile class for the filter pretest.  uniform 1: every row has parent `par`, the same
+// depth (invL) and g; uniform 2: the same invL and g, parents in [par, par_hi] (BFS order
+// keeps a tile's parents contiguous) -- the pretest takes the most permissive parent;
+// 0: generic (per-element bounds).
 struct TileF {
   int uniform;
   int par;
   float invL;
   float g;
   float beta_max, delta_max;
-  float pad0, pad1;
+  int par_hi;
+  float pad1;
 };
+constexpr int kFgMaxTileParents = 64;   // uniform 2 only up to this many parents per tile
 // fgemm MFMA shape: 1 = v_mfma_f32_16x16x32_bf16 (default), 0 = 32x32x16 (A/B builds)
 #ifndef FG_M16
 #define FG_M16 1

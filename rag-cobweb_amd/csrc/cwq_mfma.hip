@@ -406,6 +406,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     if (MODE == 0) tf = fg_tile_const(a.tf, rt);
     else tf.uniform = 0;
     const bool uni = ALLUNI || tf.uniform != 0;
+    const bool multi = !ALLUNI && tf.uniform == 2;   // per-row parent prefix for survivors
     // all setup loads are issued before any of them is used, so the tile pays one
     // memory round trip (per-query terms, then per-row terms below)
     int claimv = 0;   // the tile after this one (when not claimed ahead): in flight with the loads
@@ -441,15 +442,23 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       const float T = Tq;
       qi.w = T;
       s_qi[tid] = qi;
+      // pretest query term for a parent prefix pi (smaller = more permissive)
+      auto qv_of = [&](float pi) {
+        const float tpg = (T - pi) / tf.g;
+        float v = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x + tpg - a.slack * fabsf(pi) / tf.g -
+                  qi.y * tf.beta_max - qi.z * tf.delta_max;
+        v -= 4.f * a.gamma * (fabsf(v) + qi.x + fabsf(tpg) + fabsf(pi) / tf.g);
+        return v == v ? v : CWQ_INF;
+      };
       float pi = 0.f, qv = CWQ_INF;
       if (uni) {
         pi = Pq * tf.invL;
         if (qs < a.nq && T > -CWQ_INF) {   // T = +inf / NaN / -inf: never a candidate here
-          const float tpg = (T - pi) / tf.g;
-          float v = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x + tpg - a.slack * fabsf(pi) / tf.g -
-                    qi.y * tf.beta_max - qi.z * tf.delta_max;
-          v -= 4.f * a.gamma * (fabsf(v) + qi.x + fabsf(tpg) + fabsf(pi) / tf.g);
-          qv = v == v ? v : CWQ_INF;
+          qv = qv_of(pi);
+          if (!ALLUNI && tf.uniform == 2) {   // several parents: the most permissive one
+            const float* Pr = a.P + (size_t)qs * a.ldP;
+            for (int p = tf.par + 1; p <= tf.par_hi; ++p) qv = fminf(qv, qv_of(Pr[p] * tf.invL));
+          }
         }
       }
       s_pi[tid] = pi;
@@ -827,7 +836,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 const float init = f.R0 - s_qv[ql];
                 d = d0 - init;
                 ex = a.gamma * fabsf(init) + 0x1p-23f * (fabsf(d0) + fabsf(init));
-                pi = s_pi[ql];
+                pi = (!ALLUNI && multi) ? a.P[(size_t)q * a.ldP + f.par] * f.invL : s_pi[ql];
               } else {
                 d = d0;
                 ex = 0x1p-23f * fabsf(d0);

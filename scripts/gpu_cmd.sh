@@ -1,3 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/bench.log | tail -1 | cut -c1-900; exit $rc
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/t_gpu.log 2>&1; rc=$?; tail -1 gpurun_out/t_gpu.log; [ $rc -eq 0 ] || exit $rc
+for G in 1024 100000; do
+timeout -k 10 300 python -u scripts/filter_probe.py --clusters $G > gpurun_out/probe_g$G.log 2>&1; rc=$?; grep "mode\|identical\|differ" gpurun_out/probe_g$G.log; [ $rc -eq 0 ] || exit $rc
+done

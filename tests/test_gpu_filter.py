@@ -134,6 +134,28 @@ def test_hierarchical_two_level(gpu):
     assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
 
 
+@pytest.mark.parametrize("G", [1500, 6000])
+def test_multi_parent_tiles(gpu, G, monkeypatch):
+    """Small clusters put several parents in one 256-row tile (TileF uniform 2: pretest
+    with the most permissive parent, per-row parent prefix for survivors).  Same answer
+    as the exact scan, and as the generic per-element path (CWQ_FG_NO_MULTI)."""
+    X = gpu.synth.synthetic_corpus(24000, 64, seed=G)
+    g = torch.Generator(device=X.device)
+    g.manual_seed(G + 1)
+    labels = torch.randint(0, G, (24000,), generator=g, device=X.device)
+    ts = gpu.synth.two_level_synth(X, labels)
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=G + 2)
+    ix = gpu.index.CobwebIndex(ts["mean"], ts["var"], ts["parent"], ts["node_of_sentence"], device="cuda:0")
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert st["filter_used"] and st["fallback_queries"] <= 15, st
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    monkeypatch.setenv("CWQ_FG_NO_MULTI", "1")
+    ix2 = gpu.index.CobwebIndex(ts["mean"], ts["var"], ts["parent"], ts["node_of_sentence"], device="cuda:0")
+    ix2.set_filter(1)
+    ids2, s2 = ix2.score_topk(Q, 10)
+    assert torch.equal(ids0, ids2.cpu()) and torch.equal(s0, s2.cpu())
+
+
 def test_auto_mode_threshold(gpu):
     X = gpu.synth.synthetic_corpus(20000, 32, seed=41)
     ix = flat_index(gpu, X)
