@@ -584,12 +584,13 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
     return CWQ_OK;
   }
   ScanArgs a = base_args(ix, c);
-  const int kl = 64, tq = scan_tq(kl);
+  // raw sums need no top-k list: the hot (list width 16, two rows per lane) configuration
+  const int kl = getenv("CWQ_INT_KL64") ? 64 : 16, tq = scan_tq(kl);
   a.ld = ix->ld_int;
   a.nrows = ix->NI;
   a.nrows_pad = (int)round_up(ix->NI, kWave);
   a.n_qblocks = n_qblocks_for(c.nq, kl);
-  const int nslab = pick_nslab(ix, ix->NI, a.n_qblocks);
+  const int nslab = pick_nslab(ix, ix->NI, a.n_qblocks, kl);
   a.rows_per_slab = (int)round_up((a.nrows_pad + nslab - 1) / nslab, scan_rows_per_tile(kl));
   const int nslab2 = (a.nrows_pad + a.rows_per_slab - 1) / a.rows_per_slab;
   a.out = c.S_int;
