@@ -457,7 +457,13 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
           qv = qv_of(pi);
           if (!ALLUNI && tf.uniform == 2) {   // several parents: the most permissive one
             const float* Pr = a.P + (size_t)qs * a.ldP;
-            for (int p = tf.par + 1; p <= tf.par_hi; ++p) qv = fminf(qv, qv_of(Pr[p] * tf.invL));
+            for (int p0 = tf.par + 1; p0 <= tf.par_hi; p0 += 8) {   // 8 loads in flight per batch
+              float pv[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) pv[j] = Pr[min(p0 + j, tf.par_hi)];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) qv = fminf(qv, qv_of(pv[j] * tf.invL));
+            }
           }
         }
       }

@@ -27,12 +27,19 @@ def main():
     ap.add_argument("--queries", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--clusters", type=int, default=0, help="0: flat tree; G: root -> G random clusters -> leaves")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     L = pkg._lib
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
-    fs = pkg.synth.flat_synth(X)
+    if args.clusters:
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        labels = torch.randint(0, args.clusters, (args.n,), generator=g, device=dev)
+        fs = pkg.synth.two_level_synth(X, labels)
+    else:
+        fs = pkg.synth.flat_synth(X)
     Q, _ = pkg.synth.synthetic_queries(X, args.queries, seed=1)
     del X
     paths = args.libs.split(",")

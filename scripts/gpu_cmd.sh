@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/t_gpu.log 2>&1; rc=$?; tail -1 gpurun_out/t_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u scripts/filter_probe.py --clusters 100000 > gpurun_out/probe_g.log 2>&1; rc=$?; grep "mode\|equal" gpurun_out/probe_g.log; [ $rc -eq 0 ] || exit $rc
-CWQ_INT_KL64=1 timeout -k 10 300 python -u scripts/filter_probe.py --clusters 100000 --modes 1 > gpurun_out/probe_g64.log 2>&1; rc=$?; grep "mode" gpurun_out/probe_g64.log; exit $rc
+R=rag-cobweb_amd
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_filter.py > gpurun_out/t_f.log 2>&1; rc=$?; tail -1 gpurun_out/t_f.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python -u scripts/ab_libs.py --rounds 5 --clusters 100000 --libs $R/libcwq_head.so,$R/libcwq.so > gpurun_out/ab.log 2>&1; rc=$?; tail -3 gpurun_out/ab.log; exit $rc
