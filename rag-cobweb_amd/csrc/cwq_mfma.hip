@@ -712,13 +712,14 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       // maximum is still <= the K-th largest row lower bound (distinct groups are
       // distinct rows), and the bounds array and its select shrink 4x.
       RowF f[4];
-      float pin[4];
+      float pa[4], pb[4];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         const int r = r0 + wr * 64 + jb * 16 + r16;
         const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
         f[jb] = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-        pin[jb] = f[jb].invL;
+        pa[jb] = fmaf(f[jb].hs, f[jb].rn2, f[jb].hl);   // approximate key = pa + pb * dot (no pi, no error)
+        pb[jb] = -2.f * f[jb].hs;
       }
       const int g = (r0 + wr * 64) / 4 + r16;
 #pragma unroll
@@ -727,16 +728,32 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         for (int j = 0; j < 4; ++j) {
           const int ql = wq * 128 + ib * 16 + 4 * c16 + j;
           const int q = q0 + ql;
-          const float4 qi = s_qi[ql];
-          float m = -CWQ_INF;
+          // rigorous bound of ONE row per group: the one with the largest approximate key
+          // (any row's lower bound is a valid group value)
+          int best = -1;
+          float bk = -CWQ_INF;
 #pragma unroll
           for (int jb = 0; jb < 4; ++jb) {
-            if (f[jb].par < -1) continue;
-            const float pi = (f[jb].par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + f[jb].par] * pin[jb] : 0.f;
-            const float d0 = acc[ib][jb][j];
-            float u, lo;
-            fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f[jb], pi, a.eps_n, a.slack, u, lo);
-            m = __builtin_fmaxf(m, lo);
+            const float pk = fmaf(pb[jb], acc[ib][jb][j], pa[jb]);
+            if (f[jb].par >= -1 && (best < 0 || pk > bk)) {
+              bk = pk;
+              best = jb;
+            }
+          }
+          float m = -CWQ_INF;
+          if (best >= 0) {
+            RowF fb = f[0];
+            float d0 = acc[ib][0][j];
+#pragma unroll
+            for (int jb = 1; jb < 4; ++jb)
+              if (best == jb) {
+                fb = f[jb];
+                d0 = acc[ib][jb][j];
+              }
+            const float4 qi = s_qi[ql];
+            const float pi = (fb.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + fb.par] * fb.invL : 0.f;
+            float u;
+            fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, fb, pi, a.eps_n, a.slack, u, m);
           }
           a.lb[(size_t)q * a.ldlb + g] = m;
         }
