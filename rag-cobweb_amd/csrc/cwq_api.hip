@@ -576,7 +576,7 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
 int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   if (ix->NI == 0) return CWQ_OK;
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
-  if (ix->NI <= kWave) {   // a few internal nodes: one wave per query, same arithmetic
+  if (ix->NI <= kWave && (size_t)ix->DP * 8 <= 65536) {   // a few internal nodes: lane = query, same arithmetic
     HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, ix->NI, ix->DP, c.nq, c.S_int, ix->NI, s));
     for (auto& lv : ix->levels)
       HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,

@@ -941,35 +941,47 @@ hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, co
 // one wave per query, lane = node, the scan kernel's ANISO arithmetic op for op
 // (t = fma(x, A, -B); 16-dim fma partials; partials added in d order), so P is
 // bit-identical to the general path at a fraction of its launch cost.
+// A few internal nodes (NI <= 64): lane = query (256 queries per workgroup), each
+// node's A/B columns staged once per workgroup in LDS and read as broadcasts; the
+// arithmetic is the scan's ANISO element op, t = fmaf(x, A, -B), 16-dim fma partials
+// added in dimension order -- bit-identical to the scan kernel's raw sums.
 __global__ __launch_bounds__(256) void int_small_kernel(const float* __restrict__ X, const float* __restrict__ A,
                                                         const float* __restrict__ B, int64_t ld, int NI, int DP,
                                                         int nq, float* __restrict__ out, int64_t ldo) {
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * kWavesPerWG + (int)(threadIdx.x >> 6);
-  if (q >= nq) return;
+  extern __shared__ float s_ab[];   // [2][DP]
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int qc = q < nq ? q : nq - 1;
   const int NV16 = DP / 16;
-  const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
-  const int n = lane < NI ? lane : NI - 1;
-  float acc = 0.f;
-  for (int v = 0; v < NV16; ++v) {
-    const f32x16 xa = xg[(size_t)v * kXQ];
-    float part;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const size_t o = (size_t)(v * 16 + j) * ld + n;
-      const float t = fmaf(xa[j], A[o], -B[o]);
-      part = (j == 0) ? t * t : fmaf(t, t, part);
+  const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(qc / kXQ) * NV16 * kXQ + (qc % kXQ);
+  for (int n = 0; n < NI; ++n) {
+    __syncthreads();
+    for (int d = threadIdx.x; d < DP; d += 256) {
+      s_ab[d] = A[(size_t)d * ld + n];
+      s_ab[DP + d] = B[(size_t)d * ld + n];
     }
-    acc += part;
+    __syncthreads();
+    float acc = 0.f;
+    for (int v = 0; v < NV16; ++v) {
+      const f32x16 xa = xg[(size_t)v * kXQ];
+      const f32x16 a16 = *reinterpret_cast<const f32x16*>(s_ab + v * 16);
+      const f32x16 b16 = *reinterpret_cast<const f32x16*>(s_ab + DP + v * 16);
+      float part;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float t = fmaf(xa[j], a16[j], -b16[j]);
+        part = (j == 0) ? t * t : fmaf(t, t, part);
+      }
+      acc += part;
+    }
+    if (q < nq) out[(size_t)q * ldo + n] = acc;
   }
-  if (lane < NI) out[(size_t)q * ldo + lane] = acc;
 }
 
 hipError_t launch_int_small(const float* X, const float* A, const float* B, int64_t ld, int NI, int DP, int nq,
                             float* out, int64_t ldo, hipStream_t s) {
-  if (NI <= 0 || NI > kWave || nq <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(int_small_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, A, B, ld, NI, DP, nq, out,
-                     ldo);
+  if (NI <= 0 || NI > kWave || nq <= 0 || DP % 16 || (size_t)DP * 8 > 65536) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(int_small_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), (size_t)DP * 8, s, X, A, B, ld,
+                     NI, DP, nq, out, ldo);
   return hipGetLastError();
 }
 
