@@ -902,7 +902,25 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt;
           HIPCHK(hipMemsetAsync(gctr, 0, 64, s));
           if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
+          unsigned long long* stamp_d = nullptr;
+          const char* stamp_f = ph == nph - 1 ? getenv("CWQ_FG_STAMP") : nullptr;   // diagnostic builds
+          if (stamp_f) {
+            HIPCHK(hipMalloc(&stamp_d, 1 << 20));
+            HIPCHK(hipMemsetAsync(stamp_d, 0, 1 << 20, s));
+          }
+          g.stamp = stamp_d;
           HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
+          if (stamp_f) {
+            std::vector<unsigned long long> hs(1 << 17);
+            HIPCHK(hipMemcpyAsync(hs.data(), stamp_d, 1 << 20, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            HIPCHK(hipFree(stamp_d));
+            g.stamp = nullptr;
+            if (FILE* fo = fopen(stamp_f, "wb")) {
+              fwrite(hs.data(), 8, hs.size(), fo);
+              fclose(fo);
+            }
+          }
           if (ix->timing) {   // per-launch fgemm time (timing mode synchronises)
             float e = 0, e0 = 0;
             HIPCHK(hipEventRecord(ix->ev[6], s));

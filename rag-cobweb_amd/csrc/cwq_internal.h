@@ -188,6 +188,7 @@ struct FgArgs {
   int dir_cap;
   int* chunk_fill;                        // valid records per claimed chunk
   int* qover;                             // queries whose records were lost (re-run exactly)
+  unsigned long long* stamp;              // FG_STAMP diagnostic builds only: s_memtime stamps
 };
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
                             int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,

@@ -213,6 +213,12 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
 #ifndef FG_PRIO
 #define FG_PRIO 0
 #endif
+#ifndef FG_STAMP
+#define FG_STAMP 0   // diagnostic builds: s_memtime stamps of the ping-pong loop (FgArgs::stamp)
+#endif
+#ifndef FG_SPLITDMA
+#define FG_SPLITDMA 0   // ping-pong: second half of each stage's LDS-DMA issued from the compute section
+#endif
 #ifndef FG_SPRIO
 #define FG_SPRIO 0   // ping-pong: static s_setprio 1 for waves 4-7 during the K loop
 #endif
@@ -365,7 +371,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       ic_i = -2;
     }
   };
-  // ping-pong loop: a stage is issued in two halves, one per memory section
+  // a stage issued in two halves (FG_SPLITDMA: the second half from the compute section)
+  bool p0pend = false;
   auto issue_part = [&](int part) {
     if (part == 0 && ic_i == -2) {
       ic_i = next_i;
@@ -375,6 +382,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     if (!(a.dbg & 1))
       fg_stage(Xb, Mb, a.DPB, ic_qt * FT, ic_rt * FT, ic_k * FK, smem + (issued & (FNBUF - 1)) * FSTAGE, wave, loff,
                part);
+    p0pend = part == 0;
     if (part == 1) {
       ++issued;
       if (++ic_k == nk) {
@@ -388,6 +396,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   issue_next();
   issue_next();
   int qt, rt;
+  int tile_no = 0;   // tiles done by this workgroup (diagnostics)
+  (void)tile_no;
   fg_decode(a, xcd, i, qt, rt);
   if (tid == 0) {
     s_cnt[0] = 0;    // records of the current tile
@@ -585,22 +595,48 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // two intervals per stage: M(s) = issue stage s+3, read all 12 fragments of stage
     // s, wait for stage s+1; C(s) = all 32 MFMAs of the stage.
     if (FG_SPRIO && grp) __builtin_amdgcn_s_setprio(1);
+#if FG_STAMP
+    // diagnostic: per-stage timestamps of waves 0 and 4 (one SIMD) of workgroups 0..15,
+    // tiles 4 and 5 of each: [wg][tile-4][wave/4][stage][6]
+    const bool stp = a.stamp && blockIdx.x < 16 && (wave & 3) == 0 && lane == 0 && tile_no >= 4 && tile_no < 6;
+    unsigned long long* sp = stp ? a.stamp + ((((size_t)blockIdx.x * 2 + (tile_no - 4)) * 2 + (wave >> 2)) * 32) * 6 : nullptr;
+#define FG_ST(k) do { if (stp && t < 32) sp[t * 6 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FG_ST(k) do { } while (0)
+#endif
     for (int t = 0; t < nk; ++t) {
+      FG_ST(0);
       const char* sb = smem + (gs & (FNBUF - 1)) * FSTAGE;
+#if FG_SPLITDMA
+      issue_part(0);
+#else
       if (!FG_RDFIRST) issue_next();
+#endif
       if (!(a.dbg & 128)) {
         const char* sA = sb + wq * 128 * 64 + foff16;
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) xa1[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 1024);
         rdB(sb);
       }
+#if !FG_SPLITDMA
       if (FG_RDFIRST) issue_next();
+#endif
       ++gs;
       const int n_out = issued - gs - 1;
+#if FG_SPLITDMA
+      // younger than stage gs: n_out whole stages (4 glds) + a pending first half (2)
+      const int young = 4 * n_out + (p0pend ? 2 : 0);
+      if (young >= 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else if (young == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else if (young == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
       if (a.dbg & 256) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
       else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+      FG_ST(1);
       if (FG_CLAIM && dyn && t == 0 && next_i < ntl) {
         if (tid == 0) {
           // opaque per-lane zero: a divergent address keeps the atomic optimizer from
@@ -612,12 +648,33 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         claim_pend = true;
       }
       sbar();
+      FG_ST(2);
+#if FG_SPLITDMA
+      // second half of the stage's LDS-DMA from the compute section, between MFMA groups
+      // (its slot's last reads preceded the barrier that opened this interval)
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_part(1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ib = 4; ib < 8; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
+#else
 #pragma unroll
       for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
           acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
+#endif
+      FG_ST(3);
       if (t + 1 < nk || grp == 0) sbar();
+      FG_ST(4);
     }
     if (FG_SPRIO && grp) __builtin_amdgcn_s_setprio(0);
 #else
@@ -924,6 +981,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       if (s_cnt[7] && tid < FT && q0 + tid < a.nq) a.qover[q0 + tid] = 1;   // re-run this tile's queries exactly
     }
     i = next_i;
+    ++tile_no;
     if (i >= ntl) break;
     if (!dyn) next_i = i + nw_x;
     fg_decode(a, xcd, i, qt, rt);
