@@ -216,23 +216,11 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
 #ifndef FG_STAMP
 #define FG_STAMP 0   // diagnostic builds: s_memtime stamps of the ping-pong loop (FgArgs::stamp)
 #endif
-#ifndef FG_SPLITDMA
-#define FG_SPLITDMA 0   // ping-pong: second half of each stage's LDS-DMA issued from the compute section
-#endif
-#ifndef FG_SPRIO
-#define FG_SPRIO 0   // ping-pong: static s_setprio 1 for waves 4-7 during the K loop
-#endif
-#ifndef FG_RDFIRST
-#define FG_RDFIRST 0   // ping-pong: fragment reads before the stage's LDS-DMA issue
-#endif
-#ifndef FG_CLAIM
-#define FG_CLAIM 0   // tile claims issued one tile ahead (ping-pong loop)
-#endif
 #ifndef FG_SADDR
 #define FG_SADDR 1
 #endif
 #ifndef FG_PP
-#define FG_PP 2   // ping-pong wave groups (16x16x32 path only)
+#define FG_PP 1   // ping-pong wave groups (16x16x32 path only; 0: both waves of a SIMD per stage)
 #endif
 #ifndef FG_INTERLEAVE
 #define FG_INTERLEAVE 1   // measured +1% (and PRIO -6%) in one A/B
@@ -352,8 +340,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     if (i >= ntl) return;
   }
   int next_i = dyn ? ntl : i + nw_x;   // dynamic: claimed one tile ahead
-  int claim = 0;                       // thread 0: claim in flight for the tile after next
-  bool claim_pend = false;
   int ic_i = i, ic_k = 0, ic_qt, ic_rt, issued = 0, gs = 0;
   fg_decode(a, xcd, ic_i, ic_qt, ic_rt);
   // the next tile is resolved lazily: its first stage is issued during the current
@@ -371,27 +357,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       ic_i = -2;
     }
   };
-  // a stage issued in two halves (FG_SPLITDMA: the second half from the compute section)
-  bool p0pend = false;
-  auto issue_part = [&](int part) {
-    if (part == 0 && ic_i == -2) {
-      ic_i = next_i;
-      if (ic_i < ntl) fg_decode(a, xcd, ic_i, ic_qt, ic_rt);
-    }
-    if (ic_i >= ntl) return;
-    if (!(a.dbg & 1))
-      fg_stage(Xb, Mb, a.DPB, ic_qt * FT, ic_rt * FT, ic_k * FK, smem + (issued & (FNBUF - 1)) * FSTAGE, wave, loff,
-               part);
-    p0pend = part == 0;
-    if (part == 1) {
-      ++issued;
-      if (++ic_k == nk) {
-        ic_k = 0;
-        ic_i = -2;
-      }
-    }
-  };
-  (void)issue_part;
   issue_next();
   issue_next();
   issue_next();
@@ -420,7 +385,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // all setup loads are issued before any of them is used, so the tile pays one
     // memory round trip (per-query terms, then per-row terms below)
     int claimv = 0;   // the tile after this one (when not claimed ahead): in flight with the loads
-    if (dyn && tid == 0 && !claim_pend) {
+    if (dyn && tid == 0) {
       int z;   // opaque zero: a divergent address keeps the atomic optimizer from waiting on the spot
       asm volatile("v_mov_b32 %0, 0" : "=v"(z));
       claimv = atomicAdd(a.tctr + xcd + z, 1);
@@ -480,13 +445,9 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       s_pi[tid] = pi;
       s_qv[tid] = qv;
     }
-    // the tile after this one: claimed here for the first tile; afterwards its claim
-    // was issued during the previous tile's K loop (its latency hidden there; the
-    // return is drained by this barrier's vmcnt(0), which waits for stage 0 anyway)
-    if (dyn && tid == 0) s_cnt[8] = claim_pend ? claim : claimv;
+    if (dyn && tid == 0) s_cnt[8] = claimv;   // the tile after this one
     __syncthreads();   // stage 0 landed, setup visible
     if (dyn) next_i = __builtin_amdgcn_readfirstlane(s_cnt[8]);   // uniform: scalar tile loads
-    claim_pend = false;
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
 #if FG_M16
     // 16x16x32 layout: acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
@@ -556,16 +517,19 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
 #endif
     };
 #if FG_PP
-    // Ping-pong: waves 0-3 and 4-7 (one of each per SIMD) run one barrier interval
-    // apart, so in every interval one wave of each SIMD issues a 16-MFMA cluster while
-    // its partner reads the fragments of its next cluster and issues LDS-DMA.
-    //   group 0:     M1 B C1 B M2 B C2 B | M1 B ...        (4 barriers per stage)
-    //   group 1:   B M1 B C1 B M2 B C2 | B M1 ...          (one interval behind)
-    // M1(s): issue stage s+3, read A[0..3], B[0..3] of stage s;  C1: query blocks 0-3;
-    // M2(s): read A[4..7], wait (own vmcnt) for stage s+1;       C2: query blocks 4-7.
-    // RAW: both groups' waits for stage s+1 precede barrier B(4s+4), its first read
-    // follows it.  WAR: stage s's last read (group 1's M2(s), lgkmcnt(0)) precedes
-    // B(4s+4); the DMA that reuses its slot is issued in M1(s+1), after it.
+    // Ping-pong: waves 0-3 and 4-7 (one of each per SIMD) run one barrier interval apart,
+    // so in every interval one wave per SIMD issues its 32-MFMA cluster while its partner
+    // works through its memory section:
+    //   group 0:     M(s) B C(s) B | M(s+1) B C(s+1) B ...
+    //   group 1:   B M(s) B C(s) | B M(s+1) B C(s+1) ...
+    // M(s): issue stage s+3's LDS-DMA, read all 12 fragments of stage s, wait (own vmcnt)
+    // for stage s+1;  C(s): the stage's 32 MFMAs.  Group 1 starts with one extra barrier
+    // and skips the last one, so both groups pass the same barriers and group 1's last
+    // cluster overlaps group 0's epilogue.  RAW: both groups' waits for stage s+1 precede
+    // the barrier before its first read (group 0's M(s+1)).  WAR: the DMA into stage s-1's
+    // slot is issued in M(s), after the barrier that follows group 1's last read of it
+    // (its M(s-1) ends with lgkmcnt(0)).
+    (void)xa0;
     (void)xb1;
     const int grp = wave >> 2;
     auto sbar = [&]() {
@@ -573,134 +537,53 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
-    auto rdA = [&](const char* sb, int ib0) {
-      const char* sA = sb + wq * 128 * 64 + foff16 + ib0 * 1024;
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib) xa0[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 1024);
-    };
-    auto rdB = [&](const char* sb) {
-      const char* sB = sb + FT * 64 + wr * 64 * 64 + foff16;
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) xb0[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 1024);
-    };
-    auto clus = [&](int ib0) {
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[ib0 + ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa0[ib], xb0[jb], acc[ib0 + ib][jb], 0, 0, 0);
-    };
     if (grp) sbar();
-#if FG_PP == 2
-    // two intervals per stage: M(s) = issue stage s+3, read all 12 fragments of stage
-    // s, wait for stage s+1; C(s) = all 32 MFMAs of the stage.
-    if (FG_SPRIO && grp) __builtin_amdgcn_s_setprio(1);
 #if FG_STAMP
     // diagnostic: per-stage timestamps of waves 0 and 4 (one SIMD) of workgroups 0..15,
     // tiles 4 and 5 of each: [wg][tile-4][wave/4][stage][6]
     const bool stp = a.stamp && blockIdx.x < 16 && (wave & 3) == 0 && lane == 0 && tile_no >= 4 && tile_no < 6;
-    unsigned long long* sp = stp ? a.stamp + ((((size_t)blockIdx.x * 2 + (tile_no - 4)) * 2 + (wave >> 2)) * 32) * 6 : nullptr;
-#define FG_ST(k) do { if (stp && t < 32) sp[t * 6 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+    unsigned long long* sp =
+        stp ? a.stamp + ((((size_t)blockIdx.x * 2 + (tile_no - 4)) * 2 + (wave >> 2)) * 32) * 6 : nullptr;
+#define FG_ST(k)                                                               \
+  do {                                                                         \
+    if (stp && t < 32) sp[t * 6 + (k)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
 #else
-#define FG_ST(k) do { } while (0)
+#define FG_ST(k) \
+  do {           \
+  } while (0)
 #endif
     for (int t = 0; t < nk; ++t) {
       FG_ST(0);
       const char* sb = smem + (gs & (FNBUF - 1)) * FSTAGE;
-#if FG_SPLITDMA
-      issue_part(0);
-#else
-      if (!FG_RDFIRST) issue_next();
-#endif
+      issue_next();
       if (!(a.dbg & 128)) {
         const char* sA = sb + wq * 128 * 64 + foff16;
+        const char* sB = sb + FT * 64 + wr * 64 * 64 + foff16;
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) xa1[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 1024);
-        rdB(sb);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) xb0[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 1024);
       }
-#if !FG_SPLITDMA
-      if (FG_RDFIRST) issue_next();
-#endif
       ++gs;
       const int n_out = issued - gs - 1;
-#if FG_SPLITDMA
-      // younger than stage gs: n_out whole stages (4 glds) + a pending first half (2)
-      const int young = 4 * n_out + (p0pend ? 2 : 0);
-      if (young >= 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-      else if (young == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-      else if (young == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#else
       if (a.dbg & 256) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
       else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
       FG_ST(1);
-      if (FG_CLAIM && dyn && t == 0 && next_i < ntl) {
-        if (tid == 0) {
-          // opaque per-lane zero: a divergent address keeps the atomic optimizer from
-          // rewriting this into a form that waits for the return on the spot
-          int z;
-          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-          claim = atomicAdd(a.tctr + xcd + z, 1);
-        }
-        claim_pend = true;
-      }
       sbar();
       FG_ST(2);
-#if FG_SPLITDMA
-      // second half of the stage's LDS-DMA from the compute section, between MFMA groups
-      // (its slot's last reads preceded the barrier that opened this interval)
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_part(1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ib = 4; ib < 8; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
-#else
 #pragma unroll
       for (int ib = 0; ib < 8; ++ib)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
           acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa1[ib], xb0[jb], acc[ib][jb], 0, 0, 0);
-#endif
       FG_ST(3);
       if (t + 1 < nk || grp == 0) sbar();
       FG_ST(4);
     }
-    if (FG_SPRIO && grp) __builtin_amdgcn_s_setprio(0);
-#else
-    for (int t = 0; t < nk; ++t) {
-      const char* sb = smem + (gs & (FNBUF - 1)) * FSTAGE;
-      issue_part(0);
-      if (!(a.dbg & 128)) {
-        rdA(sb, 0);
-        rdB(sb);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      sbar();
-      clus(0);
-      sbar();
-      issue_part(1);
-      if (!(a.dbg & 128)) rdA(sb, 4);
-      ++gs;
-      const int n_out = issued - gs - 1;
-      if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-      else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      sbar();
-      clus(4);
-      if (t + 1 < nk || grp == 0) sbar();
-    }
-#endif
+#undef FG_ST
 #else
     load16(xa0, xb0, smem + (gs & (FNBUF - 1)) * FSTAGE);
     for (int t = 0; t < nk; t += 2) {

@@ -1,3 +1,4 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-CWQ_FG_STAMP=$PWD/gpurun_out/stamps.bin CWQ_LIB=$PWD/rag-cobweb_amd/libcwq_stamp.so timeout -k 10 300 python -u scripts/filter_probe.py --modes 1 --reps 1 > gpurun_out/probe_st.log 2>&1; rc=$?; grep mode gpurun_out/probe_st.log; [ $rc -eq 0 ] || exit $rc
-python scripts/stamp_summary.py gpurun_out/stamps.bin
+R=rag-cobweb_amd
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/t_gpu.log 2>&1; rc=$?; tail -1 gpurun_out/t_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u scripts/ab_libs.py --rounds 6 --libs $R/libcwq_head.so,$R/libcwq.so > gpurun_out/ab.log 2>&1; rc=$?; tail -2 gpurun_out/ab.log; exit $rc
