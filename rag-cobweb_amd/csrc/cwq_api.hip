@@ -585,7 +585,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   }
   ScanArgs a = base_args(ix, c);
   // raw sums need no top-k list: the hot (list width 16, two rows per lane) configuration
-  const int kl = getenv("CWQ_INT_KL64") ? 64 : 16, tq = scan_tq(kl);
+  const int kl = 16, tq = scan_tq(kl);
   a.ld = ix->ld_int;
   a.nrows = ix->NI;
   a.nrows_pad = (int)round_up(ix->NI, kWave);
