@@ -573,14 +573,18 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
 }
 
 // Internal nodes: raw sums -> P (path prefix), BF (bottleneck), LPF (full lp).
-int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
+// bf_lpf: also the path bottleneck BF and full lp LPF (categorize / log_prob); the fast
+// keys need only P.
+int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true) {
+  float* BF = bf_lpf ? c.BF : nullptr;
+  float* LPF = bf_lpf ? c.LPF : nullptr;
   if (ix->NI == 0) return CWQ_OK;
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   if (ix->NI <= kWave && (size_t)ix->DP * 8 <= 65536) {   // a few internal nodes: lane = query, same arithmetic
     HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, ix->NI, ix->DP, c.nq, c.S_int, ix->NI, s));
     for (auto& lv : ix->levels)
       HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
-                                 dfull, c.P, c.BF, c.LPF, s));
+                                 dfull, c.P, BF, LPF, s));
     return CWQ_OK;
   }
   ScanArgs a = base_args(ix, c);
@@ -598,7 +602,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s) {
   HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
   for (auto& lv : ix->levels)
     HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
-                               dfull, c.P, c.BF, c.LPF, s));
+                               dfull, c.P, BF, LPF, s));
   return CWQ_OK;
 }
 
@@ -802,7 +806,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     carve_chunk(ix, b, c, nqc);
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s))) return rc;
+    if ((rc = run_internal(ix, c, s, false))) return rc;
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
     if (!general) {
       float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
@@ -1070,7 +1074,7 @@ extern "C" int cwq_rank_scores(cwq_index* ix, const float* q, int64_t nq, float*
     carve_chunk(ix, b, c, nqc);
     float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s))) return rc;
+    if ((rc = run_internal(ix, c, s, false))) return rc;
     if ((rc = run_leaf_scan(ix, c, EPI_KEY, false, 16, 0.f, rowkey, ix->NL, nullptr, nullptr, nullptr, 1, nullptr, s)))
       return rc;
     HIPCHK(launch_gather_sentences(rowkey, ix->NL, nqc, ix->row_of_sent, ix->n_sent, out + q0 * ix->n_sent, s));

@@ -630,12 +630,12 @@ __global__ void prefix_level_kernel(const float* __restrict__ S, int64_t ldS, in
     if (p >= 0) {
       const size_t op = (size_t)q * ldS + p;
       P[o] = fmaf(w_int[i], lp, P[op]);
-      BF[o] = fminf(BF[op], lpf);
+      if (BF) BF[o] = fminf(BF[op], lpf);
     } else {
       P[o] = w_int[i] * lp;
-      BF[o] = lpf;
+      if (BF) BF[o] = lpf;
     }
-    LPF[o] = lpf;
+    if (LPF) LPF[o] = lpf;
   }
 }
 
