@@ -105,6 +105,7 @@ struct cwq_index {
   RowF* iso_rf = nullptr;
   TileF* iso_tf = nullptr;
   std::vector<int> tile_uni_prefix;   // prefix counts of uniform row tiles (all_uniform per launch range)
+  int n_multi_tiles = 0;              // tiles with several parents (TileF uniform 2)
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
   int* samp_rows = nullptr;
   uint16_t* iso_Sb = nullptr;
@@ -270,6 +271,8 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   ix->tile_uni_prefix.assign(n_rt + 1, 0);
   // all_uniform launches (fgemm_kernel<0, true>) need single-parent tiles
   for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform == 1 ? 1 : 0);
+  ix->n_multi_tiles = 0;
+  for (int t = 0; t < n_rt; ++t) ix->n_multi_tiles += tf[t].uniform == 2 ? 1 : 0;
   // threshold sample: ~NL_iso/64 rows at a fixed stride, 256 <= S <= 32768 (the filter
   // phases tighten T afterwards, so a small sample only costs the first phase)
   const char* sd = getenv("CWQ_FG_SAMPLE_DIV");
@@ -782,7 +785,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int n_rts = filt ? ix->ld_s / kFgTile : 0;
   // per query: bf16 query, info, sample bounds, threshold list, candidate lists, flags, records
   const size_t filt_q = filt ? (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
-                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256
+                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
+                                   (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0)
                              : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
@@ -843,7 +847,10 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         int* gctr = b.take<int>(64);
         const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
         int4* rec_dir = b.take<int4>((size_t)dir_cap);
+        float2* pmm = ix->n_multi_tiles ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
         HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
+        if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
+          HIPCHK(launch_tile_prange(c.P, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf, s));
         FgArgs g;
         memset(&g, 0, sizeof(g));
         g.DPB = ix->DPB;
@@ -856,6 +863,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.tctr = gctr + 8;
         g.rf = ix->iso_rf;
         g.tf = ix->iso_tf;
+        g.pmm = pmm;
+        g.ldq = nqf;
         g.P = c.P ? c.P : ix->dummy;
         g.ldP = std::max(ix->NI, 1);
         g.gamma = (float)fc.gamma;
@@ -903,7 +912,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         for (int ph = 0; ph < nph; ++ph) {
           g.rt_off = cuts[ph];
           g.n_rt = cuts[ph + 1] - cuts[ph];
-          g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt;
+          g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt &&
+                          !getenv("CWQ_FG_NO_ALLUNI");
           HIPCHK(hipMemsetAsync(gctr, 0, 64, s));
           if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
           unsigned long long* stamp_d = nullptr;

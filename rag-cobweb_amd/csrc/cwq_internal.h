@@ -174,6 +174,8 @@ struct FgArgs {
   int64_t ldT;
   const RowF* rf;
   const TileF* tf;
+  const float2* pmm;                      // multi-parent tiles: {min, max} parent prefix x invL, [tile][ldq]
+  int64_t ldq;
   const int* rowmap;                      // sample pass: operand row -> filter row (-1 pad)
   const float* P;                         // [nq][ldP] path prefixes of internal nodes
   int64_t ldP;
@@ -199,6 +201,8 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s);
 int fgemm_dpb(int D);   // padded bf16 operand width the fgemm build needs
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
+hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* tf, int n_rt, float2* pmm, int64_t ldq,
+                              hipStream_t s);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
 hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,

@@ -430,15 +430,19 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         pi = Pq * tf.invL;
         if (qs < a.nq && T > -CWQ_INF) {   // T = +inf / NaN / -inf: never a candidate here
           qv = qv_of(pi);
-          if (!ALLUNI && tf.uniform == 2) {   // several parents: the most permissive one
-            const float* Pr = a.P + (size_t)qs * a.ldP;
-            for (int p0 = tf.par + 1; p0 <= tf.par_hi; p0 += 8) {   // 8 loads in flight per batch
-              float pv[8];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) pv[j] = Pr[min(p0 + j, tf.par_hi)];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) qv = fminf(qv, qv_of(pv[j] * tf.invL));
-            }
+          if (multi) {
+            // several parents: a lower bound of qv_of over the tile's parent-prefix range
+            // [lo, hi] (each term of qv_of bounded separately; the margin term uses the
+            // range's largest magnitudes), from one precomputed load
+            const float2 pm = a.pmm[(size_t)rt * a.ldq + qs];
+            const float A = qi.x * (0.5f - 0.5f * a.eps_n) - 1.5f * a.slack * qi.x - qi.y * tf.beta_max -
+                            qi.z * tf.delta_max;
+            const float M = fmaxf(fabsf(pm.x), fabsf(pm.y));
+            const float v1L = A + (T - pm.y) / tf.g - a.slack * M / tf.g;
+            const float v1U = A + (T - pm.x) / tf.g;
+            const float tpm = fmaxf(fabsf(T - pm.x), fabsf(T - pm.y)) / tf.g;
+            const float v = v1L - 4.f * a.gamma * (fmaxf(fabsf(v1L), fabsf(v1U)) + qi.x + tpm + M / tf.g);
+            qv = v == v ? fminf(qv, v) : CWQ_INF;
           }
         }
       }
@@ -1006,6 +1010,42 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
     cu[(size_t)q * 64 + lane] = lk;
     crow[(size_t)q * 64 + lane] = lr;
   }
+}
+
+// Multi-parent row tiles: per (tile, query) the range of the parents' prefixes x invL, so
+// the fgemm tile setup bounds its pretest term with one load instead of walking the
+// tile's parents.  Thread = query; tiles along blockIdx.y.
+__global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restrict__ P, int64_t ldP, int nq,
+                                                          const TileF* __restrict__ tf, int t0,
+                                                          float2* __restrict__ pmm, int64_t ldq) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int t = t0 + blockIdx.y;
+  const TileF T = tf[t];
+  if (T.uniform != 2 || q >= nq) return;
+  const float* Pr = P + (size_t)q * ldP;
+  float mn = CWQ_INF, mx = -CWQ_INF;
+  for (int p0 = T.par; p0 <= T.par_hi; p0 += 8) {   // 8 loads in flight
+    float pv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[j] = Pr[min(p0 + j, T.par_hi)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pi = pv[j] * T.invL;
+      mn = fminf(mn, pi);
+      mx = fmaxf(mx, pi);
+    }
+  }
+  pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
+}
+
+hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* tf, int n_rt, float2* pmm, int64_t ldq,
+                              hipStream_t s) {
+  for (int t0 = 0; t0 < n_rt; t0 += 65535) {
+    const int nt = std::min(65535, n_rt - t0);
+    hipLaunchKernelGGL(tile_prange_kernel, dim3((unsigned)((nq + 255) / 256), (unsigned)nt), dim3(256), 0, s, P,
+                       ldP, nq, tf, t0, pmm, ldq);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s) {
