@@ -156,6 +156,25 @@ def test_multi_parent_tiles(gpu, G, monkeypatch):
     assert torch.equal(ids0, ids2.cpu()) and torch.equal(s0, s2.cpu())
 
 
+def test_multi_parent_tiles_clustered(gpu):
+    """Well-separated small clusters: the parents inside one tile have very different path
+    prefixes for a query, so the per-tile pretest bound spans a wide range -- the answer
+    must still equal the exact scan bit for bit."""
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(5)
+    G, per, D = 2400, 10, 48
+    centers = torch.randn(G, D, generator=g, device="cuda:0") * 4.0
+    labels = torch.arange(G, device="cuda:0").repeat_interleave(per)
+    X = centers[labels] + 0.3 * torch.randn(G * per, D, generator=g, device="cuda:0")
+    ts = gpu.synth.two_level_synth(X, labels)
+    Q = X[torch.randperm(G * per, generator=g, device="cuda:0")[:300]] + \
+        0.2 * torch.randn(300, D, generator=g, device="cuda:0")
+    ix = gpu.index.CobwebIndex(ts["mean"], ts["var"], ts["parent"], ts["node_of_sentence"], device="cuda:0")
+    ids0, s0, ids1, s1, st = both(ix, Q, 10)
+    assert st["filter_used"]
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
 def test_auto_mode_threshold(gpu):
     X = gpu.synth.synthetic_corpus(20000, 32, seed=41)
     ix = flat_index(gpu, X)
