@@ -119,6 +119,8 @@ struct cwq_index {
   std::mutex mu;
   void* ws = nullptr;
   size_t ws_size = 0;
+  int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
+  size_t hflags_n = 0;
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -152,6 +154,17 @@ struct cwq_index {
       if (e) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
     if (ws) (void)hipFree(ws);
+    if (hflags) (void)hipHostFree(hflags);
+  }
+  int host_flags(size_t n) {
+    if (n <= hflags_n) return CWQ_OK;
+    if (hflags) (void)hipHostFree(hflags);
+    hflags = nullptr;
+    hflags_n = 0;
+    if (hipHostMalloc((void**)&hflags, n * sizeof(int), hipHostMallocDefault) != hipSuccess)
+      return fail(CWQ_ERR_OOM, "hipHostMalloc failed");
+    hflags_n = n;
+    return CWQ_OK;
   }
 };
 
@@ -273,10 +286,10 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform == 1 ? 1 : 0);
   ix->n_multi_tiles = 0;
   for (int t = 0; t < n_rt; ++t) ix->n_multi_tiles += tf[t].uniform == 2 ? 1 : 0;
-  // threshold sample: ~NL_iso/64 rows at a fixed stride, 256 <= S <= 32768 (the filter
+  // threshold sample: ~NL_iso/128 rows at a fixed stride, 256 <= S <= 32768 (the filter
   // phases tighten T afterwards, so a small sample only costs the first phase)
   const char* sd = getenv("CWQ_FG_SAMPLE_DIV");
-  const int sdiv = sd && atoi(sd) > 0 ? atoi(sd) : 64;
+  const int sdiv = sd && atoi(sd) > 0 ? atoi(sd) : 128;
   int S = (int)std::min<int64_t>(32768, std::max<int64_t>(kFgTile, NLi / sdiv / kFgTile * kFgTile));
   const int stride = std::max(1, NLi / S);
   std::vector<int> srow(round_up(S, kFgTile), -1);
@@ -723,6 +736,31 @@ int fg_phases() {
   return e && *e ? atoi(e) : 1;
 }
 
+// filter phases over the row tiles: cut points at n_rt * f / 1024 for the fractions f in
+// CWQ_FG_CUTS (comma separated, increasing, at most 4; default 32,96,256,512: five
+// launches, the first over 1/32 of the tiles; in-process A/B vs 1/16,1/4: x1.02 per call)
+int fg_phase_cuts(int n_rt, int* cuts) {
+  if (n_rt < 16 || !fg_phases()) return 1;
+  int f[4] = {32, 96, 256, 512}, nf = 4;
+  if (const char* e = getenv("CWQ_FG_CUTS")) {
+    nf = 0;
+    for (const char* p = e; *p && nf < 4;) {
+      const int v = atoi(p);
+      if (v > 0 && v < 1024) f[nf++] = v;
+      while (*p && *p != ',') ++p;
+      if (*p == ',') ++p;
+    }
+  }
+  int n = 1;
+  for (int i = 0; i < nf; ++i) {
+    const int c = std::max(cuts[n - 1] + 1, (int)((int64_t)n_rt * f[i] / 1024));
+    if (c >= n_rt) break;
+    cuts[n++] = c;
+  }
+  cuts[n] = n_rt;
+  return n;
+}
+
 int fg_order() {   // default: dynamic per-XCD tile claims (measured fastest)
   const char* e = getenv("CWQ_FG_ORDER");
   return e && *e ? atoi(e) : 2;
@@ -803,7 +841,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     const int64_t nqf = round_up(nqc, kFgTile);
     size_t need = chunk_bytes(ix, nq_pad) + 64 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
-                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) + (size_t)nqf * filt_q + 4096 * 4;
+                    : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) + (size_t)nqf * filt_q + 4096 * 8;
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
@@ -832,10 +870,11 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         float* lb = b.take<float>((size_t)nqf * ix->ld_s + 4096);
         float* tl = b.take<float>((size_t)nqf * 64);
         int* tr = b.take<int>((size_t)nqf * 64);
-        int* qcnt = b.take<int>(nqf);
+        // [qcnt | ok | n_exact], contiguous: the host reads all three with one copy
+        int* qcnt = b.take<int>((size_t)3 * nqf);
+        okf = qcnt + nqf;
+        int* nex = qcnt + 2 * nqf;
         int* qover = b.take<int>(nqf);
-        okf = b.take<int>(nqf);
-        int* nex = b.take<int>(nqf);
         int* crow = b.take<int>((size_t)nqf * kFgCapQ);
         float* cu = b.take<float>((size_t)nqf * kFgCapQ);
         float* cl = b.take<float>((size_t)nqf * kFgCapQ);
@@ -901,14 +940,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.dir_cap = dir_cap;
         HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)nqf * 4, s));
         HIPCHK(hipMemsetAsync(qover, 0, (size_t)nqf * 4, s));
-        int cuts[4] = {0, n_rt, n_rt, n_rt};
-        int nph = 1;
-        if (n_rt >= 16 && fg_phases()) {
-          cuts[1] = std::max(1, n_rt / 16);
-          cuts[2] = std::max(cuts[1] + 1, n_rt / 4);
-          cuts[3] = n_rt;
-          nph = 3;
-        }
+        int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
+        const int nph = fg_phase_cuts(n_rt, cuts);
         for (int ph = 0; ph < nph; ++ph) {
           g.rt_off = cuts[ph];
           g.n_rt = cuts[ph + 1] - cuts[ph];
@@ -967,11 +1000,12 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
                            scores ? scores + q0 * k : nullptr, s));
       if (filt) {
-        std::vector<int> okh(nqc), cnth(nqc), nexh(nqc);
-        HIPCHK(hipMemcpyAsync(okh.data(), okf, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(cnth.data(), qcnt_d, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(nexh.data(), nex_d, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+        if ((rc = ix->host_flags((size_t)3 * nqf))) return rc;
+        HIPCHK(hipMemcpyAsync(ix->hflags, qcnt_d, (size_t)3 * nqf * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        const int* cnth = ix->hflags;
+        const int* okh = cnth + nqf;
+        const int* nexh = cnth + 2 * nqf;
         for (int i = 0; i < nqc; ++i) {
           if (!okh[i]) redo.push_back(q0 + i);
           cand_sum += cnth[i];

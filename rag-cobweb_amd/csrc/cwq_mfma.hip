@@ -1142,6 +1142,7 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
                                                     const float* __restrict__ P, int64_t ldP, int seg_base,
                                                     float* pkey, float* paux, int* prow, int64_t lstride,
                                                     int* ok_flag, int* n_exact) {
+  __shared__ int s_pend[kWavesPerWG][128];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (q >= nq) return;
@@ -1162,15 +1163,28 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
       list64_offer(tk, tr, lane, lv, j, K);
     }
     const float T2 = rl_f2(tk, K - 1);
-    // pass 2: exact keys of the survivors
-    for (int j0 = 0; j0 < n; j0 += 64) {
+    // pass 2: exact keys of the survivors (u >= T2), packed 64 to a round through a
+    // per-wave LDS list so that every lane of a round has a row (C3: ~20 survivors
+    // spread over ~3 chunks of candidates -> one round instead of three)
+    int* pend = s_pend[threadIdx.x >> 6];
+    int npend = 0;
+    for (int j0 = 0; j0 < n || npend > 0; j0 += 64) {
       const int j = j0 + lane;
       const bool c = j < n && cu[base + j] >= T2;
-      if (__ballot(c) == 0) continue;
+      const uint64_t bm = __ballot(c);
+      if (c) pend[npend + __popcll(bm & ((1ull << lane) - 1))] = j;
+      npend += __popcll(bm);
+      if (npend < 64 && j0 + 64 < n) continue;   // more candidates to pack first
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool act = lane < npend;
+      const int jj = act ? pend[lane] : 0;
+      const int rest = npend > 64 ? pend[64 + lane] : 0;   // lane < npend - 64 <= 63
       float key = -CWQ_INF, lp = 0.f;
       int rid = 0x7fffffff;
-      if (c) {
-        const int rr = crow[base + j];
+      if (act) {
+        const int rr = crow[base + jj];
         const RowMeta md = meta[rr];
         const int p = par[rr];
         const float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;
@@ -1178,7 +1192,14 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         rid = seg_base + rr;
         ++nx;
       }
-      uint64_t mask = __ballot(c);
+      __builtin_amdgcn_wave_barrier();
+      if (npend > 64 && lane < npend - 64) pend[lane] = rest;
+      npend = npend > 64 ? npend - 64 : 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool c2 = act;
+      uint64_t mask = __ballot(c2);
       while (mask) {
         const int b = __builtin_ctzll(mask);
         mask &= mask - 1;
