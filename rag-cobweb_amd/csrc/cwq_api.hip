@@ -824,7 +824,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   // per query: bf16 query, info, sample bounds, threshold list, candidate lists, flags, records
   const size_t filt_q = filt ? (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
                                    (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
-                                   (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0)
+                                   (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0) + 4 + 64 * 4
                              : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
@@ -875,6 +875,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         okf = qcnt + nqf;
         int* nex = qcnt + 2 * nqf;
         int* qover = b.take<int>(nqf);
+        int* tdone = b.take<int>(nqf);                     // tighten/final incremental state
+        float* tlk = b.take<float>((size_t)nqf * 64);
         int* crow = b.take<int>((size_t)nqf * kFgCapQ);
         float* cu = b.take<float>((size_t)nqf * kFgCapQ);
         float* cl = b.take<float>((size_t)nqf * kFgCapQ);
@@ -940,6 +942,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.dir_cap = dir_cap;
         HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)nqf * 4, s));
         HIPCHK(hipMemsetAsync(qover, 0, (size_t)nqf * 4, s));
+        HIPCHK(hipMemsetAsync(tdone, 0, (size_t)nqf * 4, s));
         int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
         const int nph = fg_phase_cuts(n_rt, cuts);
         for (int ph = 0; ph < nph; ++ph) {
@@ -981,13 +984,14 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           }
           HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl,
                                s));
-          if (ph + 1 < nph) HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, s));
+          if (ph + 1 < nph)
+            HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, tlk, tr, tdone, s));
         }
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
                             ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow,
-                            (int64_t)nst * K, okf, nex, s));
+                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, s));
         qcnt_d = qcnt;
         nex_d = nex;
         if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));

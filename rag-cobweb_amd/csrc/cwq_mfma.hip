@@ -972,7 +972,8 @@ __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float
 }
 
 // ---------------------------------------------------------------------------
-// select: top-Kp values per query of a dense [nq][ld] array (the sample bounds)
+// select: top-Kp values per query of a dense [nq][ld] array (the sample bounds; the
+// values are first reduced to maxima of up to 16 per lane)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u, int64_t ldu, int nrows, int Kp,
                                                      float* cu, int* crow) {
@@ -988,17 +989,26 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
   constexpr int STEP = 1024;
   const int per = (int)(((int64_t)nrows + 4 * STEP - 1) / (4 * STEP)) * STEP;
   const int r_lo = wave * per, r_hi = min(nrows, r_lo + per);
+  // the K-th largest of maxima over g values of a lane (distinct rows, so still a lower
+  // bound of the K-th key): g up to 16 while at least 8*Kp maxima remain
+  int g = 16;
+  while (g > 1 && nrows / g < 8 * Kp) g >>= 1;
   for (int r0 = r_lo; r0 < r_hi; r0 += STEP) {
     float4 v4[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) v4[t] = *reinterpret_cast<const float4*>(uq + r0 + t * 256 + lane * 4);
+    float m = -CWQ_INF;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const float vv[4] = {v4[t].x, v4[t].y, v4[t].z, v4[t].w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int r = r0 + t * 256 + lane * 4 + c;
-        list64_offer(lk, lr, lane, r < r_hi ? vv[c] : -CWQ_INF, r, Kp);
+        m = fmaxf(m, r < r_hi ? vv[c] : -CWQ_INF);
+        if (((t * 4 + c + 1) & (g - 1)) == 0) {
+          list64_offer(lk, lr, lane, m, r, Kp);
+          m = -CWQ_INF;
+        }
       }
     }
   }
@@ -1059,27 +1069,33 @@ hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void tighten_kernel(int nq, int K, int capq, const int* __restrict__ qcnt,
                                                       const int* __restrict__ qover, const float* __restrict__ cl,
-                                                      float* T, int64_t ldT) {
+                                                      float* T, int64_t ldT, float* lkb, int* lrb, int* done) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (q >= nq) return;
   const int n = min(qcnt[q], capq);
-  if (qover[q] || n < K) return;
+  if (qover[q]) return;
+  // incremental: the top-K candidate lower bounds so far are kept per query, and only the
+  // candidates appended since the last call are offered
+  const int d = done[q];
+  float tk = d ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
+  int tr = d ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
   const size_t base = (size_t)q * capq;
-  float tk = -CWQ_INF;
-  int tr = 0x7fffffff;
-  for (int j0 = 0; j0 < n; j0 += 64) {
+  for (int j0 = d; j0 < n; j0 += 64) {
     const int j = j0 + lane;
     list64_offer(tk, tr, lane, j < n ? cl[base + j] : -CWQ_INF, j, K);
   }
+  lkb[(size_t)q * 64 + lane] = tk;
+  lrb[(size_t)q * 64 + lane] = tr;
+  if (lane == 0) done[q] = n;
   const float kth = rl_f2(tk, K - 1);
   if (lane == 0 && kth > T[(size_t)q * ldT]) T[(size_t)q * ldT] = kth;
 }
 
 hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
-                          int64_t ldT, hipStream_t s) {
+                          int64_t ldT, float* lkb, int* lrb, int* done, hipStream_t s) {
   hipLaunchKernelGGL(tighten_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, nq, K, capq, qcnt, qover, cl, T,
-                     ldT);
+                     ldT, lkb, lrb, done);
   return hipGetLastError();
 }
 
@@ -1141,7 +1157,8 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
                                                     const RowMeta* __restrict__ meta, const int* __restrict__ par,
                                                     const float* __restrict__ P, int64_t ldP, int seg_base,
                                                     float* pkey, float* paux, int* prow, int64_t lstride,
-                                                    int* ok_flag, int* n_exact) {
+                                                    int* ok_flag, int* n_exact, const float* __restrict__ lkb,
+                                                    const int* __restrict__ lrb, const int* __restrict__ done) {
   __shared__ int s_pend[kWavesPerWG][128];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1154,10 +1171,12 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
   int nx = 0;
   if (ok) {
     const size_t base = (size_t)q * capq;
-    // pass 1: K-th largest lower bound
-    float tk = -CWQ_INF;
-    int tr = 0x7fffffff;
-    for (int j0 = 0; j0 < n; j0 += 64) {
+    // pass 1: K-th largest lower bound (continuing tighten's list: only the candidates
+    // of the last phase are offered)
+    const int d = done[q];
+    float tk = d ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
+    int tr = d ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
+    for (int j0 = d; j0 < n; j0 += 64) {
       const int j = j0 + lane;
       const float lv = j < n ? cl[base + j] : -CWQ_INF;
       list64_offer(tk, tr, lane, lv, j, K);
@@ -1241,9 +1260,10 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
-                        hipStream_t s) {
+                        const float* lkb, const int* lrb, const int* done, hipStream_t s) {
   hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
-                     crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact);
+                     crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact,
+                     lkb, lrb, done);
   return hipGetLastError();
 }
 
