@@ -199,7 +199,7 @@ def main():
         kern_ms = float(np.mean([t["fgemm_ms"] for t in tms]))
         flops_launch = 2.0 * D * NL * Qn
         peak, kname, pipe = PEAK_BF16_TFLOPS, "fgemm_kernel<0> (bf16 MFMA filter pass)", "bf16 MFMA dense"
-        launches = 3 if NL >= 16 * 256 else 1   # threshold phases over the row tiles (cwq_api.hip)
+        launches = max(1, round(float(np.mean([t["leaf_scan_launches"] for t in tms]))))   # filter phases
         phases = {"sample_ms": round(float(np.mean([t["sample_ms"] for t in tms])), 3),
                   "fgemm_ms": round(kern_ms, 3),
                   "rerank_ms": round(float(np.mean([t["rerank_ms"] for t in tms])), 3)}

@@ -113,6 +113,7 @@ struct cwq_index {
   // timing (cwq_set_timing)
   bool timing = false;
   int filter = -1;   // cwq_set_filter
+  int n_fg_launch = 0;   // filter launches of the last chunk (timing report)
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   float t_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // workspace
@@ -945,6 +946,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         HIPCHK(hipMemsetAsync(tdone, 0, (size_t)nqf * 4, s));
         int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
         const int nph = fg_phase_cuts(n_rt, cuts);
+        ix->n_fg_launch = nph;
         for (int ph = 0; ph < nph; ++ph) {
           g.rt_off = cuts[ph];
           g.n_rt = cuts[ph + 1] - cuts[ph];
@@ -1040,7 +1042,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       ix->t_ms[1] += b2;
       ix->t_ms[2] += c2;
       ix->t_ms[3] += d;
-      ix->t_ms[4] += filt ? 1 : (ix->NL_iso > 0) + (ix->NL_an > 0);
+      ix->t_ms[4] += filt ? ix->n_fg_launch : (ix->NL_iso > 0) + (ix->NL_an > 0);   // filter: fgemm launches
       if (filt) {
         float e3 = 0;
         HIPCHK(hipEventElapsedTime(&e3, ix->ev[6], ix->ev[7]));
