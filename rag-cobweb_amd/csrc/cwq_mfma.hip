@@ -222,6 +222,10 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
 #ifndef FG_PP
 #define FG_PP 1   // ping-pong wave groups (16x16x32 path only; 0: both waves of a SIMD per stage)
 #endif
+#ifndef FG_LEAN
+#define FG_LEAN 1   // filter tiles without records skip the flush's second barrier and the per-tile third one
+#endif
+#define FG_CSLOT (FG_LEAN && MODE == 0 && (tile_no & 1) ? 9 : 0)
 #ifndef FG_INTERLEAVE
 #define FG_INTERLEAVE 1   // measured +1% (and PRIO -6%) in one A/B
 #endif
@@ -365,7 +369,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   (void)tile_no;
   fg_decode(a, xcd, i, qt, rt);
   if (tid == 0) {
-    s_cnt[0] = 0;    // records of the current tile
+    s_cnt[0] = 0;    // records of the current tile (FG_LEAN: even tiles; odd tiles count in [9])
+    s_cnt[9] = 0;
     s_cnt[1] = -1;   // owned chunk
     s_cnt[2] = 0;    // its fill
   }
@@ -452,6 +457,9 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     if (dyn && tid == 0) s_cnt[8] = claimv;   // the tile after this one
     __syncthreads();   // stage 0 landed, setup visible
     if (dyn) next_i = __builtin_amdgcn_readfirstlane(s_cnt[8]);   // uniform: scalar tile loads
+    // FG_LEAN: the previous tile's record counter (every thread read it before this
+    // barrier) is cleared for the tile after this one
+    if (FG_LEAN && MODE == 0 && tid == 0 && tile_no > 0) s_cnt[(tile_no & 1) ? 0 : 9] = 0;
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
 #if FG_M16
     // 16x16x32 layout: acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
@@ -813,7 +821,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               fg_bounds(d, ex, qi, f, pi, a.eps_n, a.slack, u, lo);
               if (u >= qi.w) {
                 const int4 rv = make_int4(q, r, __float_as_int(u), __float_as_int(lo));
-                const int slot = atomicAdd(&s_cnt[0], 1);
+                const int slot = atomicAdd(&s_cnt[FG_CSLOT], 1);
                 if (slot < kFgCap) {
                   s_rec[slot] = rv;
                 } else {   // dense tile (small or clustered data): straight to the direct region
@@ -829,10 +837,13 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   flush:
     if (MODE == 0) {
       // records -> global append buffer, in chunks of kFgChunk slots owned by this
-      // workgroup (one atomic per chunk, not per tile)
+      // workgroup (one atomic per chunk, not per tile).  This barrier also ends every
+      // epilogue LDS read of the tile (wsc, s_qi/s_qv/s_pi), so the next setup may
+      // rewrite them; a tile without records skips the rest (uniform: all read cnt here).
       __syncthreads();
-      const int cnt = s_cnt[0];
+      const int cnt = s_cnt[FG_CSLOT];
       const int n = min(cnt, kFgCap);
+      if (FG_LEAN && n == 0) goto next_tile;
       if (tid == 0) {
         int chunk = s_cnt[1], fill = s_cnt[2];
         int n1 = chunk >= 0 ? min(n, kFgChunk - fill) : 0;
@@ -867,13 +878,16 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       if (tid < nw) a.rec[tid < n1 ? s_cnt[3] + tid : s_cnt[6] + (tid - n1)] = s_rec[tid];
       if (s_cnt[7] && tid < FT && q0 + tid < a.nq) a.qover[q0 + tid] = 1;   // re-run this tile's queries exactly
     }
+  next_tile:
     i = next_i;
     ++tile_no;
     if (i >= ntl) break;
     if (!dyn) next_i = i + nw_x;
     fg_decode(a, xcd, i, qt, rt);
-    __syncthreads();   // epilogue LDS reads done before the next setup rewrites them
-    if (tid == 0) s_cnt[0] = 0;
+    if (MODE != 0 || !FG_LEAN) {
+      __syncthreads();   // epilogue LDS reads done before the next setup rewrites them
+      if (tid == 0) s_cnt[0] = 0;
+    }
   }
   if (MODE == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
 }
