@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--queries", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--share-index", action="store_true",
+                    help="one index for every arm (same library; knobs read per call only)")
     ap.add_argument("--clusters", type=int, default=0, help="0: flat tree; G: root -> G random clusters -> leaves")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
@@ -68,6 +70,9 @@ def main():
         knobs[p] = dict(x.split("=", 1) for x in kv.split(";") if x)
     arms = []
     for p in paths:
+        if args.share_index and arms:
+            arms.append(arms[0])
+            continue
         with env(knobs[p]):
             L._lib = L.load_library(os.path.abspath(p.split("@")[0]))
             ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)

@@ -1,4 +1,2 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_filter.py tests/test_gpu_parity.py -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pyt.log 2>&1; rc=$?; tail -3 gpurun_out/pyt.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u scripts/ab_libs.py --rounds 10 --libs "rag-cobweb_amd/libcwq_base.so" --libs "rag-cobweb_amd/libcwq.so" > gpurun_out/ab5.log 2>&1; rc=$?; tail -3 gpurun_out/ab5.log; grep -c MISMATCH gpurun_out/ab5.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pf4 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --recall-queries 0 > gpurun_out/pf4.log 2>&1 || exit $?
+timeout -k 10 900 python -u scripts/ab_libs.py --n 10000000 --dim 1024 --queries 12500 --rounds 4 --share-index --libs "rag-cobweb_amd/libcwq.so@CWQ_FG_CUTS=64,256" --libs "rag-cobweb_amd/libcwq.so" > gpurun_out/ab7.log 2>&1; rc=$?; tail -3 gpurun_out/ab7.log; exit $rc
