@@ -183,3 +183,27 @@ def test_auto_mode_threshold(gpu):
     assert ix.last_stats()["filter_used"]          # >= 16384 iso rows, k <= 64
     ix.score_topk(Q, 70)
     assert not ix.last_stats()["filter_used"]      # k > 64: exact scan (full ranking path)
+
+
+@pytest.mark.parametrize("cuts,phases", [("64,256", None), ("8,16,32,64", None), ("1000", None), ("", None),
+                                         ("", "0")])
+def test_filter_phase_cuts(gpu, cuts, phases, monkeypatch):
+    """Any split of the row tiles into filter launches (CWQ_FG_CUTS, read per call; the
+    incremental tighten/final list carried across them, or no tighten at all with one
+    launch) returns the exact scan's answer.  A first launch over most of the rows runs
+    on the loose sample threshold alone and may overflow the record buffers: those
+    queries fall back to the exact scan, which is the designed outcome, so the fallback
+    count is bounded only for small first launches."""
+    N, D, k = 24000, 128, 10
+    X = gpu.synth.synthetic_corpus(N, D, seed=11)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, 512, seed=5)
+    monkeypatch.setenv("CWQ_FG_CUTS", cuts)
+    if phases is not None:
+        monkeypatch.setenv("CWQ_FG_PHASES", phases)
+    ids0, s0, ids1, s1, st = both(ix, Q, k)
+    assert st["filter_used"]
+    assert torch.equal(ids0, ids1)
+    assert torch.equal(s0, s1)
+    if cuts in ("64,256", "8,16,32,64"):
+        assert st["fallback_queries"] <= 20, st
