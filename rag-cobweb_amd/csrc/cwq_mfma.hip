@@ -920,20 +920,9 @@ hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_w
 // ---------------------------------------------------------------------------
 // bucket: appended records -> per-query candidate lists
 // ---------------------------------------------------------------------------
-__global__ void bucket_kernel(const int4* __restrict__ rec, const int* __restrict__ gctr,
-                              const int* __restrict__ chunk_fill, int64_t rec_cap, const int4* __restrict__ rec_dir,
-                              int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl) {
-  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int4 r;
-  if (g < rec_cap) {
-    const int chunk = (int)(g / kFgChunk);
-    if (chunk >= gctr[0] || (int)(g % kFgChunk) >= chunk_fill[chunk]) return;
-    r = rec[g];
-  } else {
-    const int64_t d = g - rec_cap;
-    if (d >= min(gctr[1], dir_cap)) return;
-    r = rec_dir[d];
-  }
+// one record into its query's candidate list
+__device__ __forceinline__ void bucket_one(const int4 r, int capq, int* qcnt, int* qover, int* crow, float* cu,
+                                           float* cl) {
   const int q = r.x;
   const int slot = atomicAdd(&qcnt[q], 1);
   if (slot < capq) {
@@ -946,11 +935,27 @@ __global__ void bucket_kernel(const int4* __restrict__ rec, const int* __restric
   }
 }
 
+// grid-stride over the claimed chunks only (gctr[0] of them) and the direct region: the
+// grid no longer scales with the buffer capacity (30k mostly idle workgroups at C3)
+__global__ __launch_bounds__(256) void bucket_kernel(const int4* __restrict__ rec, const int* __restrict__ gctr,
+                                                     const int* __restrict__ chunk_fill, int64_t rec_cap,
+                                                     const int4* __restrict__ rec_dir, int dir_cap, int capq,
+                                                     int* qcnt, int* qover, int* crow, float* cu, float* cl) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t g0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t n_rec = min((int64_t)gctr[0] * kFgChunk, rec_cap);
+  for (int64_t g = g0; g < n_rec; g += stride)
+    if ((int)(g % kFgChunk) < chunk_fill[g / kFgChunk]) bucket_one(rec[g], capq, qcnt, qover, crow, cu, cl);
+  const int n_dir = min(gctr[1], dir_cap);
+  for (int64_t d = g0; d < n_dir; d += stride) bucket_one(rec_dir[d], capq, qcnt, qover, crow, cu, cl);
+}
+
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s) {
   const int64_t n = rec_cap + dir_cap;
-  hipLaunchKernelGGL(bucket_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, gctr, chunk_fill, rec_cap,
-                     rec_dir, dir_cap, capq, qcnt, qover, crow, cu, cl);
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(bucket_kernel, dim3(grid), dim3(256), 0, s, rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap,
+                     capq, qcnt, qover, crow, cu, cl);
   return hipGetLastError();
 }
 
@@ -989,25 +994,22 @@ __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float
 // select: top-Kp values per query of a dense [nq][ld] array (the sample bounds; the
 // values are first reduced to maxima of up to 16 per lane)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u, int64_t ldu, int nrows, int Kp,
-                                                     float* cu, int* crow) {
-  __shared__ float sk[4][64];
-  __shared__ int sr[4][64];
-  const int q = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u, int64_t ldu, int nq, int nrows,
+                                                     int Kp, float* cu, int* crow) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (q >= nq) return;
   const float* uq = u + (size_t)q * ldu;
   float lk = -CWQ_INF;
   int lr = 0x7fffffff;
-  // each wave owns a contiguous range of whole 1024-row steps (16 values per lane per step;
-  // the buffer carries >= 1024 floats of tail slack, masked here)
+  // one wave per query over whole 1024-row steps (16 values per lane per step; the buffer
+  // carries >= 1024 floats of tail slack, masked here).  The K-th largest of maxima over
+  // g values of a lane (distinct rows, so still a lower bound of the K-th key): g up to
+  // 16 while at least 8*Kp maxima remain
   constexpr int STEP = 1024;
-  const int per = (int)(((int64_t)nrows + 4 * STEP - 1) / (4 * STEP)) * STEP;
-  const int r_lo = wave * per, r_hi = min(nrows, r_lo + per);
-  // the K-th largest of maxima over g values of a lane (distinct rows, so still a lower
-  // bound of the K-th key): g up to 16 while at least 8*Kp maxima remain
   int g = 16;
   while (g > 1 && nrows / g < 8 * Kp) g >>= 1;
-  for (int r0 = r_lo; r0 < r_hi; r0 += STEP) {
+  for (int r0 = 0; r0 < nrows; r0 += STEP) {
     float4 v4[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) v4[t] = *reinterpret_cast<const float4*>(uq + r0 + t * 256 + lane * 4);
@@ -1018,7 +1020,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int r = r0 + t * 256 + lane * 4 + c;
-        m = fmaxf(m, r < r_hi ? vv[c] : -CWQ_INF);
+        m = fmaxf(m, r < nrows ? vv[c] : -CWQ_INF);
         if (((t * 4 + c + 1) & (g - 1)) == 0) {
           list64_offer(lk, lr, lane, m, r, Kp);
           m = -CWQ_INF;
@@ -1026,14 +1028,14 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
       }
     }
   }
-  sk[wave][lane] = lk;
-  sr[wave][lane] = lr;
-  __syncthreads();
-  if (wave == 0) {
-    for (int w = 1; w < 4; ++w) list64_offer(lk, lr, lane, sk[w][lane], sr[w][lane], Kp);
-    cu[(size_t)q * 64 + lane] = lk;
-    crow[(size_t)q * 64 + lane] = lr;
-  }
+  cu[(size_t)q * 64 + lane] = lk;
+  crow[(size_t)q * 64 + lane] = lr;
+}
+
+hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s) {
+  hipLaunchKernelGGL(select_kernel, dim3((unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG)), dim3(256), 0, s, u, ldu,
+                     nq, nrows, Kp, cu, crow);
+  return hipGetLastError();
 }
 
 // Multi-parent row tiles: per (tile, query) the range of the parents' prefixes x invL, so
@@ -1072,10 +1074,6 @@ hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* 
   return hipGetLastError();
 }
 
-hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s) {
-  hipLaunchKernelGGL(select_kernel, dim3((unsigned)nq), dim3(256), 0, s, u, ldu, nrows, Kp, cu, crow);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
 // tighten: between filter phases, T[q] = max(T[q], K-th largest lower bound among the
