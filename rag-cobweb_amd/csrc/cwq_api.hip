@@ -704,7 +704,9 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
 // Query-chunk size that keeps the per-chunk workspace within ~2 GiB (min 128).
 int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
   const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
-  const size_t budget = (size_t)8 << 30;
+  // workspace budget per chunk of queries (8 GiB; CWQ_WS_BUDGET_MB for tests of the chunking)
+  const char* e = getenv("CWQ_WS_BUDGET_MB");
+  const size_t budget = e && atoll(e) > 0 ? (size_t)atoll(e) << 20 : (size_t)8 << 30;
   int64_t c = (int64_t)std::max<size_t>(kQPad, budget / std::max<size_t>(per_q, 1));
   c = std::max<int64_t>(kQPad, c / kQPad * kQPad);
   return std::min(nq, c);

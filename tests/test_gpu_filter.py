@@ -207,3 +207,21 @@ def test_filter_phase_cuts(gpu, cuts, phases, monkeypatch):
     assert torch.equal(s0, s1)
     if cuts in ("64,256", "8,16,32,64"):
         assert st["fallback_queries"] <= 20, st
+
+
+@pytest.mark.parametrize("filt", [0, 1])
+def test_query_chunking(gpu, filt, monkeypatch):
+    """A batch larger than one workspace chunk (CWQ_WS_BUDGET_MB shrinks the 8 GiB budget,
+    so the call splits into several query chunks — whole 256-query tiles on the filter
+    path) returns what one chunk returns, ids and scores bit-identical."""
+    N, D, k = 20000, 96, 10
+    X = gpu.synth.synthetic_corpus(N, D, seed=21)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, 1500, seed=22)
+    ix.set_filter(filt)
+    ids0, s0 = ix.score_topk(Q, k)
+    monkeypatch.setenv("CWQ_WS_BUDGET_MB", "1")
+    ids1, s1 = ix.score_topk(Q, k)
+    ix.set_filter(-1)
+    assert torch.equal(ids0.cpu(), ids1.cpu())
+    assert torch.equal(s0.cpu(), s1.cpu())
