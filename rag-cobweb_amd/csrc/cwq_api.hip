@@ -873,12 +873,15 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         float* lb = b.take<float>((size_t)nqf * ix->ld_s + 4096);
         float* tl = b.take<float>((size_t)nqf * 64);
         int* tr = b.take<int>((size_t)nqf * 64);
-        // [qcnt | ok | n_exact], contiguous: the host reads all three with one copy
-        int* qcnt = b.take<int>((size_t)3 * nqf);
+        // [qcnt | ok | n_exact | qover | tdone | gctr]: the host reads the first three with one
+        // copy; one memset clears the block before the filter launches (tighten_kernel
+        // clears gctr between them)
+        int* qcnt = b.take<int>((size_t)5 * nqf + 64);
         okf = qcnt + nqf;
         int* nex = qcnt + 2 * nqf;
-        int* qover = b.take<int>(nqf);
-        int* tdone = b.take<int>(nqf);                     // tighten/final incremental state
+        int* qover = qcnt + 3 * nqf;
+        int* tdone = qcnt + 4 * nqf;                       // tighten/final incremental state
+        int* gctr = qcnt + 5 * nqf;
         float* tlk = b.take<float>((size_t)nqf * 64);
         int* crow = b.take<int>((size_t)nqf * kFgCapQ);
         float* cu = b.take<float>((size_t)nqf * kFgCapQ);
@@ -888,7 +891,6 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                                          kFgChunk);
         int4* rec = b.take<int4>((size_t)rec_cap);
         int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
-        int* gctr = b.take<int>(64);
         const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
         int4* rec_dir = b.take<int4>((size_t)dir_cap);
         float2* pmm = ix->n_multi_tiles ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
@@ -928,9 +930,9 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.ldlb = ix->ld_s / g.lbg;
         HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
         HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
-        // 2. filter passes over row-tile phases (1/16, 3/16, 12/16 of the rows); after
-        // each phase the candidates go to per-query lists and T[q] is raised to the K-th
-        // largest candidate lower bound, so later phases emit fewer candidates
+        // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
+        // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is
+        // raised to the K-th largest candidate lower bound, so later phases emit fewer
         g.mode = 0;
         g.nrows = ix->NL_iso;
         g.rowmap = nullptr;
@@ -943,9 +945,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.qover = qover;
         g.rec_dir = rec_dir;
         g.dir_cap = dir_cap;
-        HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)nqf * 4, s));
-        HIPCHK(hipMemsetAsync(qover, 0, (size_t)nqf * 4, s));
-        HIPCHK(hipMemsetAsync(tdone, 0, (size_t)nqf * 4, s));
+        HIPCHK(hipMemsetAsync(qcnt, 0, ((size_t)5 * nqf + 64) * 4, s));
         int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
         const int nph = fg_phase_cuts(n_rt, cuts);
         ix->n_fg_launch = nph;
@@ -954,7 +954,6 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           g.n_rt = cuts[ph + 1] - cuts[ph];
           g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt &&
                           !getenv("CWQ_FG_NO_ALLUNI");
-          HIPCHK(hipMemsetAsync(gctr, 0, 64, s));
           if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
           unsigned long long* stamp_d = nullptr;
           const char* stamp_f = ph == nph - 1 ? getenv("CWQ_FG_STAMP") : nullptr;   // diagnostic builds
@@ -989,7 +988,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl,
                                s));
           if (ph + 1 < nph)
-            HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, tlk, tr, tdone, s));
+            HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, tlk, tr, tdone, gctr, s));
         }
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;

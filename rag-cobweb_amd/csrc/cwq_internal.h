@@ -206,9 +206,10 @@ hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* 
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
 // lkb/lrb [nq][64] and done [nq] carry each query's top-K candidate lower bounds between
-// the tighten calls and into final (done must start at 0)
+// the tighten calls and into final (done must start at 0); zero16[0..15] is cleared
+// (the filter's record and tile-claim counters for the next launch)
 hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
-                          int64_t ldT, float* lkb, int* lrb, int* done, hipStream_t s);
+                          int64_t ldT, float* lkb, int* lrb, int* done, int* zero16, hipStream_t s);
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,

@@ -1081,8 +1081,11 @@ hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void tighten_kernel(int nq, int K, int capq, const int* __restrict__ qcnt,
                                                       const int* __restrict__ qover, const float* __restrict__ cl,
-                                                      float* T, int64_t ldT, float* lkb, int* lrb, int* done) {
+                                                      float* T, int64_t ldT, float* lkb, int* lrb, int* done,
+                                                      int* zero16) {
   const int lane = threadIdx.x & 63;
+  // the filter's record/tile counters for the next launch (bucket has read them)
+  if (blockIdx.x == 0 && threadIdx.x < 16) zero16[threadIdx.x] = 0;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (q >= nq) return;
   const int n = min(qcnt[q], capq);
@@ -1105,9 +1108,9 @@ __global__ __launch_bounds__(256) void tighten_kernel(int nq, int K, int capq, c
 }
 
 hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
-                          int64_t ldT, float* lkb, int* lrb, int* done, hipStream_t s) {
+                          int64_t ldT, float* lkb, int* lrb, int* done, int* zero16, hipStream_t s) {
   hipLaunchKernelGGL(tighten_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, nq, K, capq, qcnt, qover, cl, T,
-                     ldT, lkb, lrb, done);
+                     ldT, lkb, lrb, done, zero16);
   return hipGetLastError();
 }
 
