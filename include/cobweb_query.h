@@ -18,8 +18,11 @@
  *   - Node numbering is the reference's BFS order (CobwebWrapper.py:107-132):
  *     node 0 is the root and the children of a node are consecutive, in the
  *     order of its children list.  Sentence ids are the reference's sentence ids.
- *   - One query call at a time per index handle (the handle owns its workspace);
- *     use one handle per device / per concurrent stream.
+ *   - A handle serialises its query calls (host mutex) and owns one device
+ *     workspace.  Calls may be issued on different streams: each call makes its
+ *     stream wait for the previous call's work (an event recorded at the end of every
+ *     call), so the workspace is never shared by two in-flight calls.  For concurrent
+ *     execution use one handle per stream.
  */
 #ifndef COBWEB_QUERY_H
 #define COBWEB_QUERY_H
@@ -41,6 +44,11 @@ typedef struct cwq_index cwq_index;
 
 /* Library version (major*10000 + minor*100 + patch). */
 int cwq_version(void);
+
+/* Build id: a hash of the sources, this header and the compile flags the library was
+ * built from (rag-cobweb_amd/build.py); the Python binding refuses a library whose id
+ * differs from the sources next to it. */
+const char* cwq_build_id(void);
 
 /* Thread-local message describing the last error on this thread. */
 const char* cwq_last_error(void);
@@ -71,7 +79,13 @@ int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean
 int cwq_index_destroy(cwq_index* idx);
 
 /* Index facts: out[0]=n_nodes out[1]=dim out[2]=n_sent out[3]=internal nodes
- * out[4]=leaf-class rows out[5]=isotropic rows out[6]=max depth out[7]=device bytes */
+ * out[4]=leaf-class rows out[5]=isotropic rows out[6]=max depth out[7]=device bytes
+ * (the handle's own copies; the workspace grows on demand up to ~8 GiB per call).
+ * Device footprint per node row: internal nodes 8*DP B (1/sigma, mu/sigma), isotropic
+ * leaf rows 4*DP (dim-major mean) + 4*DP (row-major mean) + 2*DPB (bf16) + 32 B,
+ * anisotropic leaf rows 8*DP B; C3 (1M x 768) 7.8 GB, C4 (10M x 1024) 104 GB -- the
+ * largest flat tree one 288 GB MI355X holds is ~25M x 1024 (the caller may free its
+ * mean/var tensors after cwq_index_create). */
 int cwq_index_info(const cwq_index* idx, int64_t* out8);
 
 /*

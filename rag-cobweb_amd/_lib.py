@@ -24,6 +24,7 @@ _I64 = _c.c_int64
 _I32 = _c.c_int32
 SIGNATURES = {
     "cwq_version": (_c.c_int, []),
+    "cwq_build_id": (_c.c_char_p, []),
     "cwq_last_error": (_c.c_char_p, []),
     "cwq_index_create": (_c.c_int, [_c.c_int, _I64, _I32, _P, _P, _P, _P, _I64, _P, _I32, _P, _c.POINTER(_P)]),
     "cwq_index_destroy": (_c.c_int, [_P]),
@@ -67,11 +68,19 @@ def load_library(path):
 
 
 def lib():
-    """Load libcwq.so (once).  Raises ImportError when it is not built."""
+    """Load libcwq.so (once).  Raises ImportError when it is not built, or when it was
+    built from other sources than the ones in csrc/ (stale binary: rebuild it)."""
     global _lib
     with _lock:
         if _lib is None:
-            _lib = load_library(LIB_PATH)
+            L = load_library(LIB_PATH)
+            if not os.environ.get("CWQ_LIB"):
+                from .build import source_id
+                got, want = L.cwq_build_id().decode(), source_id()
+                if got != want:
+                    raise ImportError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                                      f"rebuild it with __graft_entry__.build()")
+            _lib = L
     return _lib
 
 

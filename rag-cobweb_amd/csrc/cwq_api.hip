@@ -116,12 +116,21 @@ struct cwq_index {
   int n_fg_launch = 0;   // filter launches of the last chunk (timing report)
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   float t_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // workspace
+  // workspace.  Every query call carves its buffers from `ws`; the call's kernels may
+  // still be running when it returns, so the end of each call records `ws_ev` on its
+  // stream and the next call makes its own stream wait for it (ws_begin / ws_end):
+  // calls on different streams reuse the workspace in order.
   std::mutex mu;
   void* ws = nullptr;
   size_t ws_size = 0;
+  hipEvent_t ws_ev = nullptr;
+  bool ws_ev_live = false;
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
   size_t hflags_n = 0;
+  // fallback re-runs (cwq_score_topk / cwq_categorize): gathered queries, their results
+  // and the device index lists, kept between calls (grown on demand)
+  void* fb = nullptr;
+  size_t fb_size = 0;
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -142,6 +151,7 @@ struct cwq_index {
   }
   int reserve(size_t b) {
     if (b <= ws_size) return CWQ_OK;
+    if (ws_ev_live) (void)hipEventSynchronize(ws_ev);   // earlier calls' kernels may still read it
     if (ws) (void)hipFree(ws);
     ws = nullptr;
     ws_size = 0;
@@ -150,11 +160,38 @@ struct cwq_index {
     ws_size = b;
     return CWQ_OK;
   }
+  int reserve_fb(size_t b) {
+    if (b <= fb_size) return CWQ_OK;
+    if (ws_ev_live) (void)hipEventSynchronize(ws_ev);
+    if (fb) (void)hipFree(fb);
+    fb = nullptr;
+    fb_size = 0;
+    b = round_up((int64_t)b, 1 << 20);
+    if (hipMalloc(&fb, b) != hipSuccess) return fail(CWQ_ERR_OOM, "fallback hipMalloc failed (" + std::to_string(b) + " B)");
+    fb_size = b;
+    return CWQ_OK;
+  }
+  // start of a query call on stream s: wait for the previous call's use of the workspace
+  int ws_begin(hipStream_t s) {
+    if (!ws_ev && hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming) != hipSuccess)
+      return fail(CWQ_ERR_HIP, "hipEventCreate failed");
+    if (ws_ev_live && hipStreamWaitEvent(s, ws_ev, 0) != hipSuccess) return fail(CWQ_ERR_HIP, "hipStreamWaitEvent failed");
+    return CWQ_OK;
+  }
+  // end of a query call: the workspace is busy until the work queued on s so far is done
+  int ws_end(hipStream_t s) {
+    if (hipEventRecord(ws_ev, s) != hipSuccess) return fail(CWQ_ERR_HIP, "hipEventRecord failed");
+    ws_ev_live = true;
+    return CWQ_OK;
+  }
   ~cwq_index() {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (ws_ev_live) (void)hipEventSynchronize(ws_ev);
+    if (ws_ev) (void)hipEventDestroy(ws_ev);
     for (void* p : allocs) (void)hipFree(p);
     if (ws) (void)hipFree(ws);
+    if (fb) (void)hipFree(fb);
     if (hflags) (void)hipHostFree(hflags);
   }
   int host_flags(size_t n) {
@@ -169,7 +206,22 @@ struct cwq_index {
   }
 };
 
-extern "C" int cwq_version(void) { return 100; }
+// RAII: a query entry point's use of the handle workspace on stream s (cwq_index::ws_begin)
+struct WsUse {
+  cwq_index* ix;
+  hipStream_t s;
+  int rc;
+  WsUse(cwq_index* i, hipStream_t st) : ix(i), s(st) { rc = ix->ws_begin(s); }
+  ~WsUse() { (void)ix->ws_end(s); }
+};
+
+#ifndef CWQ_BUILD_ID
+#define CWQ_BUILD_ID "unversioned"
+#endif
+extern "C" int cwq_version(void) { return 200; }
+// "CWQ_BUILD_ID=<id>" is also searched for in the file by build.py (no dlopen needed)
+static const char kBuildId[] = "CWQ_BUILD_ID=" CWQ_BUILD_ID;
+extern "C" const char* cwq_build_id(void) { return kBuildId + 13; }
 extern "C" const char* cwq_last_error(void) { return g_err.c_str(); }
 
 namespace {
@@ -701,7 +753,8 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
   }
 }
 
-// Query-chunk size that keeps the per-chunk workspace within ~2 GiB (min 128).
+// Query-chunk size that keeps the per-chunk workspace within the budget (8 GiB by
+// default, CWQ_WS_BUDGET_MB; at least 128 queries).
 int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
   const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
   // workspace budget per chunk of queries (8 GiB; CWQ_WS_BUDGET_MB for tests of the chunking)
@@ -780,33 +833,25 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
 // Queries whose certificate failed: exact scan, results scattered back in place.
 int rerun_exact(cwq_index* ix, const float* q, const std::vector<int64_t>& qi, int32_t k, int64_t* ids, float* scores,
                 hipStream_t s) {
+  // buffers from the handle's fallback region; one gather launch in, one scatter out
   const int64_t n = (int64_t)qi.size();
-  float* tq = nullptr;
-  float* ts = nullptr;
-  int64_t* tid = nullptr;
   const size_t D = (size_t)ix->D;
-  if (hipMalloc(&tq, n * D * 4) != hipSuccess || hipMalloc(&tid, n * k * 8) != hipSuccess ||
-      (scores && hipMalloc(&ts, n * k * 4) != hipSuccess)) {
-    (void)hipFree(tq);
-    (void)hipFree(tid);
-    return fail(CWQ_ERR_OOM, "fallback buffers");
-  }
-  int rc = CWQ_OK;
-  for (int64_t i = 0; i < n && rc == CWQ_OK; ++i)
-    if (hipMemcpyAsync(tq + i * D, q + qi[i] * D, D * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      rc = fail(CWQ_ERR_HIP, "fallback gather");
-  if (rc == CWQ_OK) rc = score_topk_impl(ix, tq, n, k, tid, ts, s, false);
-  for (int64_t i = 0; i < n && rc == CWQ_OK; ++i) {
-    if (hipMemcpyAsync(ids + qi[i] * k, tid + i * k, (size_t)k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-        (scores && hipMemcpyAsync(scores + qi[i] * k, ts + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s) !=
-                       hipSuccess))
-      rc = fail(CWQ_ERR_HIP, "fallback scatter");
-  }
-  if (hipStreamSynchronize(s) != hipSuccess && rc == CWQ_OK) rc = fail(CWQ_ERR_HIP, "fallback sync");
-  (void)hipFree(tq);
-  (void)hipFree(tid);
-  if (ts) (void)hipFree(ts);
-  return rc;
+  const size_t o_tq = round_up(n * 8, 256), o_tid = o_tq + round_up(n * D * 4, 256),
+               o_ts = o_tid + round_up((int64_t)n * k * 8, 256), tot = o_ts + round_up((int64_t)n * k * 4, 256);
+  int rc = ix->reserve_fb(tot);
+  if (rc) return rc;
+  char* fb = (char*)ix->fb;
+  int64_t* d_idx = (int64_t*)fb;
+  float* tq = (float*)(fb + o_tq);
+  int64_t* tid = (int64_t*)(fb + o_tid);
+  float* ts = scores ? (float*)(fb + o_ts) : nullptr;
+  HIPCHK(hipMemcpyAsync(d_idx, qi.data(), n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(launch_copy_rows(q, (int64_t)D, d_idx, tq, (int64_t)D, nullptr, n, (int64_t)D, s));
+  if ((rc = score_topk_impl(ix, tq, n, k, tid, ts, s, false))) return rc;
+  HIPCHK(launch_copy_rows(tid, 2 * (int64_t)k, nullptr, ids, 2 * (int64_t)k, d_idx, n, 2 * (int64_t)k, s));
+  if (scores) HIPCHK(launch_copy_rows(ts, k, nullptr, scores, k, d_idx, n, k, s));
+  HIPCHK(hipStreamSynchronize(s));   // qi (pageable host memory) must outlive the upload
+  return CWQ_OK;
 }
 
 int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
@@ -926,7 +971,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         // large samples: lower bounds reduced to maxima over groups of 4 rows in the
         // kernel (fgemm_kernel<1>); small ones keep one value per row so that K groups exist
         g.lb = lb;
-        g.lbg = (FG_M16 && ix->n_samp >= 64 * K) ? 4 : 1;
+        g.lbg = ix->n_samp >= 64 * K ? 4 : 1;
         g.ldlb = ix->ld_s / g.lbg;
         HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
         HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
@@ -1077,7 +1122,10 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   DevGuard dg(ix->device);
   for (float& t : ix->t_ms) t = 0.f;
   for (int64_t& t : ix->stats) t = 0;
-  return score_topk_impl(ix, q, nq, k, ids, scores, (hipStream_t)stream, true);
+  hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  if (wu.rc) return wu.rc;
+  return score_topk_impl(ix, q, nq, k, ids, scores, s, true);
 }
 
 extern "C" int cwq_set_filter(cwq_index* ix, int mode) {
@@ -1114,6 +1162,8 @@ extern "C" int cwq_rank_scores(cwq_index* ix, const float* q, int64_t nq, float*
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  if (wu.rc) return wu.rc;
   const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
   int rc;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
@@ -1139,6 +1189,8 @@ extern "C" int cwq_node_logprob(cwq_index* ix, const float* q, int64_t nq, int32
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  if (wu.rc) return wu.rc;
   const float dconst = full ? (float)((double)ix->D * (double)logf(2.0f * (float)M_PI)) : 0.f;
   const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
   int rc;
@@ -1168,6 +1220,8 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  if (wu.rc) return wu.rc;
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   const int R = std::max(1, std::min(64, ix->NL));
   const bool complete = ix->NL <= R;
@@ -1265,9 +1319,12 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
       int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
       int* found2 = b2.take<int>(ns_pad);
       int64_t* calls2 = b2.take<int64_t>(ns_pad);
-      for (int i = 0; i < ns; ++i)
-        HIPCHK(hipMemcpyAsync(qsub + (size_t)i * ix->D, q + (q0 + redo[r0 + i]) * ix->D, ix->D * sizeof(float),
-                              hipMemcpyDeviceToDevice, s));
+      std::vector<int64_t> gq(ns);   // global query index of each hard query
+      for (int i = 0; i < ns; ++i) gq[i] = q0 + redo[r0 + i];
+      if ((rc = ix->reserve_fb((size_t)ns * 8))) return rc;
+      int64_t* d_gq = (int64_t*)ix->fb;
+      HIPCHK(hipMemcpyAsync(d_gq, gq.data(), (size_t)ns * 8, hipMemcpyHostToDevice, s));
+      HIPCHK(launch_copy_rows(q, ix->D, d_gq, qsub, ix->D, nullptr, ns, ix->D, s));
       HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
       if ((rc = run_internal(ix, c2, s))) return rc;
       if ((rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1, nullptr,
@@ -1290,13 +1347,10 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
       sd.n_calls = calls2;
       sd.status = status2;
       HIPCHK(launch_simulate(sd, s));
-      for (int i = 0; i < ns; ++i) {
-        const int64_t qq = q0 + redo[r0 + i];
-        HIPCHK(hipMemcpyAsync(nodes + qq * k, nodes2 + (size_t)i * k, k * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipMemcpyAsync(n_found + qq, found2 + i, sizeof(int), hipMemcpyDeviceToDevice, s));
-        if (n_calls) HIPCHK(hipMemcpyAsync(n_calls + qq, calls2 + i, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-      }
-      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(launch_copy_rows(nodes2, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_gq, ns, 2 * (int64_t)k, s));
+      HIPCHK(launch_copy_rows(found2, 1, nullptr, n_found, 1, d_gq, ns, 1, s));
+      if (n_calls) HIPCHK(launch_copy_rows(calls2, 2, nullptr, n_calls, 2, d_gq, ns, 2, s));
+      HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
     }
   }
   return CWQ_OK;

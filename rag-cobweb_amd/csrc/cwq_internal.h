@@ -85,6 +85,9 @@ struct SimArgs {
 
 // ---- launchers (cwq_kernels.hip) ----
 hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s);
+// rows of `words` 4-byte words: dst[di ? di[i] : i] = src[si ? si[i] : i] (strides in words)
+hipError_t launch_copy_rows(const void* src, int64_t src_stride_w, const int64_t* src_idx, void* dst,
+                            int64_t dst_stride_w, const int64_t* dst_idx, int64_t n, int64_t words, hipStream_t s);
 hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s);
 // mode 0: dst = mean, 1: dst = 1/sqrt(var), 2: dst = mean/sqrt(var)
 hipError_t launch_gather_T(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n, int mode,
@@ -156,10 +159,6 @@ struct TileF {
   float pad1;
 };
 constexpr int kFgMaxTileParents = 64;   // uniform 2 only up to this many parents per tile
-// fgemm MFMA shape: 1 = v_mfma_f32_16x16x32_bf16 (default), 0 = 32x32x16 (A/B builds)
-#ifndef FG_M16
-#define FG_M16 1
-#endif
 
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)

@@ -799,6 +799,26 @@ hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64
   return hipGetLastError();
 }
 
+// Row gather/scatter in 4-byte words: dst[(di ? di[i] : i) * dst_stride + w] =
+// src[(si ? si[i] : i) * src_stride + w] for i < n, w < words.  One launch replaces the
+// per-row hipMemcpyAsync loops of the fallback paths (queries in, results out).
+__global__ void copy_rows_kernel(const int* __restrict__ src, int64_t src_stride, const int64_t* __restrict__ si,
+                                 int* dst, int64_t dst_stride, const int64_t* __restrict__ di, int64_t n,
+                                 int64_t words) {
+  for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t a = si ? si[i] : i, b = di ? di[i] : i;
+    for (int64_t w = threadIdx.x; w < words; w += blockDim.x) dst[b * dst_stride + w] = src[a * src_stride + w];
+  }
+}
+
+hipError_t launch_copy_rows(const void* src, int64_t src_stride_w, const int64_t* src_idx, void* dst,
+                            int64_t dst_stride_w, const int64_t* dst_idx, int64_t n, int64_t words, hipStream_t s) {
+  if (n <= 0 || words <= 0) return hipSuccess;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(words >= 256 ? 256 : 64), 0, s,
+                     (const int*)src, src_stride_w, src_idx, (int*)dst, dst_stride_w, dst_idx, n, words);
+  return hipGetLastError();
+}
+
 // flags[r] = 1 when var[node[r], :] is one value repeated (bitwise).
 __global__ void iso_flags_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
                                  int* flags) {

@@ -25,13 +25,15 @@
 //   Queries whose lists overflow (or have no usable threshold) are flagged and re-run
 //   by the exact scan, so the result never depends on the filter's statistics.
 //
-// CDNA4 mapping of fgemm: persistent, one 512-thread workgroup per CU, 256 queries x
-// 256 rows per tile, 8 waves as 2 (queries) x 4 (rows), each 128 x 64 = 4 x 2
-// v_mfma_f32_32x32x16_bf16 accumulators; K staged 64 deep by global_load_lds (16 B per
-// lane) into two LDS buffers (128 KiB), XOR-swizzled 16-B chunks (conflict-free
-// ds_read_b128), next stage (or the next tile's first stage) in flight during the
-// MFMAs.  Tiles are split over the 8 XCDs by query group so each XCD keeps its query
-// panel in L2 while all XCDs stream the same row panels (Infinity-Cache sharing).
+// CDNA4 mapping of fgemm: persistent, one 512-thread workgroup per CU,
+// 256 queries x 256 rows per tile, 8 waves as 2 (queries) x 4 (rows), each 128 x 64 =
+// 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators; K staged 32 deep by global_load_lds (16 B
+// per lane) into a 4-buffer LDS ring (128 KiB: three stages in flight while one is
+// consumed), XOR-swizzled 16-B chunks (conflict-free ds_read_b128); ping-pong wave
+// groups (waves 0-3 / 4-7 one barrier interval apart: one wave per SIMD issues its MFMA
+// cluster while its partner stages and reads the next stage).  Tiles are split over the
+// 8 XCDs by query group so each XCD keeps its query panel in L2 while all XCDs stream
+// the same row panels; within an XCD, tiles are claimed from a per-XCD counter.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -210,31 +212,18 @@ __device__ __forceinline__ int fg_count(const FgArgs& a, int xcd) {
   return nq_l * nr_l;
 }
 
-#ifndef FG_PRIO
-#define FG_PRIO 0
-#endif
 #ifndef FG_STAMP
 #define FG_STAMP 0   // diagnostic builds: s_memtime stamps of the ping-pong loop (FgArgs::stamp)
-#endif
-#ifndef FG_SADDR
-#define FG_SADDR 1
-#endif
-#ifndef FG_PP
-#define FG_PP 1   // ping-pong wave groups (16x16x32 path only; 0: both waves of a SIMD per stage)
 #endif
 #ifndef FG_LEAN
 #define FG_LEAN 1   // filter tiles without records skip the flush's second barrier and the per-tile third one
 #endif
 #define FG_CSLOT (FG_LEAN && MODE == 0 && (tile_no & 1) ? 9 : 0)
-#ifndef FG_INTERLEAVE
-#define FG_INTERLEAVE 1   // measured +1% (and PRIO -6%) in one A/B
-#endif
 // 16-B chunk position of logical chunk 0 in row r of a stage image (a permutation of the
-// row's 4 chunks, XORed with the chunk index).  Chosen per MFMA shape so that the
-// ds_read_b128 fragment reads of a wave are bank-conflict free:
-//   32x32x16: lane l reads row l&31, chunk 2kk + (l>>5)      -> f = (r>>2)&3
-//   16x16x32: lane l reads row l&15, chunk l>>4              -> f = (4 - ((r>>2)&3))&3
-__device__ __forceinline__ int fg_swz(int r) { return FG_M16 ? (4 - ((r >> 2) & 3)) & 3 : (r >> 2) & 3; }
+// row's 4 chunks, XORed with the chunk index), chosen so that the ds_read_b128 fragment
+// reads of a wave are bank-conflict free: for 16x16x32 lane l reads row l&15, chunk
+// l>>4 -> f = (4 - ((r>>2)&3))&3.
+__device__ __forceinline__ int fg_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
 
 // one K stage (32 deep) of both operands into an LDS stage buffer: 4 glds per wave.
 // Image: [256 rows][64 B] per operand; 16-B chunk c of row r sits at position
@@ -247,7 +236,6 @@ __device__ __forceinline__ int fg_swz(int r) { return FG_M16 ? (4 - ((r >> 2) & 
 // computed on the scalar unit from the wave-uniform wave index.
 __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __bf16* __restrict__ Mb, int DPB, int q0,
                                          int r0, int k0, char* sb, int wave, const uint32_t* loff, int ipart = -1) {
-#if FG_SADDR
   const char* gA = reinterpret_cast<const char*>(Xb) + ((size_t)q0 * DPB + k0) * 2;
   const char* gB = reinterpret_cast<const char*>(Mb) + ((size_t)r0 * DPB + k0) * 2;
 #pragma unroll
@@ -257,20 +245,6 @@ __device__ __forceinline__ void fg_stage(const __bf16* __restrict__ Xb, const __
     __builtin_amdgcn_global_load_lds((glb_void*)(gB + loff[i]), (lds_void*)(sb + FT * 64 + (wave * 32 + i * 16) * 64), 16,
                                      0, 0);
   }
-#else
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if (ipart >= 0 && i != ipart) continue;
-    const int row = wave * 32 + i * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ fg_swz(row);
-    const __bf16* ga = Xb + (size_t)(q0 + row) * DPB + k0 + c * 8;
-    const __bf16* gb = Mb + (size_t)(r0 + row) * DPB + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((glb_void*)ga, (lds_void*)(sb + (wave * 32 + i * 16) * 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)gb, (lds_void*)(sb + FT * 64 + (wave * 32 + i * 16) * 64), 16, 0, 0);
-  }
-  (void)loff;
-#endif
 }
 
 // A tile's TileF (wave-uniform) through the constant address space: scalar loads,
@@ -296,13 +270,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   __shared__ __attribute__((aligned(16))) char smem[FLDS];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-#if FG_SADDR
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-#else
-  const int wave = tid >> 6;
-#endif
   const int wq = wave & 1, wr = wave >> 1;
-  const int h = lane >> 5, l31 = lane & 31;
   const int xcd = blockIdx.x & 7;
   const int lw = blockIdx.x >> 3;
   const int nw_x = ((int)gridDim.x - xcd + 7) >> 3;
@@ -324,15 +293,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   }
   // fragment read offsets (bytes) within an operand image; the swizzle term is the
   // same for every 32-row block, so one per-lane value per k-substep
-#if FG_M16
   const int r16 = lane & 15, c16 = lane >> 4;
   const int foff16 = r16 * 64 + ((c16 ^ fg_swz(r16)) << 4);
-#else
-  const int fsw = fg_swz(l31);
-  int foff[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) foff[kk] = l31 * 64 + (((2 * kk + h) ^ fsw) << 4);
-#endif
 
   // stage ring: stages are numbered over this workgroup's whole tile sequence, so the
   // next tile's first stages are in flight during the current tile's last steps
@@ -374,11 +336,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     s_cnt[1] = -1;   // owned chunk
     s_cnt[2] = 0;    // its fill
   }
-#if FG_M16
   f32x4 acc[8][4];
-#else
-  f32x16 acc[4][2];
-#endif
   for (;;) {
     const int q0 = qt * FT, r0 = rt * FT;
     // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
@@ -403,21 +361,12 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       if (qs < a.nq && MODE == 0) Tq = a.T[(size_t)qs * a.ldT];
       if (uni && tf.par >= 0 && qs < a.nq) Pq = a.P[(size_t)qs * a.ldP + tf.par];
     }
-#if FG_M16
     float R0[4];
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
       const int r = r0 + wr * 64 + jb * 16 + r16;
       R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
     }
-#else
-    float R0[2];
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      const int r = r0 + wr * 64 + jb * 32 + l31;
-      R0[jb] = (uni && r < a.nrows) ? a.rf[r].R0 : 0.f;
-    }
-#endif
     if (tid < FT) {
       const float T = Tq;
       qi.w = T;
@@ -461,7 +410,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // barrier) is cleared for the tile after this one
     if (FG_LEAN && MODE == 0 && tid == 0 && tile_no > 0) s_cnt[(tile_no & 1) ? 0 : 9] = 0;
     // ---- accumulator init: R_r - Qv_q on uniform tiles, 0 otherwise ----
-#if FG_M16
     // 16x16x32 layout: acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
 #pragma unroll
     for (int ib = 0; ib < 8; ++ib) {
@@ -475,60 +423,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         acc[ib][jb][3] = R0[jb] - qv4.w;
       }
     }
-    // ---- K loop: one 32-deep v_mfma_f32_16x16x32_bf16 substep per stage; the barrier
-    // sits between the two halves of the MFMAs (query blocks 0-3 | 4-7), the next
-    // stage's fragments are read after it, under the second half.  Two fragment sets,
-    // the loop unrolled by two so they alternate without copies.
-    bf16x8 xa0[8], xb0[4], xa1[8], xb1[4];
-    auto load16 = [&](bf16x8* fa, bf16x8* fb, const char* sb) {
-      const char* sA = sb + wq * 128 * 64 + foff16;
-      const char* sB = sb + FT * 64 + wr * 64 * 64 + foff16;
-#pragma unroll
-      for (int ib = 0; ib < 8; ++ib) fa[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 1024);
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) fb[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 1024);
-    };
-    auto mfma16 = [&](const bf16x8* fa, const bf16x8* fb, int ib0) {
-#pragma unroll
-      for (int ib = ib0; ib < ib0 + 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ib], fb[jb], acc[ib][jb], 0, 0, 0);
-    };
-    auto step16 = [&](const bf16x8* ca, const bf16x8* cb, bf16x8* na, bf16x8* nb) {
-      issue_next();
-#if FG_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-      mfma16(ca, cb, 0);
-#if FG_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      ++gs;
-      const int n_out = issued - gs - 1;
-      if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (!(a.dbg & 128)) load16(na, nb, smem + (gs & (FNBUF - 1)) * FSTAGE);   // unconditional: keeps lgkmcnt counted
-#if FG_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-      mfma16(ca, cb, 4);
-#if FG_INTERLEAVE
-      // one fragment read between consecutive MFMAs of the second half
-#pragma unroll
-      for (int g = 0; g < 12; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x0008, 4, 0);
-#endif
-#if FG_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-    };
-#if FG_PP
+    // ---- K loop: one 32-deep v_mfma_f32_16x16x32_bf16 substep per stage ----
+    bf16x8 xa1[8], xb0[4];
     // Ping-pong: waves 0-3 and 4-7 (one of each per SIMD) run one barrier interval apart,
     // so in every interval one wave per SIMD issues its 32-MFMA cluster while its partner
     // works through its memory section:
@@ -541,8 +437,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // the barrier before its first read (group 0's M(s+1)).  WAR: the DMA into stage s-1's
     // slot is issued in M(s), after the barrier that follows group 1's last read of it
     // (its M(s-1) ends with lgkmcnt(0)).
-    (void)xa0;
-    (void)xb1;
     const int grp = wave >> 2;
     auto sbar = [&]() {
       __builtin_amdgcn_sched_barrier(0);
@@ -596,65 +490,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       FG_ST(4);
     }
 #undef FG_ST
-#else
-    load16(xa0, xb0, smem + (gs & (FNBUF - 1)) * FSTAGE);
-    for (int t = 0; t < nk; t += 2) {
-      step16(xa0, xb0, xa1, xb1);
-      step16(xa1, xb1, xa0, xb0);
-    }
-#endif
-#else
-#pragma unroll
-    for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 qv4 = uni ? *reinterpret_cast<const float4*>(s_qv + wq * 128 + ib * 32 + 8 * g + 4 * h)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          acc[ib][jb][4 * g + 0] = R0[jb] - qv4.x;
-          acc[ib][jb][4 * g + 1] = R0[jb] - qv4.y;
-          acc[ib][jb][4 * g + 2] = R0[jb] - qv4.z;
-          acc[ib][jb][4 * g + 3] = R0[jb] - qv4.w;
-        }
-      }
-    // ---- K loop ----
-    bf16x8 fa0[4], fb0[2], fa1[4], fb1[2];
-    auto load_frags = [&](bf16x8* fa, bf16x8* fb, const char* sb, int kk) {
-      const char* sA = sb + wq * 128 * 64;
-      const char* sB = sb + FT * 64 + wr * 64 * 64;
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib) fa[ib] = *reinterpret_cast<const bf16x8*>(sA + ib * 2048 + foff[kk]);
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) fb[jb] = *reinterpret_cast<const bf16x8*>(sB + jb * 2048 + foff[kk]);
-    };
-    auto mfma8 = [&](const bf16x8* fa, const bf16x8* fb) {
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-          acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ib], fb[jb], acc[ib][jb], 0, 0, 0);
-    };
-    load_frags(fa0, fb0, smem + (gs & (FNBUF - 1)) * FSTAGE, 0);
-    for (int t = 0; t < nk; ++t) {
-      issue_next();
-      load_frags(fa1, fb1, smem + (gs & (FNBUF - 1)) * FSTAGE, 1);
-      mfma8(fa0, fb0);
-      ++gs;
-      const int n_out = issued - gs - 1;
-      if (n_out >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (n_out == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      load_frags(fa0, fb0, smem + (gs & (FNBUF - 1)) * FSTAGE, 0);
-      mfma8(fa1, fb1);
-    }
-#endif
     // ---- epilogue ----
     // The stage buffer just consumed is free until the next tile's first K step
     // re-issues it: 4 KiB per wave of it hold one 32x32 block for the scalar paths.
     float* wsc = reinterpret_cast<float*>(smem + ((gs - 1) & (FNBUF - 1)) * FSTAGE) + wave * 1024;
-#if FG_M16
     // blocks: jb (16 rows) x half (query blocks 0-3 / 4-7): 16 values per lane
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
@@ -749,52 +588,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
           const float d0 = wsc[e * 64 + lane];
           const int ql = wq * 128 + (hf * 4 + (e >> 2)) * 16 + 4 * c16 + (e & 3);
           const int q = q0 + ql;
-#else
-    bool anyb[4][2];
-    if (a.dbg & 2) goto flush;
-    if (MODE == 0 && uni) {
-      bool any = false;
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          float m = __builtin_fmaxf(acc[ib][jb][0], acc[ib][jb][1]);
-#pragma unroll
-          for (int e = 2; e < 16; e += 2) m = __builtin_fmaxf(m, __builtin_fmaxf(acc[ib][jb][e], acc[ib][jb][e + 1]));
-          anyb[ib][jb] = __ballot(m >= 0.f) != 0;
-          any = any || anyb[ib][jb];
-        }
-      if (!any) goto flush;
-    } else {
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) anyb[ib][jb] = true;
-    }
-    {
-      RowF rf[2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int r = r0 + wr * 64 + jb * 32 + l31;
-        const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
-        rf[jb] = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-      }
-#pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          if (!anyb[ib][jb]) continue;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) wsc[e * 64 + lane] = acc[ib][jb][e];
-          const int r = r0 + wr * 64 + jb * 32 + l31;
-          const RowF f = rf[jb];
-          const bool usable = f.par >= -1;
-#pragma unroll 1
-          for (int e = 0; e < 16; ++e) {
-            const float d0 = wsc[e * 64 + lane];
-            const int ql = wq * 128 + ib * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            const int q = q0 + ql;
-#endif
             if (MODE == 1) {
               float lo = -CWQ_INF;
               if (usable) {
@@ -892,12 +685,12 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   if (MODE == 0 && tid == 0 && s_cnt[1] >= 0) a.chunk_fill[s_cnt[1]] = s_cnt[2];
 }
 
-// Padded bf16 operand width: whole stages, an even number of them for the 16x16x32
-// loop (unrolled by two), at least the ring's prefetch depth.
+// Padded bf16 operand width: whole stages (an even number of them), at least the ring's
+// prefetch depth.
 int fgemm_dpb(int D) {
-  const int g = FG_M16 ? 2 * FK : FK;
+  const int g = 2 * FK;
   const int r = (D + g - 1) / g * g;
-  const int lo = FG_M16 ? 4 * FK : 3 * FK;
+  const int lo = 4 * FK;
   return r > lo ? r : lo;
 }
 

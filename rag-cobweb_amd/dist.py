@@ -21,33 +21,86 @@ def world():
     return 0, 1
 
 
-def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None):
+def _default_device():
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None, stats=None):
     """Broadcast a BFS-flattened tree from `src`.  Non-src ranks pass None for the
     arrays; every rank returns (mean, var, parent, node_of_sentence) with mean/var
-    on `device` (the RCCL buffers) and the small structure arrays as numpy."""
+    on `device` (the RCCL buffers) and the small structure arrays as numpy.
+
+    `var` travels compressed: a row whose D values are one value repeated (every
+    count-1 leaf: var = prior_var exactly, CobwebTorchTree.py:336-342) is sent as that
+    scalar, and only the other rows are sent in full.  The receivers rebuild var
+    bit for bit.  For a flat-synth tree that is N+1 scalars + one row instead of
+    (N+1) x D floats (3.07 GB at C3).  `stats` (dict) receives the bytes sent."""
     rank, ws = world()
-    dev = torch.device(device) if device is not None else (
-        torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu"))
-    if rank == src:
-        meta = torch.tensor([mean.shape[0], mean.shape[1], len(node_of_sentence)], dtype=torch.int64)
-    else:
-        meta = torch.zeros(3, dtype=torch.int64)
-    meta = meta.to(dev)
-    dist.broadcast(meta, src)
-    n_nodes, dim, n_sent = (int(v) for v in meta.tolist())
+    dev = torch.device(device) if device is not None else _default_device()
     if rank == src:
         mean = torch.as_tensor(mean, dtype=torch.float32).to(dev).contiguous()
         var = torch.as_tensor(var, dtype=torch.float32).to(dev).contiguous()
+        bits = var.view(torch.int32)
+        iso = (bits == bits[:, :1]).all(1)
+        an_idx = torch.nonzero(~iso).squeeze(1).to(torch.int64)
+        meta = torch.tensor([mean.shape[0], mean.shape[1], len(node_of_sentence), an_idx.numel()], dtype=torch.int64)
+    else:
+        meta = torch.zeros(4, dtype=torch.int64)
+    meta = meta.to(dev)
+    dist.broadcast(meta, src)
+    n_nodes, dim, n_sent, n_an = (int(v) for v in meta.tolist())
+    if rank == src:
+        v0 = var[:, 0].contiguous()
+        an_rows = var[an_idx].contiguous()
         par = torch.as_tensor(np.asarray(parent, np.int64)).to(dev)
         nos = torch.as_tensor(np.asarray(node_of_sentence, np.int64)).to(dev)
     else:
         mean = torch.empty((n_nodes, dim), dtype=torch.float32, device=dev)
-        var = torch.empty((n_nodes, dim), dtype=torch.float32, device=dev)
+        v0 = torch.empty(n_nodes, dtype=torch.float32, device=dev)
+        an_idx = torch.empty(n_an, dtype=torch.int64, device=dev)
+        an_rows = torch.empty((n_an, dim), dtype=torch.float32, device=dev)
         par = torch.empty(n_nodes, dtype=torch.int64, device=dev)
         nos = torch.empty(n_sent, dtype=torch.int64, device=dev)
-    for t in (mean, var, par, nos):
-        dist.broadcast(t, src)
+    sent = 0
+    for t in (mean, v0, an_idx, an_rows, par, nos):
+        if t.numel():
+            dist.broadcast(t, src)
+            sent += t.numel() * t.element_size()
+    if rank != src:
+        var = v0[:, None].expand(n_nodes, dim).contiguous()
+        if n_an:
+            var[an_idx] = an_rows
+    if stats is not None:
+        stats["bytes"] = sent
+        stats["var_rows_sent"] = n_an
     return mean, var, par.cpu().numpy(), nos.cpu().numpy()
+
+
+def timed_steps(step, steps, warmup, sync=None):
+    """The bench's timed region: `warmup` untimed calls of step(), then exactly `steps`
+    calls bracketed by a barrier + device sync on both sides; returns the MAX over ranks
+    of the elapsed seconds (every rank gets the same value)."""
+    import time
+    rank, ws = world()
+    sync = sync or (lambda: None)
+    for _ in range(warmup):
+        step()
+    sync()
+    if ws > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if ws > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=_default_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
 
 
 def shard_bounds(n, rank, ws):
@@ -57,14 +110,15 @@ def shard_bounds(n, rank, ws):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def sharded_query(fn, queries, k):
+def sharded_query(fn, queries, k, gather=True):
     """Run `fn(local_queries, k) -> (ids [q,k] int64, scores [q,k] f32)` on this
-    rank's slice and all-gather the results in global query order."""
+    rank's slice and (gather=True) all-gather the results in global query order;
+    gather=False returns this rank's slice only (the serving loop, no collective)."""
     rank, ws = world()
     n = queries.shape[0]
     lo, hi = shard_bounds(n, rank, ws)
     ids, scores = fn(queries[lo:hi], k)
-    if ws == 1:
+    if ws == 1 or not gather:
         return ids, scores
     sizes = [shard_bounds(n, r, ws) for r in range(ws)]
     mx = max(h - l for l, h in sizes)

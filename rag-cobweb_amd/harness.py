@@ -43,8 +43,14 @@ def retrieval_metrics(retrieved, targets, top_k, lengths=None):
     if lengths is None:
         lengths = (retrieved >= 0).sum(1)
     lengths = torch.as_tensor(lengths, device=retrieved.device)
+    # The reference's loop aborts a query whose result list holds ONE entry that is the
+    # target: ndcg_score raises on a single document ("only meaningful when there is
+    # more than 1 document"), the exception ends the k loop after recall/mrr of the
+    # first k were added (benchmark_utils.py:807-820), so that query counts for
+    # recall@k0 and mrr@k0 only and for no ndcg.
+    single_hit = (lengths == 1) & (retrieved[:, 0] == targets)
     out = {}
-    for k in get_eval_ks(top_k):
+    for ki, k in enumerate(get_eval_ks(top_k)):
         top = retrieved[:, :k]
         n = torch.clamp(lengths, max=k)                                    # len(top_k_results)
         pos = torch.arange(k, device=top.device)[None, :]
@@ -66,6 +72,10 @@ def retrieval_metrics(retrieved, targets, top_k, lengths=None):
         dcg = torch.where(m > 0, a / m.clamp(min=1) * s_head, torch.zeros_like(m)) + \
             torch.where(nm > 0, (m - a) / nm.clamp(min=1) * s_tail, torch.zeros_like(m))
         ndcg = torch.where(m > 0, dcg / s_head.clamp(min=1e-300), torch.zeros_like(m))
+        ndcg = torch.where(single_hit, torch.zeros_like(ndcg), ndcg)
+        if ki > 0:
+            recall = torch.where(single_hit, torch.zeros_like(recall), recall)
+            mrr = torch.where(single_hit, torch.zeros_like(mrr), mrr)
         out[f"recall@{k}"] = round(float(recall.mean()), 4)
         out[f"mrr@{k}"] = round(float(mrr.mean()), 4)
         out[f"ndcg@{k}"] = round(float(ndcg.mean()), 4)

@@ -55,8 +55,9 @@ def flat_synth(X):
     parent = torch.zeros(N + 1, dtype=torch.int64)
     parent[0] = -1
     nos = torch.arange(1, N + 1, dtype=torch.int64)
+    count = torch.cat([cnt, torch.ones(N, device=X.device)])
     return dict(mean=mean, var=var, parent=parent.numpy(), node_of_sentence=nos.numpy(),
-                root=(cnt, mu, m2))
+                root=(cnt, mu, m2), count=count, meanSq_root=m2)
 
 
 def two_level_synth(X, labels):
@@ -79,5 +80,7 @@ def two_level_synth(X, labels):
                         1 + torch.repeat_interleave(torch.arange(G), counts.cpu())])
     node_of_sentence = torch.empty(N, dtype=torch.int64)
     node_of_sentence[order.cpu()] = torch.arange(1 + G, 1 + G + N)
+    count = torch.cat([r_cnt, c_cnt, torch.ones(N, device=dev)])
+    meanSq = torch.cat([r_m2, c_m2, torch.zeros((N, D), device=dev)])   # leaves: count 1, meanSq 0
     return dict(mean=mean, var=var, parent=parent.numpy(), node_of_sentence=node_of_sentence.numpy(),
-                n_clusters=G)
+                n_clusters=G, count=count, meanSq=meanSq)

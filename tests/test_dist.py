@@ -90,3 +90,72 @@ def test_gloo_world2_broadcast_and_gather(tmp_path, q):
     np.testing.assert_array_equal(r["ids"], g["fast_ids"][:q])   # gathered in global order
     np.testing.assert_allclose(r["scores"], np.take_along_axis(g["rank_scores"][:q], g["fast_ids"][:q], 1),
                                rtol=1e-5)
+
+
+def _bench_path_worker(rank, ws, port, result_path, strong):
+    """The functions bench.py calls on every rank, in bench.py's order: broadcast_tree
+    (compressed var), timed_steps (barrier + max over ranks) around sharded_query /
+    a per-rank batch, on gloo with the CPU oracle as the per-rank scorer."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import cobweb_pkg
+        from oracle import cobweb_oracle as O
+        D = cobweb_pkg.load().dist
+        rng = np.random.default_rng(5)
+        X = rng.standard_normal((300, 24)).astype(np.float32)
+        ref = O.flat_synth_index(X)
+        if rank == 0:
+            var = ref.vars.copy()
+            var[7, 3] *= np.float32(1.5)          # one anisotropic row: sent in full
+            args = (ref.means, var, ref.parent, np.arange(1, 301))
+        else:
+            args = (None, None, None, None)
+        st = {}
+        mean, var, parent, nos = D.broadcast_tree(*args, device="cpu", stats=st)
+        idx = O.FlatIndex(mean.numpy(), var.numpy(), parent, [[0, int(s)] for s in nos])
+
+        def scorer(qs, k):
+            out = [O.topk_ids_scores(O.rank_scores(x, idx), k) for x in qs.numpy()]
+            return (torch.tensor(np.array([o[0] for o in out]), dtype=torch.int64),
+                    torch.tensor(np.array([o[1] for o in out])))
+
+        Q = torch.from_numpy(np.concatenate([X[:6] + 0.05, rng.standard_normal((5, 24)).astype(np.float32)]))
+        calls = []
+        if strong:
+            step = lambda: calls.append(D.sharded_query(scorer, Q, 5, gather=False))   # noqa: E731
+        else:
+            step = lambda: calls.append(scorer(Q, 5))                                   # noqa: E731
+        dt = D.timed_steps(step, 2, 1)
+        lo, hi = D.shard_bounds(Q.shape[0], rank, ws) if strong else (0, Q.shape[0])
+        gathered = D.sharded_query(scorer, Q, 5)          # the all-gathered form, for the check
+        np.savez(result_path + f".{rank}.npz", var=var.numpy(), ids=calls[-1][0].numpy(), lo=lo, hi=hi, dt=dt,
+                 n_calls=len(calls), bytes=st["bytes"], an=st["var_rows_sent"], gathered=gathered[0].numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("strong", [False, True])
+def test_gloo_world2_bench_path(tmp_path, strong):
+    from oracle import cobweb_oracle as O
+    out = str(tmp_path / "bench")
+    mp.spawn(_bench_path_worker, args=(2, _free_port(), out, strong), nprocs=2, join=True)
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((300, 24)).astype(np.float32)
+    ref = O.flat_synth_index(X)
+    var = ref.vars.copy()
+    var[7, 3] *= np.float32(1.5)
+    Q = np.concatenate([X[:6] + 0.05, rng.standard_normal((5, 24)).astype(np.float32)])
+    want = np.array([O.topk_ids_scores(O.rank_scores(x, O.FlatIndex(ref.means, var, ref.parent,
+                                                                   [[0, 1 + i] for i in range(300)])), 5)[0]
+                     for x in Q])
+    r = [np.load(out + f".{i}.npz") for i in range(2)]
+    for ri in r:
+        np.testing.assert_array_equal(ri["var"], var)            # compressed var rebuilt bit for bit
+        assert int(ri["an"]) == 2                                  # only the root and the anisotropic leaf in full
+        assert int(ri["n_calls"]) == 3                             # warmup 1 + steps 2
+        np.testing.assert_array_equal(ri["gathered"], want)
+        np.testing.assert_array_equal(ri["ids"], want[int(ri["lo"]):int(ri["hi"])])
+    assert float(r[0]["dt"]) == float(r[1]["dt"])                  # max over ranks on both
+    if strong:
+        assert [int(r[0]["lo"]), int(r[0]["hi"]), int(r[1]["lo"]), int(r[1]["hi"])] == [0, 6, 6, 11]

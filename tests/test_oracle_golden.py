@@ -152,3 +152,20 @@ def test_tree_json_is_reference_format():
     g = load_golden("g1_hier_d32")
     assert d["root"]["count"] == float(g["count"][0])
     np.testing.assert_array_equal(np.float32(d["root"]["mean"]), g["mean"][0])
+
+
+@pytest.mark.parametrize("name", HIER + ["g3_flat_inject_d32"])
+def test_torch_fast_restatement(name):
+    """The torch-CPU op sequence bench.py times as the CPU baseline (TorchFastIndex,
+    CobwebWrapper.py:222-257) returns the reference's Fast top-k on the goldens."""
+    g = load_golden(name)
+    if "parent" in g:
+        idx = O.flatten_tree(tree_of(g), int(g["n_sent"]))
+        T = O.TorchFastIndex(idx.means, idx.vars, idx.paths, idx.weights)
+    else:   # injected flat index: root stats + one leaf per row
+        root_var = O.compute_var(g["root_meanSq"], g["root_count"])
+        T = O.TorchFastIndex.flat(g["root_mean"], root_var, g["X"])
+    k = int(g["k"])
+    for qi, x in enumerate(g["Xq"]):
+        got = T.predict(x, k)
+        assert_topk_equiv(got, g["fast_ids"][qi], g["rank_scores"][qi])
