@@ -35,16 +35,10 @@ def test_gpu_ifit_reproduces_reference_tree(pkg, name):
     np.testing.assert_array_equal(parent, g["parent"])
     np.testing.assert_array_equal([s for n in nodes for s in n.sentence_id], g["sid_list"])
     np.testing.assert_array_equal(np.array([n.count for n in nodes], np.float32), g["count"])
-    np.testing.assert_allclose(np.stack([n.mean for n in nodes]), g["mean"], rtol=1e-5, atol=1e-6)
-    # meanSq (Welford M2) relative to each node's largest entry: M2 entries near zero carry
-    # the rounding of the entries they were merged from, so an elementwise relative bound
-    # is not meaningful for them (the reference's own fp32 has the same absolute error)
-    m2 = np.stack([n.meanSq for n in nodes]).astype(np.float64)
-    ref = g["meanSq"].astype(np.float64)
-    row = np.maximum(np.abs(ref).max(1, keepdims=True), 1e-30)
-    err = float(np.max(np.abs(m2 - ref) / row))
-    print(f"{name}: meanSq max row-relative error {err:.3e}, exact entries {np.mean(m2 == ref):.4f}")
-    assert err < 1e-5
+    # the fit kernels use the reference's fp32 op order with contraction off: the node
+    # statistics come out bit-identical (measured on MI355X: every mean/meanSq entry)
+    np.testing.assert_array_equal(np.stack([n.mean for n in nodes]), g["mean"])
+    np.testing.assert_array_equal(np.stack([n.meanSq for n in nodes]), g["meanSq"])
     # the drop-in answers like the reference
     k = int(g["k"])
     for qi in range(6):
