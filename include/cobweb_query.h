@@ -155,9 +155,12 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  *            candidate filter + exact rerank when k <= 64 and the index holds
  *            >= 16384 isotropic rows, the exact fp32 scan otherwise
  *   mode  0: always the exact fp32 scan      mode 1: the filter whenever k <= 64
+ * Calls with nq <= 64 take the small-batch stream filter instead of the batch MFMA
+ * filter (one HBM pass over the bf16 row panel; env CWQ_STREAM=0 disables it).
  * cwq_last_stats(out6): [queries served by the filter, of which re-run by the exact
- * scan (candidate list overflow / no threshold), filter used (0/1), mean candidate
- * records per query, mean exact reranks per query, threshold-sample rows].
+ * scan (candidate list overflow / no threshold), filter used (0 exact scan, 1 batch
+ * MFMA filter, 2 small-batch stream filter), mean candidate records per query, mean
+ * exact reranks per query, threshold-sample rows].
  */
 int cwq_set_filter(cwq_index* idx, int mode);
 int cwq_last_stats(cwq_index* idx, int64_t* out6);

@@ -854,10 +854,161 @@ int rerun_exact(cwq_index* ix, const float* q, const std::vector<int64_t>& qi, i
   return CWQ_OK;
 }
 
+// Small-batch path (cwq_stream.hip): nq <= kStreamMaxQ queries, isotropic rows through
+// the stream filter (probe -> filter -> exact rerank), anisotropic rows through the exact
+// scan; the reference harness's one-query-per-call mode.  false: not applicable.
+bool use_stream(const cwq_index* ix, int64_t nq, int k) {
+  if (nq > kStreamMaxQ || k > kFiltMaxK || !ix->iso_Mb) return false;
+  if (stream_lds_bytes((int)((nq + 15) / 16), ix->DPB) > (size_t)kStreamMaxLds) return false;
+  const char* e = getenv("CWQ_STREAM");
+  return !(e && *e && atoi(e) == 0);
+}
+
+int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                     hipStream_t s) {
+  const int K = k, kl = k <= 16 ? 16 : 64;
+  const int nqc = (int)nq;
+  const int nqb = (nqc + 15) / 16, nq16 = nqb * 16;
+  const int64_t nq_pad = round_up(nqc, kQPad);
+  const int nqb_scan = n_qblocks_for(nqc, kl);
+  const int slabs = 1 + (pick_nslab(ix, ix->NL_an, nqb_scan) + 1) * scan_lists_per_slab(kl);
+  const int capq = kFgCapQ;
+  size_t need = chunk_bytes(ix, nq_pad) + 64 * 256 + (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) +
+                (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)64 * nqc * 4 + (size_t)nqc * 4 +
+                (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
+                (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256;
+  int rc;
+  if ((rc = ix->reserve(need))) return rc;
+  Bump b(ix->ws, ix->ws_size);
+  Chunk c;
+  carve_chunk(ix, b, c, nqc);
+  float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
+  float* paux = b.take<float>((size_t)nq_pad * slabs * K);
+  int* prow = b.take<int>((size_t)nq_pad * slabs * K);
+  float* okey = b.take<float>((size_t)nq_pad * K);
+  float* oaux = b.take<float>((size_t)nq_pad * K);
+  int* orow = b.take<int>((size_t)nq_pad * K);
+  uint16_t* Xb = b.take<uint16_t>((size_t)nq16 * ix->DPB);
+  float4* qinfo = b.take<float4>(nq16);
+  int* Tb = b.take<int>((size_t)(K + 1) * nqc);   // [K][nq] blocks + [nq] live threshold
+  float* T = b.take<float>(nqc);
+  int* qcnt = b.take<int>((size_t)5 * nqc);   // [qcnt | ok | n_exact | qover | done]
+  int* okf = qcnt + nqc;
+  int* nex = qcnt + 2 * nqc;
+  int* qover = qcnt + 3 * nqc;
+  int* done = qcnt + 4 * nqc;
+  int* crow = b.take<int>((size_t)nqc * capq);
+  float* cu = b.take<float>((size_t)nqc * capq);
+  float* cl = b.take<float>((size_t)nqc * capq);
+  float* lkb = b.take<float>((size_t)nqc * 64);
+  int* lrb = b.take<int>((size_t)nqc * 64);
+  const int64_t ldlb = round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024;   // select reads whole 1024 steps
+  float* lb = b.take<float>((size_t)nqc * ldlb);
+  float* tl = b.take<float>((size_t)nqc * 64);
+  int* tr = b.take<int>((size_t)nqc * 64);
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
+  HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+  if ((rc = run_internal(ix, c, s, false))) return rc;
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
+  HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
+  HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
+  HIPCHK(launch_stream_init(Tb, (K + 1) * nqc, s));
+  const FiltConsts fc = filt_consts(ix->DPB);
+  StreamArgs a;
+  memset(&a, 0, sizeof(a));
+  a.DPB = ix->DPB;
+  a.nq = nqc;
+  a.nqb = nqb;
+  a.nrows = ix->NL_iso;
+  a.K = K;
+  a.Xb = Xb;
+  a.qinfo = qinfo;
+  a.Mb = ix->iso_Mb;
+  a.rf = ix->iso_rf;
+  a.P = c.P ? c.P : ix->dummy;
+  a.ldP = std::max(ix->NI, 1);
+  a.eps_n = (float)fc.eps_n;
+  a.slack = (float)fc.slack;
+  a.Tb = Tb;
+  a.Tlive = Tb + (size_t)K * nqc;
+  // live threshold (CWQ_STREAM_LIVE=n: refresh every n groups): measured slower at C3 --
+  // the publishing atomics cost more than the ~3x fewer candidates save -- so off
+  a.live_every = 0;
+  if (const char* e = getenv("CWQ_STREAM_LIVE")) a.live_every = std::max(0, atoi(e));
+  a.T = T;
+  a.qcnt = qcnt;
+  a.qover = qover;
+  a.capq = capq;
+  a.crow = crow;
+  a.cu = cu;
+  a.cl = cl;
+  // probe: ~3*K*rows/1024 rows (a 16-row group per probe_stride groups), so that the
+  // K-th largest probe bound leaves ~1k candidates per query before the live threshold
+  // takes over; CWQ_STREAM_PROBE_DIV overrides (groups / div)
+  const int64_t ngroups = (ix->NL_iso + 15) / 16;
+  int64_t n_probe = std::max<int64_t>((int64_t)3 * K * ngroups / 1024, (int64_t)8 * K);
+  if (const char* e = getenv("CWQ_STREAM_PROBE_DIV"))
+    if (atoi(e) > 0) n_probe = std::max<int64_t>(ngroups / atoi(e), (int64_t)K);
+  n_probe = std::min(n_probe, ngroups);
+  a.probe_stride = std::max<int64_t>(1, ngroups / std::max<int64_t>(n_probe, 1));
+  a.n_probe = std::min<int64_t>(n_probe, (ngroups + a.probe_stride - 1) / a.probe_stride);
+  a.lb = lb;
+  a.ldlb = ldlb;
+  a.T0 = tl;
+  a.ldT0 = 64;
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
+  HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
+  HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
+  HIPCHK(launch_stream(a, 0, ix->cus, s));
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
+  int nst = 0;
+  if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1))) return rc;
+  HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
+                      ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
+                      nex, lkb, lrb, done, s));
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
+  HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
+  HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids, scores, s));
+  if ((rc = ix->host_flags((size_t)3 * nqc))) return rc;
+  HIPCHK(hipMemcpyAsync(ix->hflags, qcnt, (size_t)3 * nqc * 4, hipMemcpyDeviceToHost, s));
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[3], s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<int64_t> redo;
+  int64_t cand_sum = 0, exact_sum = 0;
+  for (int i = 0; i < nqc; ++i) {
+    if (!ix->hflags[nqc + i]) redo.push_back(i);
+    cand_sum += ix->hflags[i];
+    exact_sum += ix->hflags[2 * nqc + i];
+  }
+  if (ix->timing) {
+    float e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(hipEventElapsedTime(&e[0], ix->ev[1], ix->ev[2]));
+    HIPCHK(hipEventElapsedTime(&e[1], ix->ev[0], ix->ev[1]));
+    HIPCHK(hipEventElapsedTime(&e[2], ix->ev[2], ix->ev[3]));
+    HIPCHK(hipEventElapsedTime(&e[3], ix->ev[0], ix->ev[3]));
+    HIPCHK(hipEventElapsedTime(&e[5], ix->ev[4], ix->ev[5]));
+    HIPCHK(hipEventElapsedTime(&e[6], ix->ev[5], ix->ev[6]));
+    HIPCHK(hipEventElapsedTime(&e[7], ix->ev[6], ix->ev[7]));
+    for (int i = 0; i < 8; ++i) ix->t_ms[i] += e[i];
+    ix->t_ms[4] += 1;   // one filter launch
+  }
+  if (!redo.empty() && (rc = rerun_exact(ix, q, redo, k, ids, scores, s))) return rc;
+  ix->stats[0] = nq;
+  ix->stats[1] = (int64_t)redo.size();
+  ix->stats[2] = 2;   // the stream filter
+  ix->stats[3] = (cand_sum + nq / 2) / nq;
+  ix->stats[4] = (exact_sum + nq / 2) / nq;
+  ix->stats[5] = a.n_probe * 16;
+  return CWQ_OK;
+}
+
 int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                     hipStream_t s, bool allow_filter) {
   const bool general = k > 64;
   const bool filt = !general && allow_filter && use_filter(ix, k);
+  if (filt && use_stream(ix, nq, k)) return stream_topk_impl(ix, q, nq, k, ids, scores, s);
   const int kl = k <= 16 ? 16 : 64;
   const int K = std::min<int>(k, 64);
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));

@@ -160,6 +160,21 @@ struct TileF {
 };
 constexpr int kFgMaxTileParents = 64;   // uniform 2 only up to this many parents per tile
 
+// Rigorous bounds l <= key_fp32 <= u of an isotropic row's Fast key from an approximate
+// bf16-MFMA dot product x_hi.mu_hi (error eextra on top of the bf16 split terms; see the
+// cwq_mfma.hip header).  Shared by the fgemm filter and the small-batch stream filter.
+__device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, const RowF& rf, float pi, float eps_n,
+                                          float slack, float& u, float& l) {
+  const float n2 = qi.x + rf.rn2;
+  const float S = fmaf(-2.f, dot, n2);
+  const float key = pi + fmaf(rf.hs, S, rf.hl);
+  const float ES = 2.f * fmaf(qi.y, rf.beta, fmaf(qi.z, rf.delta, eextra)) + eps_n * n2;
+  const float ahs = fabsf(rf.hs);
+  const float err = fmaf(ahs, ES, slack * (fabsf(pi) + fabsf(rf.hl) + 3.f * ahs * n2));
+  u = key + err;
+  l = key - err;
+}
+
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
   int rt_off;                             // first row tile of this launch (filter phases)
@@ -191,6 +206,41 @@ struct FgArgs {
   int* qover;                             // queries whose records were lost (re-run exactly)
   unsigned long long* stamp;              // FG_STAMP diagnostic builds only: s_memtime stamps
 };
+// Small-batch stream filter (cwq_stream.hip): nq <= kStreamMaxQ queries per launch
+constexpr int kStreamMaxQ = 64;
+constexpr int kStreamMaxLds = 160 * 1024;
+inline size_t stream_lds_bytes(int nqb, int DPB) { return (size_t)nqb * (DPB / 32) * 64 * 16; }
+struct StreamArgs {
+  int DPB, nq, nqb;            // queries, 16-query blocks (nqb * 16 >= nq)
+  int64_t nrows;               // isotropic filter rows
+  int K;                       // top-K width = threshold blocks
+  int64_t n_probe;             // probe: 16-row groups sampled
+  int64_t probe_stride;        // probe: group stride
+  float* lb;                   // probe: [nq][ldlb] per-group max lower bound
+  int64_t ldlb;
+  const float* T0;             // filter: initial threshold T0[q * ldT0 + K - 1] (select over lb)
+  int64_t ldT0;
+  const uint16_t* Xb;          // [>= nqb*16][DPB] bf16 hi of the centred queries
+  const float4* qinfo;         // [>= nqb*16]
+  const uint16_t* Mb;          // [ld_f][DPB] bf16 row panel
+  const RowF* rf;              // [ld_f]
+  const float* P;              // [nq][ldP] internal-node path prefixes
+  int64_t ldP;
+  float eps_n, slack;
+  int* Tb;                     // [K][nq] ordered-int block maxima of candidate lower bounds (filter)
+  int* Tlive;                  // [nq] ordered-int live threshold (= Tb + K * nq)
+  int live_every;              // filter: raise T to Tlive every this many groups (0: off)
+  float* T;                    // [nq] initial threshold (written by the filter launch, read by final_kernel)
+  int* qcnt;                   // [nq] candidates per query
+  int* qover;                  // [nq] list overflow
+  int capq;                    // candidate slots per query
+  int* crow;                   // [nq][capq]
+  float* cu;
+  float* cl;
+};
+hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s);   // mode 1 probe, 0 filter
+hipError_t launch_stream_init(int* Tb, int n, hipStream_t s);
+
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
                             int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,
                             hipStream_t s);

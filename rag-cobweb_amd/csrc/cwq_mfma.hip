@@ -170,19 +170,6 @@ constexpr int OFF_REC = OFF_PI + FT * 4;  // int4   [kFgCap] record staging
 constexpr int OFF_CNT = OFF_REC + kFgCap * 16;   // int[16]: count, chunk, fill, flush scratch, claim
 constexpr int FLDS = OFF_CNT + 64;
 
-// Rigorous bounds l <= key_fp32 <= u from an approximate dot product (error eextra on
-// top of the bf16 split terms).
-__device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, const RowF& rf, float pi, float eps_n,
-                                          float slack, float& u, float& l) {
-  const float n2 = qi.x + rf.rn2;
-  const float S = fmaf(-2.f, dot, n2);
-  const float key = pi + fmaf(rf.hs, S, rf.hl);
-  const float ES = 2.f * fmaf(qi.y, rf.beta, fmaf(qi.z, rf.delta, eextra)) + eps_n * n2;
-  const float ahs = fabsf(rf.hs);
-  const float err = fmaf(ahs, ES, slack * (fabsf(pi) + fabsf(rf.hl) + 3.f * ahs * n2));
-  u = key + err;
-  l = key - err;
-}
 
 // XCD-local tile i -> (query tile, row tile).  order 0/2: query tiles fastest (the
 // XCD's query panels stay in L2 while row panels stream past, each read by every

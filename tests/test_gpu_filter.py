@@ -225,3 +225,35 @@ def test_query_chunking(gpu, filt, monkeypatch):
     ix.set_filter(-1)
     assert torch.equal(ids0.cpu(), ids1.cpu())
     assert torch.equal(s0.cpu(), s1.cpu())
+
+
+@pytest.mark.parametrize("N,D,k,nq", [(60000, 768, 10, 1), (60000, 768, 10, 7), (60000, 768, 10, 64),
+                                      (40000, 96, 1, 16), (40000, 96, 64, 17), (30000, 1024, 10, 33),
+                                      (30000, 200, 5, 48), (20000, 256, 32, 64)])
+def test_stream_path_equals_exact_scan(gpu, N, D, k, nq):
+    """Small batches (nq <= 64) take the stream filter (cwq_stream.hip): bit-identical to
+    the exact scan, with and without the filter's threshold probe finding the targets."""
+    X = gpu.synth.synthetic_corpus(N, D, seed=N + D + k)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, nq, seed=nq)
+    ids0, s0, ids1, s1, st = both(ix, Q, k)
+    assert st["path"] == "stream" and st["filter_queries"] == nq, st
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    assert st["fallback_queries"] == 0, st
+
+
+def test_stream_path_two_level_tree(gpu):
+    """Stream filter on a hierarchical tree (per-row parent prefixes) and on a tree with
+    anisotropic leaves (exact scan for those rows, merged with the stream candidates)."""
+    N, D = 50000, 128
+    X = gpu.synth.synthetic_corpus(N, D, seed=77)
+    labels = torch.randint(0, 500, (N,), device="cuda:0", generator=torch.Generator(device="cuda:0").manual_seed(1))
+    ts = gpu.synth.two_level_synth(X, labels)
+    var = ts["var"].clone()
+    var[-100:, :7] *= 1.25          # 100 anisotropic leaves
+    ix = gpu.index.CobwebIndex(ts["mean"], var, ts["parent"], ts["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 40, seed=3)
+    for k in (1, 10, 40):
+        ids0, s0, ids1, s1, st = both(ix, Q, k)
+        assert st["path"] == "stream", st
+        assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
