@@ -132,9 +132,14 @@ PRESETS = {
 
 def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
     """The reference harness's mode: one cobweb_predict_fast-sized call at a time with a
-    host sync after each (benchmark_utils.py:801-805).  Median us per call and the HBM
-    rate of the leaf-row pass (bytes the pass streams / its HIP-event time)."""
-    out = {}
+    host sync after each (benchmark_utils.py:801-805).  Median us per call; for the
+    small-batch stream filter (cwq_stream.hip, nq <= 64) the HBM rate of its pass over
+    the row panel: bytes = isotropic rows x (2*DPB bf16 + 32 B row constants), divided by
+    the filter launch's HIP-event time, against the 8 TB/s HBM peak."""
+    NL, D = index.info["isotropic_rows"], index.dim
+    DPB = max(128, -(-D // 64) * 64)                     # fgemm_dpb: whole 64-dim stage pairs
+    bytes_pass = NL * (2.0 * DPB + 32.0)
+    out = {"bytes_per_pass": bytes_pass}
     for nq in nqs:
         q = Q[:nq].contiguous()
         index.score_topk(q, k)
@@ -148,14 +153,21 @@ def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
         ts.sort()
         index.set_timing(True)
         tm = []
-        for _ in range(3):
+        for _ in range(5):
             index.score_topk(q, k)
             tm.append(index.last_timing())
         index.set_timing(False)
         st = index.last_stats()
-        leaf_ms = float(np.median([t["leaf_scan_ms"] for t in tm]))
-        out[str(nq)] = {"us_per_call": round(ts[len(ts) // 2] * 1e6, 1), "queries_per_s": round(nq / ts[len(ts) // 2], 1),
-                        "leaf_pass_ms": round(leaf_ms, 4), "path": st.get("path", "filter" if st["filter_used"] else "scan")}
+        med = {key: float(np.median([t[key] for t in tm])) for key in tm[0]}
+        row = {"us_per_call": round(ts[len(ts) // 2] * 1e6, 1), "queries_per_s": round(nq / ts[len(ts) // 2], 1),
+               "path": st["path"], "call_ms_events": round(med["call_ms"], 4)}
+        if st["path"] == "stream":
+            gbs = bytes_pass / (med["fgemm_ms"] * 1e-3) / 1e9
+            row.update({"stream_filter_ms": round(med["fgemm_ms"], 4), "probe_ms": round(med["sample_ms"], 4),
+                        "rerank_ms": round(med["rerank_ms"], 4),
+                        "hbm_roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                                         "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)}})
+        out[str(nq)] = row
     return out
 
 
@@ -295,7 +307,6 @@ def main():
     pc = None
     if rank == 0 and not args.no_per_call:
         pc = per_call(index, Ql, k)
-        pc["bytes_per_pass"] = {"bf16_rows": 2.0 * NL * D, "fp32_rows": 4.0 * NL * D}
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

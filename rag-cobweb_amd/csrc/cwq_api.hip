@@ -107,6 +107,15 @@ struct cwq_index {
   std::vector<int> tile_uni_prefix;   // prefix counts of uniform row tiles (all_uniform per launch range)
   int n_multi_tiles = 0;              // tiles with several parents (TileF uniform 2)
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
+  // internal-node bounds (hierarchical trees, cwq_mfma.hip int_bounds): bf16 b' rows,
+  // their RowF constants, row-major fp32 A/B copies for the exact chain in final_kernel
+  bool int_bounds = false;
+  int DPB2 = 0;
+  int64_t ld_i2 = 0;
+  uint16_t* int_Mb2 = nullptr;
+  RowF* int_rf2 = nullptr;
+  float *int_Ar = nullptr, *int_Br = nullptr;
+  float root_w = 1.f, root_ld = 0.f;   // the root's level weight and logdet (host copies)
   int* samp_rows = nullptr;
   uint16_t* iso_Sb = nullptr;
   int64_t stats[6] = {0, 0, 0, 0, 0, 0};   // cwq_last_stats
@@ -558,6 +567,22 @@ extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const 
   if ((rc = ix->upload(&ix->sent_ids, sids, s))) return rc;
   if ((rc = ix->upload(&ix->row_of_sent, row_of_sent, s))) return rc;
   if ((rc = ix->upload(&ix->node_src, node_src, s))) return rc;
+  if (ix->NL_iso > 0 && ix->NI >= 2 && ix->max_depth <= kMaxChain) {
+    // internal-node bound operands: K = [x'^2, x'] -> DPB2 = fgemm width of 2*DP
+    ix->DPB2 = fgemm_dpb(2 * ix->DP);
+    ix->ld_i2 = round_up(ix->NI, kFgTile);
+    if ((rc = ix->alloc(&ix->int_Mb2, (size_t)ix->DPB2 * ix->ld_i2))) return rc;
+    if ((rc = ix->alloc(&ix->int_rf2, (size_t)ix->ld_i2))) return rc;
+    if ((rc = ix->alloc(&ix->int_Ar, (size_t)ix->NI * DP))) return rc;
+    if ((rc = ix->alloc(&ix->int_Br, (size_t)ix->NI * DP))) return rc;
+    const float gamma2 = (float)((ix->DPB2 + 64) * std::ldexp(1.0, -23));
+    ix->root_w = w_int[0];
+    HIPCHK(hipMemcpyAsync(&ix->root_ld, ix->logdet_int, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes, ix->NI, ix->iso_c, ix->logdet_int, ix->par_int, ix->w_int, DP,
+                           ix->DPB2, ix->ld_i2, ix->int_Mb2, ix->int_rf2, ix->int_Ar, ix->int_Br, gamma2, s));
+    ix->int_bounds = true;
+  }
   if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
   HIPCHK(hipStreamSynchronize(s));
   *out = ix.release();
@@ -675,6 +700,66 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true) {
   return CWQ_OK;
 }
 
+int fg_order();
+void fg_groups(int n_qt, int& qg, int& rg);
+
+// Filter paths on hierarchical trees: bounded internal prefixes instead of the exact
+// internal pass (CWQ_INT_BOUND=0 disables).  Anisotropic leaf rows need exact prefixes
+// (the exact scan reads them), so such trees keep the exact pass.
+bool use_int_bounds(const cwq_index* ix) {
+  if (!ix->int_bounds || ix->NL_an > 0) return false;
+  const char* e = getenv("CWQ_INT_BOUND");
+  return !(e && *e && atoi(e) == 0);
+}
+
+size_t int_bounds_bytes(const cwq_index* ix, int64_t nqf) {
+  return ix->int_bounds ? (size_t)nqf * ix->DPB2 * 2 + (size_t)nqf * 16 + (size_t)nqf * 4 + 3 * 256 : 0;
+}
+
+// Internal nodes by bounds: c.P <- lower, c.S_int <- upper bounds of the path prefix of
+// every internal node (the root exact in both).  q: the caller's [nq][D] queries.
+int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bump& b, hipStream_t s) {
+  uint16_t* Xb2 = b.take<uint16_t>((size_t)nqf * ix->DPB2);
+  float4* qinfo2 = b.take<float4>(nqf);
+  float* Sroot = b.take<float>(nqf);
+  int* tctr = b.take<int>(64);
+  HIPCHK(launch_query_prep2(q, c.nq, ix->D, ix->iso_c, ix->DP, ix->DPB2, nqf, Xb2, qinfo2, s));
+  HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, c.nq, Sroot, 1, s));   // root, exact
+  HIPCHK(hipMemsetAsync(tctr, 0, 64 * 4, s));
+  FgArgs g;
+  memset(&g, 0, sizeof(g));
+  g.DPB = ix->DPB2;
+  g.nq = c.nq;
+  g.n_qt = (int)(nqf / kFgTile);
+  fg_groups(g.n_qt, g.qgroups, g.rgroups);
+  g.qinfo = qinfo2;
+  g.order = fg_order();
+  g.tctr = tctr;
+  g.rf = ix->int_rf2;
+  g.tf = ix->iso_tf;
+  g.P = ix->dummy;
+  g.ldP = 1;
+  g.ldq = nqf;
+  g.mode = 2;
+  g.n_rt = (int)(ix->ld_i2 / kFgTile);
+  g.nrows = ix->NI;
+  g.lb = c.P;
+  g.lb_hi = c.S_int;
+  g.ldlb = std::max(ix->NI, 1);
+  g.Sroot = Sroot;
+  g.root_w = ix->root_w;
+  g.root_ld = ix->root_ld;
+  // one pass: the root row gets its exact prefix, rows whose parent is the root their
+  // prefix bounds (fused), deeper rows lp' bounds for the level passes below
+  HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+  for (size_t lv = 2; lv < ix->levels.size(); ++lv)
+    HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first, ix->levels[lv].second,
+                                ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
+  return CWQ_OK;
+}
+
+IntChain int_chain(const cwq_index* ix) { return IntChain{ix->int_Ar, ix->int_Br, ix->par_int, ix->w_int, ix->logdet_int}; }
+
 // One scan over both leaf-row segments.
 // seg_mask: bit 0 = isotropic segment, bit 1 = anisotropic; TOPK lists start at
 // slab_off0 (slots before it are filled by the caller).
@@ -736,11 +821,13 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
 }
 
 // Workspace for one chunk: X + internal arrays.
-size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad) {
-  return (size_t)nq_pad * ix->DP * 4 + 4 * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256;
+// Workspace of one chunk: X + the [nq][NI] internal arrays -- S_int and P always; BF and
+// LPF (path bottleneck, full log_prob) only for categorize / log_prob (`full`).
+size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad, bool full = true) {
+  return (size_t)nq_pad * ix->DP * 4 + (full ? 4 : 2) * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256;
 }
 
-void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
+void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
   c.nq = nq;
   c.nq_pad = round_up(nq, kQPad);
   c.X = b.take<float>((size_t)c.nq_pad * ix->DP);
@@ -748,23 +835,24 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq) {
     const size_t n = (size_t)c.nq_pad * ix->NI;
     c.S_int = b.take<float>(n);
     c.P = b.take<float>(n);
-    c.BF = b.take<float>(n);
-    c.LPF = b.take<float>(n);
+    if (full) {
+      c.BF = b.take<float>(n);
+      c.LPF = b.take<float>(n);
+    }
   }
 }
 
-// Query-chunk size that keeps the per-chunk workspace within the budget (8 GiB by
-// default, CWQ_WS_BUDGET_MB; at least 128 queries).
-int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra) {
-  const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
-  // workspace budget per chunk of queries (8 GiB; CWQ_WS_BUDGET_MB for tests of the chunking)
+// Query-chunk size that keeps the per-chunk workspace within the budget (16 GiB by
+// default -- 288 GB of HBM hold it beside the largest indexes; CWQ_WS_BUDGET_MB; at
+// least 128 queries).
+int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra, bool full = true) {
+  const size_t per_q = (size_t)ix->DP * 4 + (full ? 4 : 2) * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
   const char* e = getenv("CWQ_WS_BUDGET_MB");
-  const size_t budget = e && atoll(e) > 0 ? (size_t)atoll(e) << 20 : (size_t)8 << 30;
+  const size_t budget = e && atoll(e) > 0 ? (size_t)atoll(e) << 20 : (size_t)16 << 30;
   int64_t c = (int64_t)std::max<size_t>(kQPad, budget / std::max<size_t>(per_q, 1));
   c = std::max<int64_t>(kQPad, c / kQPad * kQPad);
   return std::min(nq, c);
 }
-
 }  // namespace
 
 namespace {
@@ -873,15 +961,16 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   const int nqb_scan = n_qblocks_for(nqc, kl);
   const int slabs = 1 + (pick_nslab(ix, ix->NL_an, nqb_scan) + 1) * scan_lists_per_slab(kl);
   const int capq = kFgCapQ;
-  size_t need = chunk_bytes(ix, nq_pad) + 64 * 256 + (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) +
+  size_t need = chunk_bytes(ix, nq_pad, false) + 64 * 256 + (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) +
                 (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)64 * nqc * 4 + (size_t)nqc * 4 +
                 (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
-                (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256;
+                (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256 +
+                int_bounds_bytes(ix, kFgTile);
   int rc;
   if ((rc = ix->reserve(need))) return rc;
   Bump b(ix->ws, ix->ws_size);
   Chunk c;
-  carve_chunk(ix, b, c, nqc);
+  carve_chunk(ix, b, c, nqc, false);
   float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
   float* paux = b.take<float>((size_t)nq_pad * slabs * K);
   int* prow = b.take<int>((size_t)nq_pad * slabs * K);
@@ -906,9 +995,14 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
+  const bool ib = use_int_bounds(ix);
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
   HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-  if ((rc = run_internal(ix, c, s, false))) return rc;
+  if (ib) {
+    if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
+  } else if ((rc = run_internal(ix, c, s, false))) {
+    return rc;
+  }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
   HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
   HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
@@ -926,6 +1020,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.Mb = ix->iso_Mb;
   a.rf = ix->iso_rf;
   a.P = c.P ? c.P : ix->dummy;
+  a.Phi = ib ? c.S_int : nullptr;
   a.ldP = std::max(ix->NI, 1);
   a.eps_n = (float)fc.eps_n;
   a.slack = (float)fc.slack;
@@ -964,9 +1059,10 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
   int nst = 0;
   if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1))) return rc;
+  const IntChain chain = int_chain(ix);
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
-                      nex, lkb, lrb, done, s));
+                      nex, lkb, lrb, done, ib ? &chain : nullptr, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
   HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
@@ -1027,7 +1123,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                              : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
-  int64_t cq = chunk_queries(ix, nq, extra);
+  int64_t cq = chunk_queries(ix, nq, extra, false);
   if (filt && cq < nq) cq = std::max<int64_t>(kFgTile, cq / kFgTile * kFgTile);   // whole query tiles
   int64_t n_fallback = 0, cand_sum = 0, exact_sum = 0;
   std::vector<int64_t> redo;
@@ -1038,16 +1134,22 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     const int nqb = n_qblocks_for(nqc, kl);
     const int slabs = n_slabs(nqb);
     const int64_t nqf = round_up(nqc, kFgTile);
-    size_t need = chunk_bytes(ix, nq_pad) + 64 * 256;
+    size_t need = chunk_bytes(ix, nq_pad, false) + 64 * 256;
     need += general ? (size_t)nq_pad * ((size_t)ix->NL * 4 + (size_t)n_pow2 * 8)
                     : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) + (size_t)nqf * filt_q + 4096 * 8;
+    const bool ib = filt && use_int_bounds(ix);
+    if (ib) need += int_bounds_bytes(ix, nqf);
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
-    carve_chunk(ix, b, c, nqc);
+    carve_chunk(ix, b, c, nqc, false);
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s, false))) return rc;
+    if (ib) {
+      if ((rc = run_internal_bounds(ix, c, q + q0 * ix->D, nqf, b, s))) return rc;
+    } else if ((rc = run_internal(ix, c, s, false))) {
+      return rc;
+    }
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
     if (!general) {
       float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
@@ -1092,7 +1194,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         float2* pmm = ix->n_multi_tiles ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
         HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
         if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
-          HIPCHK(launch_tile_prange(c.P, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf, s));
+          HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf,
+                                    s));
         FgArgs g;
         memset(&g, 0, sizeof(g));
         g.DPB = ix->DPB;
@@ -1108,6 +1211,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         g.pmm = pmm;
         g.ldq = nqf;
         g.P = c.P ? c.P : ix->dummy;
+        g.Phi = ib ? c.S_int : nullptr;
         g.ldP = std::max(ix->NI, 1);
         g.gamma = (float)fc.gamma;
         g.eps_n = (float)fc.eps_n;
@@ -1188,9 +1292,10 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         }
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;
+        const IntChain chain = int_chain(ix);
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
                             ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow,
-                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, s));
+                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, ib ? &chain : nullptr, s));
         qcnt_d = qcnt;
         nex_d = nex;
         if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
@@ -1315,15 +1420,15 @@ extern "C" int cwq_rank_scores(cwq_index* ix, const float* q, int64_t nq, float*
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
   if (wu.rc) return wu.rc;
-  const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
+  const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4, false);
   int rc;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
-    if ((rc = ix->reserve(chunk_bytes(ix, nq_pad) + (size_t)nq_pad * std::max(ix->NL, 1) * 4 + 8 * 256))) return rc;
+    if ((rc = ix->reserve(chunk_bytes(ix, nq_pad, false) + (size_t)nq_pad * std::max(ix->NL, 1) * 4 + 8 * 256))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
-    carve_chunk(ix, b, c, nqc);
+    carve_chunk(ix, b, c, nqc, false);
     float* rowkey = b.take<float>((size_t)nq_pad * std::max(ix->NL, 1));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if ((rc = run_internal(ix, c, s, false))) return rc;

@@ -163,20 +163,27 @@ constexpr int kFgMaxTileParents = 64;   // uniform 2 only up to this many parent
 // Rigorous bounds l <= key_fp32 <= u of an isotropic row's Fast key from an approximate
 // bf16-MFMA dot product x_hi.mu_hi (error eextra on top of the bf16 split terms; see the
 // cwq_mfma.hip header).  Shared by the fgemm filter and the small-batch stream filter.
-__device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, const RowF& rf, float pi, float eps_n,
-                                          float slack, float& u, float& l) {
+// pi_u / pi_l: upper / lower bound of the parent-prefix term P[parent]/L (equal when the
+// prefix is exact; internal-node bounds otherwise, cwq_mfma.hip int_bounds).
+__device__ __forceinline__ void fg_bounds2(float dot, float eextra, float4 qi, const RowF& rf, float pi_u, float pi_l,
+                                           float eps_n, float slack, float& u, float& l) {
   const float n2 = qi.x + rf.rn2;
   const float S = fmaf(-2.f, dot, n2);
-  const float key = pi + fmaf(rf.hs, S, rf.hl);
+  const float kr = fmaf(rf.hs, S, rf.hl);
   const float ES = 2.f * fmaf(qi.y, rf.beta, fmaf(qi.z, rf.delta, eextra)) + eps_n * n2;
   const float ahs = fabsf(rf.hs);
-  const float err = fmaf(ahs, ES, slack * (fabsf(pi) + fabsf(rf.hl) + 3.f * ahs * n2));
-  u = key + err;
-  l = key - err;
+  const float err = fmaf(ahs, ES, slack * (fmaxf(fabsf(pi_u), fabsf(pi_l)) + fabsf(rf.hl) + 3.f * ahs * n2));
+  u = (pi_u + kr) + err;
+  l = (pi_l + kr) - err;
+}
+__device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, const RowF& rf, float pi, float eps_n,
+                                          float slack, float& u, float& l) {
+  fg_bounds2(dot, eextra, qi, rf, pi, pi, eps_n, slack, u, l);
 }
 
 struct FgArgs {
-  int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds)
+  int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds),
+                                          // 2: internal-node lp' bounds (dense lo/hi)
   int rt_off;                             // first row tile of this launch (filter phases)
   int all_uniform;                        // every row tile of the launch is uniform (TileF)
   int qgroups, rgroups;                   // XCD split (qgroups * rgroups == 8)
@@ -191,10 +198,14 @@ struct FgArgs {
   const float2* pmm;                      // multi-parent tiles: {min, max} parent prefix x invL, [tile][ldq]
   int64_t ldq;
   const int* rowmap;                      // sample pass: operand row -> filter row (-1 pad)
-  const float* P;                         // [nq][ldP] path prefixes of internal nodes
+  const float* P;                         // [nq][ldP] path prefixes of internal nodes (lower bounds when Phi)
+  const float* Phi;                       // [nq][ldP] upper bounds of the prefixes (NULL: P is exact)
   int64_t ldP;
   float gamma, eps_n, slack;              // error-bound constants (cwq_mfma.hip header)
-  float* lb;                              // sample: [nq_pad][ldlb]
+  float* lb;                              // sample: [nq_pad][ldlb]; internal bounds (mode 2): lp' lower bounds
+  float* lb_hi;                           // internal bounds (mode 2): lp' upper bounds [nq][ldlb]
+  const float* Sroot;                     // mode 2: exact raw sum of the root per query
+  float root_w, root_ld;                  // mode 2: the root's level weight and logdet
   int64_t ldlb;
   int lbg;                                // sample: rows per lower-bound group (1 or 4)
   int4* rec;                              // filter: appended records {q, row, u, l}
@@ -224,7 +235,8 @@ struct StreamArgs {
   const float4* qinfo;         // [>= nqb*16]
   const uint16_t* Mb;          // [ld_f][DPB] bf16 row panel
   const RowF* rf;              // [ld_f]
-  const float* P;              // [nq][ldP] internal-node path prefixes
+  const float* P;              // [nq][ldP] internal-node path prefixes (lower bounds when Phi)
+  const float* Phi;            // [nq][ldP] upper bounds (NULL: P exact)
   int64_t ldP;
   float eps_n, slack;
   int* Tb;                     // [K][nq] ordered-int block maxima of candidate lower bounds (filter)
@@ -250,8 +262,34 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s);
 int fgemm_dpb(int D);   // padded bf16 operand width the fgemm build needs
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);
-hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* tf, int n_rt, float2* pmm, int64_t ldq,
-                              hipStream_t s);
+// Internal-node bound operands (hierarchical trees): for internal node i (ids [0, n)),
+// b' = [-w/2, mu'w] (w = A^2, A = 1/sqrtf(var), mu' = mean - c) as bf16 hi [ld][DPB2],
+// its RowF {R0 = M_n, beta, delta, rn2 = c_n, hs = wmax, hl = logdet, invL = level weight
+// w_int, par = parent internal id (-1 root, -2 padding)}, and row-major
+// fp32 copies Ar = A, Br = mean * A (bit-identical to the exact scan's int_A / int_B).
+hipError_t launch_int_prep(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n,
+                           const float* c, const float* logdet, const int* par_int, const float* w_int, int DP, int DPB2,
+                           int64_t ld, void* Mb2, RowF* rf, float* Ar, float* Br, float gamma, hipStream_t s);
+// Queries for the internal bounds: a = [x'^2, x'] bf16 hi [nq_pad][DPB2], qinfo =
+// {sum x^2 + sum x'^2, |a_hi|, |a_lo|, 0}.
+hipError_t launch_query_prep2(const float* q, int64_t nq, int D, const float* c, int DP, int DPB2, int64_t nq_pad,
+                              void* Xb2, float4* qinfo, hipStream_t s);
+// P bounds level by level: lp' bounds (Plo, Phi) -> prefix bounds in place; the root
+// level (i0 == 0, one node) from its exact raw sum Sroot[q].
+hipError_t launch_prefix_bounds(float* Plo, float* Phi, int64_t ldP, int nq, int i0, int i1, const int* par_int,
+                                const float* w_int, const float* logdet_int, const float* Sroot, hipStream_t s);
+// Exact internal-node chain for final_kernel (bounded prefixes): P of a parent recomputed
+// with the scan's arithmetic from the exact root prefix P[q][0].
+constexpr int kMaxChain = 64;   // deepest internal-node chain final_kernel recomputes (host checks max depth)
+struct IntChain {
+  const float* Ar;
+  const float* Br;
+  const int* par_int;
+  const float* w_int;
+  const float* logdet_int;
+};
+hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int nq, const TileF* tf, int n_rt,
+                              float2* pmm, int64_t ldq, hipStream_t s);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
 // lkb/lrb [nq][64] and done [nq] carry each query's top-K candidate lower bounds between
@@ -263,7 +301,7 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
-                        const float* lkb, const int* lrb, const int* done, hipStream_t s);
+                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, hipStream_t s);
 
 // PCA + ICA whitening (cwq_whiten.hip): C[m][n] = sum_k (A[m][k] - ctr[k]) B[n][k] (/ denom[n])
 hipError_t launch_gemm_nt_f32(const float* A, int64_t M, int K, const float* ctr, const float* B, int N,

@@ -156,6 +156,177 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
   return hipGetLastError();
 }
 
+// One prefix_level_kernel step on intervals: parent prefix in [pl, ph], lp' in [lo, hi]
+// -> [lo, hi] <- bounds of fmaf(w, lp', P_parent) as the exact pass computes it (fp64,
+// widened by 2^-22 of the magnitudes for the fp32 fmaf's rounding, rounded outward).
+__device__ __forceinline__ void prefix_step(float pl, float ph, float w, float& lo, float& hi) {
+  const double a = (double)w * (double)lo, b = (double)w * (double)hi;
+  const double wl = fmin(a, b), wh = fmax(a, b);
+  const double m = 0x1p-22 * (fmax(fabs((double)pl), fabs((double)ph)) + fmax(fabs(wl), fabs(wh)));
+  const double l = (double)pl + wl - m, h = (double)ph + wh + m;
+  float fl = (float)l, fh = (float)h;
+  if ((double)fl > l) fl = nextafterf(fl, -CWQ_INF);
+  if ((double)fh < h) fh = nextafterf(fh, CWQ_INF);
+  lo = fl;
+  hi = fh;
+}
+
+// Internal-node bound operands (launch_int_prep, cwq_internal.h).  One wave per node.
+__global__ void int_prep_kernel(const float* __restrict__ mean, const float* __restrict__ var, int D,
+                                const int64_t* __restrict__ nodes, int64_t n, const float* __restrict__ c,
+                                const float* __restrict__ logdet, const int* __restrict__ par_int,
+                                const float* __restrict__ w_int, int DP, int DPB2, int64_t ld, __bf16* Mb2, RowF* rf,
+                                float* Ar, float* Br, float gamma) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= ld) return;
+  double shi = 0.0, slo = 0.0, cn = 0.0, mn = 0.0;
+  float wmax = 0.f;
+  for (int k = lane; k < DPB2; k += kWave) {   // b' = [-w/2 (DP wide), mu' w (DP wide), 0 pad]
+    const int d = k < DP ? k : k - DP;
+    const bool ok = r < n && k < 2 * DP && d < D;
+    float v = 0.f;
+    if (ok) {
+      const int64_t o = nodes[r] * (int64_t)D + d;
+      const float A = 1.0f / sqrtf(var[o]);      // as gather_T_kernel (the exact scan's A)
+      const float w = A * A;
+      const float mu = mean[o];
+      const float mc = mu - c[d];
+      if (k < DP) {
+        v = -0.5f * w;
+        const double am = fabs((double)mu) + fabs((double)c[d]);
+        cn += (double)mc * (double)mc * (double)w;
+        mn += (double)w * am * am;
+        wmax = fmaxf(wmax, w);
+        Ar[r * DP + d] = A;
+        Br[r * DP + d] = mu * A;
+      } else {
+        v = mc * w;
+      }
+    } else if (r < n && k < DP) {
+      Ar[r * DP + k] = 0.f;   // padding dims, as int_A / int_B
+      Br[r * DP + k] = 0.f;
+    }
+    const __bf16 h = (__bf16)v;
+    const float hf = (float)h;
+    const float lo = v - hf;
+    Mb2[r * DPB2 + k] = h;
+    shi += (double)hf * (double)hf;
+    slo += (double)lo * (double)lo;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    shi += __shfl_xor(shi, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+    cn += __shfl_xor(cn, off, 64);
+    mn += __shfl_xor(mn, off, 64);
+    wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
+  }
+  if (lane == 0) {
+    RowF f;
+    if (r < n) {
+      const double bh = sqrt(shi) * (1.0 + 0x1p-20), bl = sqrt(slo) * (1.0 + 0x1p-20);
+      f.R0 = up(mn);
+      f.beta = up(bl + (double)gamma * bh);
+      f.delta = up(bh + bl);
+      f.rn2 = (float)cn;
+      f.hs = wmax;
+      f.hl = logdet[r];
+      f.invL = w_int[r];
+      f.par = par_int[r];
+    } else {
+      f = RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+    }
+    rf[r] = f;
+  }
+}
+
+hipError_t launch_int_prep(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n,
+                           const float* c, const float* logdet, const int* par_int, const float* w_int, int DP, int DPB2,
+                           int64_t ld, void* Mb2, RowF* rf, float* Ar, float* Br, float gamma, hipStream_t s) {
+  if (ld <= 0) return hipSuccess;
+  hipLaunchKernelGGL(int_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, var, D, nodes, n, c,
+                     logdet, par_int, w_int, DP, DPB2, ld, (__bf16*)Mb2, rf, Ar, Br, gamma);
+  return hipGetLastError();
+}
+
+// Queries for the internal bounds: a = [x'^2 (DP wide), x' (DP wide), 0 pad].
+__global__ void query_prep2_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c,
+                                   int DP, int DPB2, int64_t nq_pad, __bf16* Xb2, float4* qinfo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= nq_pad) return;
+  double shi = 0.0, slo = 0.0, sx = 0.0;
+  for (int k = lane; k < DPB2; k += kWave) {
+    const int d = k < DP ? k : k - DP;
+    float v = 0.f;
+    if (r < nq && k < 2 * DP && d < D) {
+      const float x = q[r * D + d];
+      const float xc = x - c[d];
+      v = k < DP ? xc * xc : xc;
+      if (k < DP) sx += (double)x * (double)x + (double)xc * (double)xc;
+    }
+    const __bf16 h = (__bf16)v;
+    const float hf = (float)h;
+    const float lo = v - hf;
+    Xb2[r * DPB2 + k] = h;
+    shi += (double)hf * (double)hf;
+    slo += (double)lo * (double)lo;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    shi += __shfl_xor(shi, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+    sx += __shfl_xor(sx, off, 64);
+  }
+  if (lane == 0) qinfo[r] = make_float4(up(sx), up(sqrt(shi)), up(sqrt(slo)), 0.f);
+}
+
+hipError_t launch_query_prep2(const float* q, int64_t nq, int D, const float* c, int DP, int DPB2, int64_t nq_pad,
+                              void* Xb2, float4* qinfo, hipStream_t s) {
+  hipLaunchKernelGGL(query_prep2_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DP, DPB2,
+                     nq_pad, (__bf16*)Xb2, qinfo);
+  return hipGetLastError();
+}
+
+// Prefix bounds of one tree level (prefix_level_kernel's recurrence P = fmaf(w, lp,
+// P[parent]) on intervals): lp' bounds in (Plo, Phi) become prefix bounds, in fp64 and
+// widened by 2^-22 of the magnitudes for the exact fp32 fmaf's rounding.  Root level:
+// exact, from Sroot (same arithmetic as prefix_level_kernel).
+__global__ void prefix_bounds_kernel(float* Plo, float* Phi, int64_t ldP, int nq, int i0, int i1,
+                                     const int* __restrict__ par_int, const float* __restrict__ w_int,
+                                     const float* __restrict__ logdet_int, const float* __restrict__ Sroot) {
+  const int n = i1 - i0;
+  const int64_t total = (int64_t)n * nq;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / n);
+    const int i = i0 + (int)(t % n);
+    const size_t o = (size_t)q * ldP + i;
+    const int p = par_int[i];
+    const float w = w_int[i];
+    if (p < 0) {   // the root: exact
+      const float lp = -0.5f * (logdet_int[i] + Sroot[q]);
+      const float P = w * lp;
+      Plo[o] = P;
+      Phi[o] = P;
+      continue;
+    }
+    const size_t op = (size_t)q * ldP + p;
+    float lo = Plo[o], hi = Phi[o];
+    prefix_step(Plo[op], Phi[op], w, lo, hi);
+    Plo[o] = lo;
+    Phi[o] = hi;
+  }
+}
+
+hipError_t launch_prefix_bounds(float* Plo, float* Phi, int64_t ldP, int nq, int i0, int i1, const int* par_int,
+                                const float* w_int, const float* logdet_int, const float* Sroot, hipStream_t s) {
+  const int64_t total = (int64_t)(i1 - i0) * nq;
+  if (total <= 0) return hipSuccess;
+  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(prefix_bounds_kernel, grid, dim3(256), 0, s, Plo, Phi, ldP, nq, i0, i1, par_int, w_int,
+                     logdet_int, Sroot);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // fgemm: bf16-MFMA bounds over (query tile x row tile), persistent
 // ---------------------------------------------------------------------------
@@ -165,11 +336,36 @@ constexpr int FNBUF = 4;          // LDS stage ring: 3 stages in flight while on
 constexpr int FSTAGE = 2 * FT * FK * 2;   // bytes of one stage (A + B images) = 32 KiB
 constexpr int OFF_QV = FNBUF * FSTAGE;    // float  [FT]   pretest query terms
 constexpr int OFF_QI = OFF_QV + FT * 4;   // float4 [FT]   {|x'|^2, a, c, T}
-constexpr int OFF_PI = OFF_QI + FT * 16;  // float  [FT]   pi of the tile's parent
-constexpr int OFF_REC = OFF_PI + FT * 4;  // int4   [kFgCap] record staging
+constexpr int OFF_PI = OFF_QI + FT * 16;  // float  [FT]   pi of the tile's parent (upper bound)
+constexpr int OFF_PL = OFF_PI + FT * 4;   // float  [FT]   its lower bound (= pi when exact)
+constexpr int OFF_REC = OFF_PL + FT * 4;  // int4   [kFgCap] record staging
 constexpr int OFF_CNT = OFF_REC + kFgCap * 16;   // int[16]: count, chunk, fill, flush scratch, claim
 constexpr int FLDS = OFF_CNT + 64;
 
+
+// Internal node i, query x (mode 2): lp'(i) = -0.5 (logdet_i + S), S = sum_d w_d (x_d - mu_d)^2
+// (w = A^2, A = 1/sqrtf(var): the exact scan's sum_d (x_d A_d - B_d)^2).  With x' = x - c,
+// mu' = mu - c, a = [x'^2, x'], b' = [-w/2, mu' w]:  S = c_n - 2 a.b',  c_n = sum w mu'^2.
+// The MFMA gives a_hi.b'_hi; as for the leaves (header), |a.b' - a_hi.b'_hi| <= |a_hi||b_lo|
+// + |a_lo||b_hi| + |a_lo||b_lo| + gamma |a_hi||b_hi| (+ 2^-23 |dot| for the last rounding).
+// The fp32 evaluation of the exact S (scan order, stored A/B = fl(1/sqrt v), fl(mu A), the
+// query/mean centring and the fp32 squares) differs from that real value by far less than
+// 2^-12 (wmax (sum x^2 + sum x'^2) + M_n), M_n = sum w (|mu| + |c|)^2, which is added as
+// slack; lp' then gets 2^-20 (|logdet| + S) for its own two roundings.  Returns bounds
+// lo <= lp'_fp32 <= hi.  RowF fields: beta = |b_lo| + gamma|b_hi|, delta = |b_hi| + |b_lo|,
+// rn2 = c_n, hs = wmax, hl = logdet, R0 = M_n.  qinfo: {sum x^2 + sum x'^2, |a_hi|, |a_lo|}.
+__device__ __forceinline__ void int_bounds(float dot, float4 qi, const RowF& f, float gamma, float& lo, float& hi) {
+  (void)gamma;   // inside f.beta
+  const float S0 = fmaf(-2.f, dot, f.rn2);
+  const float E = 2.f * (fmaf(qi.y, f.beta, qi.z * f.delta) + 0x1p-23f * fabsf(dot)) + 0x1p-20f * fabsf(f.rn2) +
+                  0x1p-12f * fmaf(f.hs, qi.x, f.R0);
+  const float Eu = E * (1.f + 0x1p-20f);   // the fp32 evaluation of E itself
+  const float Shi = (S0 + Eu) * (1.f + 0x1p-22f);
+  const float Slo = fmaxf(0.f, (S0 - Eu) * (1.f - 0x1p-22f));
+  const float m = 0x1p-20f * (fabsf(f.hl) + Shi);
+  hi = -0.5f * (f.hl + Slo) + m;
+  lo = -0.5f * (f.hl + Shi) - m;
+}
 
 // XCD-local tile i -> (query tile, row tile).  order 0/2: query tiles fastest (the
 // XCD's query panels stay in L2 while row panels stream past, each read by every
@@ -269,6 +465,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   float* s_qv = reinterpret_cast<float*>(smem + OFF_QV);
   float4* s_qi = reinterpret_cast<float4*>(smem + OFF_QI);
   float* s_pi = reinterpret_cast<float*>(smem + OFF_PI);
+  float* s_pl = reinterpret_cast<float*>(smem + OFF_PL);
+  const float* Pu = a.Phi ? a.Phi : a.P;   // upper bounds of the parent prefixes
   int4* s_rec = reinterpret_cast<int4*>(smem + OFF_REC);
   int* s_cnt = reinterpret_cast<int*>(smem + OFF_CNT);
   // per-lane source offsets of the two 16-row pieces a wave stages per operand
@@ -342,11 +540,14 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     }
     const int qs = q0 + tid;
     float4 qi = make_float4(0.f, 0.f, 0.f, 0.f);
-    float Tq = CWQ_INF, Pq = 0.f;
+    float Tq = CWQ_INF, Pq = 0.f, Pql = 0.f;
     if (tid < FT) {
       qi = a.qinfo[qs];
       if (qs < a.nq && MODE == 0) Tq = a.T[(size_t)qs * a.ldT];
-      if (uni && tf.par >= 0 && qs < a.nq) Pq = a.P[(size_t)qs * a.ldP + tf.par];
+      if (uni && tf.par >= 0 && qs < a.nq) {
+        Pq = Pu[(size_t)qs * a.ldP + tf.par];
+        Pql = a.P[(size_t)qs * a.ldP + tf.par];
+      }
     }
     float R0[4];
 #pragma unroll
@@ -388,6 +589,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         }
       }
       s_pi[tid] = pi;
+      s_pl[tid] = uni ? Pql * tf.invL : 0.f;
+      if (MODE == 2) s_pl[tid] = qs < a.nq ? a.root_w * (-0.5f * (a.root_ld + a.Sroot[qs])) : 0.f;   // exact root P
       s_qv[tid] = qv;
     }
     if (dyn && tid == 0) s_cnt[8] = claimv;   // the tile after this one
@@ -575,7 +778,19 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
           const float d0 = wsc[e * 64 + lane];
           const int ql = wq * 128 + (hf * 4 + (e >> 2)) * 16 + 4 * c16 + (e & 3);
           const int q = q0 + ql;
-            if (MODE == 1) {
+            if (MODE == 2) {
+              if (usable && q < a.nq && r < a.nrows) {
+                float lo, hi;
+                if (f.par < 0) {   // the root: its exact prefix
+                  lo = hi = s_pl[ql];
+                } else {
+                  int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
+                  if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
+                }
+                a.lb[(size_t)q * a.ldlb + r] = lo;
+                a.lb_hi[(size_t)q * a.ldlb + r] = hi;
+              }
+            } else if (MODE == 1) {
               float lo = -CWQ_INF;
               if (usable) {
                 const float4 qi = s_qi[ql];
@@ -586,19 +801,26 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               a.lb[(size_t)q * a.ldlb + r] = lo;
             } else if (usable && q < a.nq && (!uni || d0 >= 0.f)) {
               const float4 qi = s_qi[ql];
-              float d, ex, pi;
+              float d, ex, pi, pl;
               if (uni) {
                 const float init = f.R0 - s_qv[ql];
                 d = d0 - init;
                 ex = a.gamma * fabsf(init) + 0x1p-23f * (fabsf(d0) + fabsf(init));
-                pi = (!ALLUNI && multi) ? a.P[(size_t)q * a.ldP + f.par] * f.invL : s_pi[ql];
+                if (!ALLUNI && multi) {
+                  pi = Pu[(size_t)q * a.ldP + f.par] * f.invL;
+                  pl = a.P[(size_t)q * a.ldP + f.par] * f.invL;
+                } else {
+                  pi = s_pi[ql];
+                  pl = s_pl[ql];
+                }
               } else {
                 d = d0;
                 ex = 0x1p-23f * fabsf(d0);
-                pi = f.par >= 0 ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+                pi = f.par >= 0 ? Pu[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+                pl = f.par >= 0 ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
               }
               float u, lo;
-              fg_bounds(d, ex, qi, f, pi, a.eps_n, a.slack, u, lo);
+              fg_bounds2(d, ex, qi, f, pi, pl, a.eps_n, a.slack, u, lo);
               if (u >= qi.w) {
                 const int4 rv = make_int4(q, r, __float_as_int(u), __float_as_int(lo));
                 const int slot = atomicAdd(&s_cnt[FG_CSLOT], 1);
@@ -687,6 +909,9 @@ hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_w
   n_wg = std::max(8, n_wg / 8 * 8);
   if (a.mode == 1)
     hipLaunchKernelGGL((fgemm_kernel<1, false>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
+                       (const __bf16*)Mb, a);
+  else if (a.mode == 2)
+    hipLaunchKernelGGL((fgemm_kernel<2, false>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
                        (const __bf16*)Mb, a);
   else if (a.all_uniform)
     hipLaunchKernelGGL((fgemm_kernel<0, true>), dim3((unsigned)n_wg), dim3(512), 0, s, (const __bf16*)Xb,
@@ -821,35 +1046,39 @@ hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp,
 // Multi-parent row tiles: per (tile, query) the range of the parents' prefixes x invL, so
 // the fgemm tile setup bounds its pretest term with one load instead of walking the
 // tile's parents.  Thread = query; tiles along blockIdx.y.
-__global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restrict__ P, int64_t ldP, int nq,
-                                                          const TileF* __restrict__ tf, int t0,
+__global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restrict__ P, const float* __restrict__ Phi,
+                                                          int64_t ldP, int nq, const TileF* __restrict__ tf, int t0,
                                                           float2* __restrict__ pmm, int64_t ldq) {
   const int q = blockIdx.x * 256 + threadIdx.x;
   const int t = t0 + blockIdx.y;
   const TileF T = tf[t];
   if (T.uniform != 2 || q >= nq) return;
   const float* Pr = P + (size_t)q * ldP;
+  const float* Ph = Phi + (size_t)q * ldP;   // == Pr when the prefixes are exact
   float mn = CWQ_INF, mx = -CWQ_INF;
   for (int p0 = T.par; p0 <= T.par_hi; p0 += 8) {   // 8 loads in flight
-    float pv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pv[j] = Pr[min(p0 + j, T.par_hi)];
+    float pv[8], ph[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float pi = pv[j] * T.invL;
-      mn = fminf(mn, pi);
-      mx = fmaxf(mx, pi);
+      pv[j] = Pr[min(p0 + j, T.par_hi)];
+      ph[j] = Ph[min(p0 + j, T.par_hi)];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = pv[j] * T.invL, b = ph[j] * T.invL;
+      mn = fminf(mn, fminf(a, b));
+      mx = fmaxf(mx, fmaxf(a, b));
     }
   }
   pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
 }
 
-hipError_t launch_tile_prange(const float* P, int64_t ldP, int nq, const TileF* tf, int n_rt, float2* pmm, int64_t ldq,
-                              hipStream_t s) {
+hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int nq, const TileF* tf, int n_rt,
+                              float2* pmm, int64_t ldq, hipStream_t s) {
   for (int t0 = 0; t0 < n_rt; t0 += 65535) {
     const int nt = std::min(65535, n_rt - t0);
     hipLaunchKernelGGL(tile_prange_kernel, dim3((unsigned)((nq + 255) / 256), (unsigned)nt), dim3(256), 0, s, P,
-                       ldP, nq, tf, t0, pmm, ldq);
+                       Phi ? Phi : P, ldP, nq, tf, t0, pmm, ldq);
   }
   return hipGetLastError();
 }
@@ -944,6 +1173,55 @@ __device__ __forceinline__ float exact_iso_key(const float* __restrict__ X, cons
   return fmaf(pp, md.invL, md.cw * lp);
 }
 
+// Raw sum S = sum_d (x_d A_d - B_d)^2 of internal node i for query q in the exact scan's
+// arithmetic (16-dim fma partials in dim order, summed in order): bit-identical to the
+// scan_kernel / int_small_kernel values.  Ar/Br: row-major copies of int_A/int_B.
+__device__ __forceinline__ float exact_aniso_S(const float* __restrict__ X, const float* __restrict__ Ar,
+                                               const float* __restrict__ Br, int DP, int q, int i) {
+  const float* __restrict__ ar = Ar + (size_t)i * DP;
+  const float* __restrict__ br = Br + (size_t)i * DP;
+  const int NV16 = DP / 16;
+  const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
+  float acc = 0.f;
+  for (int v = 0; v < NV16; ++v) {
+    float4 a4[4], b4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a4[j] = *reinterpret_cast<const float4*>(ar + v * 16 + j * 4);
+      b4[j] = *reinterpret_cast<const float4*>(br + v * 16 + j * 4);
+    }
+    const f32x16 xa = xg[(size_t)v * kXQ];
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 ta = a4[j >> 2], tb = b4[j >> 2];
+      const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
+      const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
+      const float t = fmaf(xa[j], aj, -bj);
+      part = (j == 0) ? t * t : fmaf(t, t, part);
+    }
+    acc += part;
+  }
+  return acc;
+}
+
+// Exact path prefix P of internal node p (> 0) from the exact root prefix: the chain of
+// prefix_level_kernel steps P = fmaf(w, lp', P[parent]) recomputed for p's ancestors.
+__device__ __forceinline__ float exact_prefix(const float* __restrict__ X, const IntChain& ch, int DP, int q, int p,
+                                              float proot) {
+  int ids[kMaxChain];
+  int n = 0;
+  for (int j = p; j > 0 && n < kMaxChain; j = ch.par_int[j]) ids[n++] = j;
+  float P = proot;
+  for (int t = n - 1; t >= 0; --t) {
+    const int a = ids[t];
+    const float S = exact_aniso_S(X, ch.Ar, ch.Br, DP, q, a);
+    const float lp = -0.5f * (ch.logdet_int[a] + S);
+    P = fmaf(ch.w_int[a], lp, P);
+  }
+  return P;
+}
+
 __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X, const float* __restrict__ Mf, int DP,
                                                     int nq, int K, int capq, const int* __restrict__ qcnt,
                                                     const int* __restrict__ qover, const int* __restrict__ crow,
@@ -953,7 +1231,8 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
                                                     const float* __restrict__ P, int64_t ldP, int seg_base,
                                                     float* pkey, float* paux, int* prow, int64_t lstride,
                                                     int* ok_flag, int* n_exact, const float* __restrict__ lkb,
-                                                    const int* __restrict__ lrb, const int* __restrict__ done) {
+                                                    const int* __restrict__ lrb, const int* __restrict__ done,
+                                                    const IntChain chain, int use_chain) {
   __shared__ int s_pend[kWavesPerWG][128];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1001,7 +1280,8 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         const int rr = crow[base + jj];
         const RowMeta md = meta[rr];
         const int p = par[rr];
-        const float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;
+        float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;   // exact, or the root's exact prefix below
+        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
         key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp);
         rid = seg_base + rr;
         ++nx;
@@ -1055,10 +1335,11 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
-                        const float* lkb, const int* lrb, const int* done, hipStream_t s) {
+                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, hipStream_t s) {
+  const IntChain ch = chain ? *chain : IntChain{nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
                      crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact,
-                     lkb, lrb, done);
+                     lkb, lrb, done, ch, chain ? 1 : 0);
   return hipGetLastError();
 }
 

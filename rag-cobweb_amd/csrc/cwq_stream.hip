@@ -99,9 +99,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   // parent-prefix cache: pi = P[q][par] * invL changes only with the parent (flat trees:
   // one load per wave)
   int cpar = -3;
-  float cP[SK_MAXQB];
+  float cP[SK_MAXQB], cPh[SK_MAXQB];   // lower / upper bound of the parent prefix (equal when exact)
 #pragma unroll
-  for (int qb = 0; qb < SK_MAXQB; ++qb) cP[qb] = 0.f;
+  for (int qb = 0; qb < SK_MAXQB; ++qb) cP[qb] = cPh[qb] = 0.f;
+  const float* Pu = a.Phi ? a.Phi : a.P;
   auto panel = [&](int64_t gi) {
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
     return reinterpret_cast<const char*>(a.Mb) + ((size_t)(grp * 16 + r16) * a.DPB + 8 * c16) * 2;
@@ -174,15 +175,19 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       if (rok && rf[j].par != cpar) {
         cpar = rf[j].par;
 #pragma unroll
-        for (int qb = 0; qb < SK_MAXQB; ++qb)
-          cP[qb] = (qok[qb] && cpar >= 0) ? a.P[(size_t)(qb * 16 + r16) * a.ldP + cpar] : 0.f;
+        for (int qb = 0; qb < SK_MAXQB; ++qb) {
+          const size_t o = (size_t)(qb * 16 + r16) * a.ldP + cpar;
+          cP[qb] = (qok[qb] && cpar >= 0) ? a.P[o] : 0.f;
+          cPh[qb] = (qok[qb] && cpar >= 0) ? Pu[o] : 0.f;
+        }
       }
 #pragma unroll
       for (int qb = 0; qb < SK_MAXQB; ++qb) {
         if (qb >= nqb) break;
         if (!rok || !qok[qb]) continue;
         float u, l;
-        fg_bounds(acc[qb][j], 0x1p-23f * fabsf(acc[qb][j]), qi[qb], rf[j], cP[qb] * rf[j].invL, a.eps_n, a.slack, u, l);
+        fg_bounds2(acc[qb][j], 0x1p-23f * fabsf(acc[qb][j]), qi[qb], rf[j], cPh[qb] * rf[j].invL,
+                   cP[qb] * rf[j].invL, a.eps_n, a.slack, u, l);
         if (MODE == 1) {
           pmax[qb] = fmaxf(pmax[qb], l);
         } else if (u >= Tq[qb]) {

@@ -257,3 +257,61 @@ def test_stream_path_two_level_tree(gpu):
         ids0, s0, ids1, s1, st = both(ix, Q, k)
         assert st["path"] == "stream", st
         assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+
+
+def three_level(pkg, X, G1, S, seed=0):
+    """root -> G1 clusters -> S sub-clusters each -> leaves (BFS order), node statistics
+    by the GPU Welford builder (the reference's increment_counts order)."""
+    N, D = X.shape
+    g = torch.Generator(device=X.device)
+    g.manual_seed(seed)
+    l1 = torch.randint(0, G1, (N,), generator=g, device=X.device)
+    l2 = l1 * S + torch.randint(0, S, (N,), generator=g, device=X.device)
+    u1, inv1, c1 = torch.unique(l1, return_inverse=True, return_counts=True)
+    u2, inv2, c2 = torch.unique(l2, return_inverse=True, return_counts=True)
+    ar = torch.arange(N, device=X.device)
+    o1 = torch.argsort(inv1 * N + ar)
+    o2 = torch.argsort(inv2 * N + ar)
+    p1 = torch.cat([torch.zeros(1, dtype=torch.int64, device=X.device), torch.cumsum(c1, 0)])
+    p2 = torch.cat([torch.zeros(1, dtype=torch.int64, device=X.device), torch.cumsum(c2, 0)])
+    n1, m1, q1 = pkg.index.welford_groups(X, o1, p1)
+    n2, m2, q2 = pkg.index.welford_groups(X, o2, p2)
+    n0, m0, q0 = pkg.index.welford_groups(X, ar, torch.tensor([0, N], device=X.device))
+    var = lambda n, q: q / n[:, None] + float(pkg.PRIOR_VAR)   # noqa: E731
+    G1n, G2n = u1.numel(), u2.numel()
+    mean = torch.cat([m0, m1, m2, X[o2]])
+    vv = torch.cat([var(n0, q0), var(n1, q1), var(n2, q2), torch.full((N, D), float(pkg.PRIOR_VAR), device=X.device)])
+    par2 = 1 + torch.searchsorted(u1, u2 // S)                          # level-2 node -> its level-1 node
+    parent = torch.cat([torch.tensor([-1]), torch.zeros(G1n, dtype=torch.int64), par2.cpu(),
+                        1 + G1n + torch.repeat_interleave(torch.arange(G2n), c2.cpu())])
+    nos = torch.empty(N, dtype=torch.int64)
+    nos[o2.cpu()] = torch.arange(1 + G1n + G2n, 1 + G1n + G2n + N)
+    return mean, vv, parent.numpy(), nos.numpy()
+
+
+@pytest.mark.parametrize("N,D,G1,S,weights", [(60000, 128, 64, 8, None), (40000, 96, 200, 4, (1.0, 0.5, 2.0, 1.0)),
+                                              (30000, 256, 16, 32, (0.3, 1.0, 1.0, 1.5))])
+def test_internal_bounds_three_level(gpu, N, D, G1, S, weights):
+    """Hierarchical trees through the filter with BOUNDED internal prefixes (bf16-MFMA
+    internal-node bounds + exact parent chains in the rerank): ids and scores identical to
+    the exact scan, for the batch filter (300 queries) and the stream filter (40)."""
+    import os
+    X = gpu.synth.synthetic_corpus(N, D, seed=N + G1)
+    mean, var, parent, nos = three_level(gpu, X, G1, S)
+    ix = gpu.index.CobwebIndex(mean, var, parent, nos, weights, device="cuda:0")
+    assert ix.info["max_depth"] == 3
+    for nq in (300, 40):
+        Q, _ = gpu.synth.synthetic_queries(X, nq, seed=nq)
+        for k in (1, 10):
+            ids0, s0, ids1, s1, st = both(ix, Q, k)
+            assert st["path"] == ("fgemm" if nq > 64 else "stream"), st
+            assert torch.equal(ids0, ids1) and torch.equal(s0, s1), (nq, k, st)
+    # the exact internal pass (bounds off) gives the same
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=300)
+    ids1, s1 = ix.score_topk(Q, 10)
+    os.environ["CWQ_INT_BOUND"] = "0"
+    try:
+        ids2, s2 = ix.score_topk(Q, 10)
+    finally:
+        del os.environ["CWQ_INT_BOUND"]
+    assert torch.equal(ids1, ids2) and torch.equal(s1, s2)
