@@ -106,6 +106,12 @@ struct cwq_index {
   TileF* iso_tf = nullptr;
   std::vector<int> tile_uni_prefix;   // prefix counts of uniform row tiles (all_uniform per launch range)
   int n_multi_tiles = 0;              // tiles with several parents (TileF uniform 2)
+  // the same tables for the categorize key min(BF[parent], lp) (cwq_categorize through the
+  // filter): lp with the 2*pi constant, no prefix term (invL 0), the categorize usable rule
+  RowF* cat_rf = nullptr;
+  TileF* cat_tf = nullptr;
+  std::vector<int> cat_uni_prefix;
+  float cat_dconst = 0.f;
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
   // internal-node bounds (hierarchical trees, cwq_mfma.hip int_bounds): bf16 b' rows,
   // their RowF constants, row-major fp32 A/B copies for the exact chain in final_kernel
@@ -140,6 +146,8 @@ struct cwq_index {
   // and the device index lists, kept between calls (grown on demand)
   void* fb = nullptr;
   size_t fb_size = 0;
+  void* fb2 = nullptr;    // categorize's filter fallback (its exact re-run uses fb itself)
+  size_t fb2_size = 0;
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -201,6 +209,7 @@ struct cwq_index {
     for (void* p : allocs) (void)hipFree(p);
     if (ws) (void)hipFree(ws);
     if (fb) (void)hipFree(fb);
+    if (fb2) (void)hipFree(fb2);
     if (hflags) (void)hipHostFree(hflags);
   }
   int host_flags(size_t n) {
@@ -276,71 +285,85 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   HIPCHK(hipMemcpyAsync(hhi.data(), nhi, ld * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const FiltConsts fc = filt_consts(DPB);
-  std::vector<RowF> rf(ld);
-  std::vector<double> gr(ld, 0.0);
-  for (int64_t r = 0; r < ld; ++r) {
-    RowF& f = rf[r];
-    const bool usable = r < NLi && (row_flags[r] & FLAG_HAS_SENT);
-    if (!usable) {
-      f = RowF{-INFINITY, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-      continue;
-    }
-    const RowMeta& m = meta[r];
-    const double hs = -0.5 * (double)m.cw * (double)m.iv, hl = -0.5 * (double)m.cw * (double)m.logdet;
-    const double g = (double)m.cw * (double)m.iv;
-    f.beta = round_up_f((double)hlo[r] + fc.gamma * (double)hhi[r]);
-    f.delta = round_up_f((double)hhi[r] + (double)hlo[r]);
-    f.rn2 = hn2[r];
-    f.hs = (float)hs;
-    f.hl = (float)hl;
-    f.invL = m.invL;
-    f.par = row_par[r];
-    gr[r] = g;
-    if (g > 0.0 && std::isfinite(g) && std::isfinite(hl)) {
-      const double rn2 = hn2[r];
-      double R = hl / g - 0.5 * rn2 + 0.5 * fc.eps_n * rn2 + fc.slack * (std::fabs(hl) / g + 1.5 * rn2);
-      R += 4.0 * fc.gamma * (std::fabs(R) + std::fabs(hl) / g + rn2);
-      f.R0 = round_up_f(R);
-    } else {
-      f.R0 = 0.f;   // only ever on non-uniform tiles
-    }
-  }
-  const int n_rt = (int)(ld / kFgTile);
-  std::vector<TileF> tf(n_rt);
-  for (int t = 0; t < n_rt; ++t) {
-    TileF& T = tf[t];
-    T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, -1, 0.f};
-    bool first = true, same_par = true;
-    int plo = INT32_MAX, phi = -1;
-    for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
-      if (rf[r].par < -1) continue;
-      const double g = gr[r];
-      if (!(g > 0.0) || !std::isfinite(g) || !std::isfinite(rf[r].R0)) T.uniform = 0;
-      if (first) {
-        T.par = rf[r].par;
-        T.invL = rf[r].invL;
-        T.g = (float)g;
-        first = false;
-      } else if (rf[r].invL != T.invL || (float)g != T.g) {
-        T.uniform = 0;
+  // per-row and per-tile constants.  Fast key (cat = false): pi + hs*S + hl with
+  // hs = -cw*iv/2, hl = -cw*logdet/2, pi = P[parent]/L.  Categorize (cat = true): the
+  // full lp = -(logdet + D log 2pi)/2 - iv*S/2 (cw = 1, no prefix term: invL = 0, tiles
+  // parent-free), min'ed with BF[parent] in the kernels; usable = not an internal copy.
+  const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
+  ix->cat_dconst = dfull;
+  auto tables = [&](bool cat, std::vector<RowF>& rf, std::vector<TileF>& tf) {
+    rf.assign(ld, RowF{});
+    std::vector<double> gr(ld, 0.0);
+    for (int64_t r = 0; r < ld; ++r) {
+      RowF& f = rf[r];
+      const bool usable = r < NLi && (cat ? !(row_flags[r] & FLAG_INT_COPY) : (row_flags[r] & FLAG_HAS_SENT) != 0);
+      if (!usable) {
+        f = RowF{-INFINITY, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+        continue;
       }
-      if (rf[r].par != T.par) same_par = false;
-      plo = std::min(plo, rf[r].par);
-      phi = std::max(phi, rf[r].par);
-      T.beta_max = std::max(T.beta_max, rf[r].beta);
-      T.delta_max = std::max(T.delta_max, rf[r].delta);
-    }
-    T.par_hi = T.par;
-    if (T.uniform && !same_par) {
-      if (plo >= 0 && phi - plo < kFgMaxTileParents && !getenv("CWQ_FG_NO_MULTI")) {
-        T.uniform = 2;
-        T.par = plo;
-        T.par_hi = phi;
+      const RowMeta& m = meta[r];
+      const double cw = cat ? 1.0 : (double)m.cw;
+      const double ldet = cat ? (double)(m.logdet + dfull) : (double)m.logdet;   // fp32 add, as the scan
+      const double hs = -0.5 * cw * (double)m.iv, hl = -0.5 * cw * ldet;
+      const double g = cw * (double)m.iv;
+      f.beta = round_up_f((double)hlo[r] + fc.gamma * (double)hhi[r]);
+      f.delta = round_up_f((double)hhi[r] + (double)hlo[r]);
+      f.rn2 = hn2[r];
+      f.hs = (float)hs;
+      f.hl = (float)hl;
+      f.invL = cat ? 0.f : m.invL;
+      f.par = row_par[r];
+      gr[r] = g;
+      if (g > 0.0 && std::isfinite(g) && std::isfinite(hl)) {
+        const double rn2 = hn2[r];
+        double R = hl / g - 0.5 * rn2 + 0.5 * fc.eps_n * rn2 + fc.slack * (std::fabs(hl) / g + 1.5 * rn2);
+        R += 4.0 * fc.gamma * (std::fabs(R) + std::fabs(hl) / g + rn2);
+        f.R0 = round_up_f(R);
       } else {
-        T.uniform = 0;
+        f.R0 = 0.f;   // only ever on non-uniform tiles
       }
     }
-  }
+    const int n_rt = (int)(ld / kFgTile);
+    tf.assign(n_rt, TileF{});
+    for (int t = 0; t < n_rt; ++t) {
+      TileF& T = tf[t];
+      T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, -1, 0.f};
+      bool first = true, same_par = true;
+      int plo = INT32_MAX, phi = -1;
+      for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
+        if (rf[r].par < -1) continue;
+        const double g = gr[r];
+        if (!(g > 0.0) || !std::isfinite(g) || !std::isfinite(rf[r].R0)) T.uniform = 0;
+        if (first) {
+          T.par = cat ? -1 : rf[r].par;
+          T.invL = rf[r].invL;
+          T.g = (float)g;
+          first = false;
+        } else if (rf[r].invL != T.invL || (float)g != T.g) {
+          T.uniform = 0;
+        }
+        if (!cat && rf[r].par != T.par) same_par = false;
+        plo = std::min(plo, rf[r].par);
+        phi = std::max(phi, rf[r].par);
+        T.beta_max = std::max(T.beta_max, rf[r].beta);
+        T.delta_max = std::max(T.delta_max, rf[r].delta);
+      }
+      T.par_hi = T.par;
+      if (T.uniform && !same_par) {
+        if (plo >= 0 && phi - plo < kFgMaxTileParents && !getenv("CWQ_FG_NO_MULTI")) {
+          T.uniform = 2;
+          T.par = plo;
+          T.par_hi = phi;
+        } else {
+          T.uniform = 0;
+        }
+      }
+    }
+  };
+  std::vector<RowF> rf;
+  std::vector<TileF> tf;
+  tables(false, rf, tf);
+  const int n_rt = (int)(ld / kFgTile);
   if ((rc = ix->upload(&ix->iso_rf, rf, s))) return rc;
   if ((rc = ix->upload(&ix->iso_tf, tf, s))) return rc;
   ix->tile_uni_prefix.assign(n_rt + 1, 0);
@@ -348,6 +371,13 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   for (int t = 0; t < n_rt; ++t) ix->tile_uni_prefix[t + 1] = ix->tile_uni_prefix[t] + (tf[t].uniform == 1 ? 1 : 0);
   ix->n_multi_tiles = 0;
   for (int t = 0; t < n_rt; ++t) ix->n_multi_tiles += tf[t].uniform == 2 ? 1 : 0;
+  HIPCHK(hipStreamSynchronize(s));   // the uploads read rf / tf, rebuilt below
+  tables(true, rf, tf);
+  if ((rc = ix->upload(&ix->cat_rf, rf, s))) return rc;
+  if ((rc = ix->upload(&ix->cat_tf, tf, s))) return rc;
+  ix->cat_uni_prefix.assign(n_rt + 1, 0);
+  for (int t = 0; t < n_rt; ++t) ix->cat_uni_prefix[t + 1] = ix->cat_uni_prefix[t] + (tf[t].uniform == 1 ? 1 : 0);
+  HIPCHK(hipStreamSynchronize(s));   // the host vectors above are freed on return
   // threshold sample: ~NL_iso/128 rows at a fixed stride, 256 <= S <= 32768 (the filter
   // phases tighten T afterwards, so a small sample only costs the first phase)
   const char* sd = getenv("CWQ_FG_SAMPLE_DIV");
@@ -1062,7 +1092,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   const IntChain chain = int_chain(ix);
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
-                      nex, lkb, lrb, done, ib ? &chain : nullptr, s));
+                      nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
   HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
@@ -1100,6 +1130,158 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   return CWQ_OK;
 }
 
+// Isotropic leaf rows through the batch bf16-MFMA filter (cwq_mfma.hip): sample pass ->
+// select -> filter launches over row-tile phases (bucket / tighten between them).  The
+// caller then runs final_kernel on the returned candidate lists (exact keys -> list
+// slot 0).  cat: the categorize key min(BF[parent], lp) (cwq_categorize) instead of the
+// Fast key; ib: bounded internal prefixes (c.P lower, c.S_int upper).
+struct IsoFilter {
+  int *qcnt, *okf, *nex, *qover, *tdone, *crow, *tr;
+  float *cu, *cl, *tl, *tlk;
+};
+
+size_t iso_filter_bytes_per_query(const cwq_index* ix, int n_rt) {
+  return (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
+         (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
+         (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0) + 4 + 64 * 4;
+}
+
+int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int K, bool cat, bool ib, Bump& b,
+                   IsoFilter& o, hipStream_t s) {
+  const int nqc = c.nq;
+  const int n_rt = (int)(ix->ld_f / kFgTile);
+  const int n_rts = ix->ld_s / kFgTile;
+  const FiltConsts fc = filt_consts(ix->DPB);
+  const int n_qt = (int)(nqf / kFgTile);
+  uint16_t* Xb = b.take<uint16_t>((size_t)nqf * ix->DPB);
+  float4* qinfo = b.take<float4>(nqf);
+  float* lb = b.take<float>((size_t)nqf * ix->ld_s + 4096);
+  float* tl = b.take<float>((size_t)nqf * 64);
+  int* tr = b.take<int>((size_t)nqf * 64);
+  // [qcnt | ok | n_exact | qover | tdone | gctr]: the host reads the first three with one
+  // copy; one memset clears the block before the filter launches (tighten_kernel
+  // clears gctr between them)
+  int* qcnt = b.take<int>((size_t)5 * nqf + 64);
+  int* okf = qcnt + nqf;
+  int* nex = qcnt + 2 * nqf;
+  int* qover = qcnt + 3 * nqf;
+  int* tdone = qcnt + 4 * nqf;                       // tighten/final incremental state
+  int* gctr = qcnt + 5 * nqf;
+  float* tlk = b.take<float>((size_t)nqf * 64);
+  int* crow = b.take<int>((size_t)nqf * kFgCapQ);
+  float* cu = b.take<float>((size_t)nqf * kFgCapQ);
+  float* cl = b.take<float>((size_t)nqf * kFgCapQ);
+  // every workgroup holds one partly filled chunk at a time: keep room for two per workgroup
+  const int64_t rec_cap = round_up(std::max<int64_t>((int64_t)nqf * kFgRecPerQ, (int64_t)2 * ix->cus * kFgChunk),
+                                   kFgChunk);
+  int4* rec = b.take<int4>((size_t)rec_cap);
+  int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
+  const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
+  int4* rec_dir = b.take<int4>((size_t)dir_cap);
+  float2* pmm = (!cat && ix->n_multi_tiles) ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
+  HIPCHK(launch_query_prep(qsrc, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
+  if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
+    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf,
+                              s));
+  FgArgs g;
+  memset(&g, 0, sizeof(g));
+  g.DPB = ix->DPB;
+  g.nq = nqc;
+  g.n_qt = n_qt;
+  fg_groups(n_qt, g.qgroups, g.rgroups);
+  g.qinfo = qinfo;
+  g.order = fg_order();
+  g.dbg = getenv("CWQ_FG_DBG") ? atoi(getenv("CWQ_FG_DBG")) : 0;
+  g.tctr = gctr + 8;
+  g.rf = cat ? ix->cat_rf : ix->iso_rf;
+  g.tf = cat ? ix->cat_tf : ix->iso_tf;
+  g.cat = cat ? 1 : 0;
+  g.pmm = pmm;
+  g.ldq = nqf;
+  g.P = cat ? (c.BF ? c.BF : ix->dummy) : (c.P ? c.P : ix->dummy);
+  g.Phi = (!cat && ib) ? c.S_int : nullptr;
+  g.ldP = std::max(ix->NI, 1);
+  g.gamma = (float)fc.gamma;
+  g.eps_n = (float)fc.eps_n;
+  g.slack = (float)fc.slack;
+  // 1. sample pass -> T[q] = K-th largest lower bound over the sample rows
+  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
+  g.mode = 1;
+  if (g.order == 2) HIPCHK(hipMemsetAsync(g.tctr, 0, 32, s));
+  g.n_rt = n_rts;
+  g.nrows = ix->ld_s;
+  g.rowmap = ix->samp_rows;
+  // large samples: lower bounds reduced to maxima over groups of 4 rows in the
+  // kernel (fgemm_kernel<1>); small ones keep one value per row so that K groups exist
+  g.lb = lb;
+  g.lbg = ix->n_samp >= 64 * K ? 4 : 1;
+  g.ldlb = ix->ld_s / g.lbg;
+  HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
+  HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
+  // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
+  // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is
+  // raised to the K-th largest candidate lower bound, so later phases emit fewer
+  g.mode = 0;
+  g.nrows = ix->NL_iso;
+  g.rowmap = nullptr;
+  g.T = tl + (K - 1);
+  g.ldT = 64;
+  g.rec = rec;
+  g.rec_cap = rec_cap;
+  g.gctr = gctr;
+  g.chunk_fill = chunk_fill;
+  g.qover = qover;
+  g.rec_dir = rec_dir;
+  g.dir_cap = dir_cap;
+  HIPCHK(hipMemsetAsync(qcnt, 0, ((size_t)5 * nqf + 64) * 4, s));
+  int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
+  const int nph = fg_phase_cuts(n_rt, cuts);
+  ix->n_fg_launch = nph;
+  for (int ph = 0; ph < nph; ++ph) {
+    g.rt_off = cuts[ph];
+    g.n_rt = cuts[ph + 1] - cuts[ph];
+    const std::vector<int>& up = cat ? ix->cat_uni_prefix : ix->tile_uni_prefix;
+    g.all_uniform = up[cuts[ph + 1]] - up[cuts[ph]] == g.n_rt && !getenv("CWQ_FG_NO_ALLUNI");
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
+    unsigned long long* stamp_d = nullptr;
+    const char* stamp_f = ph == nph - 1 ? getenv("CWQ_FG_STAMP") : nullptr;   // diagnostic builds
+    if (stamp_f) {
+      HIPCHK(hipMalloc(&stamp_d, 1 << 20));
+      HIPCHK(hipMemsetAsync(stamp_d, 0, 1 << 20, s));
+    }
+    g.stamp = stamp_d;
+    HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
+    if (stamp_f) {
+      std::vector<unsigned long long> hs(1 << 17);
+      HIPCHK(hipMemcpyAsync(hs.data(), stamp_d, 1 << 20, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(stamp_d));
+      g.stamp = nullptr;
+      if (FILE* fo = fopen(stamp_f, "wb")) {
+        fwrite(hs.data(), 8, hs.size(), fo);
+        fclose(fo);
+      }
+    }
+    if (ix->timing) {   // per-launch fgemm time (timing mode synchronises)
+      float e = 0, e0 = 0;
+      HIPCHK(hipEventRecord(ix->ev[6], s));
+      HIPCHK(hipEventSynchronize(ix->ev[6]));
+      HIPCHK(hipEventElapsedTime(&e, ix->ev[5], ix->ev[6]));
+      ix->t_ms[6] += e;
+      if (ph == 0) {
+        HIPCHK(hipEventElapsedTime(&e0, ix->ev[4], ix->ev[5]));
+        ix->t_ms[5] += e0;
+      }
+    }
+    HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl,
+                         s));
+    if (ph + 1 < nph)
+      HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, tlk, tr, tdone, gctr, s));
+  }
+  o = IsoFilter{qcnt, okf, nex, qover, tdone, crow, tr, cu, cl, tl, tlk};
+  return CWQ_OK;
+}
+
 int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                     hipStream_t s, bool allow_filter) {
   const bool general = k > 64;
@@ -1117,10 +1299,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
   const int n_rts = filt ? ix->ld_s / kFgTile : 0;
   // per query: bf16 query, info, sample bounds, threshold list, candidate lists, flags, records
-  const size_t filt_q = filt ? (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
-                                   (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
-                                   (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0) + 4 + 64 * 4
-                             : 0;
+  const size_t filt_q = filt ? iso_filter_bytes_per_query(ix, n_rt) : 0;
   const size_t extra = general ? (size_t)ix->NL * 4 + (size_t)n_pow2 * 8
                                : (size_t)n_slabs(nqb_est) * K * 12 + K * 12 + filt_q;
   int64_t cq = chunk_queries(ix, nq, extra, false);
@@ -1164,138 +1343,25 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       if (filt) {
         // isotropic rows: sample bounds -> thresholds -> MFMA filter -> candidates ->
         // exact rerank into list slot 0; anisotropic rows: exact scan into slots 1..
-        const FiltConsts fc = filt_consts(ix->DPB);
-        const int n_qt = (int)(nqf / kFgTile);
-        uint16_t* Xb = b.take<uint16_t>((size_t)nqf * ix->DPB);
-        float4* qinfo = b.take<float4>(nqf);
-        float* lb = b.take<float>((size_t)nqf * ix->ld_s + 4096);
-        float* tl = b.take<float>((size_t)nqf * 64);
-        int* tr = b.take<int>((size_t)nqf * 64);
-        // [qcnt | ok | n_exact | qover | tdone | gctr]: the host reads the first three with one
-        // copy; one memset clears the block before the filter launches (tighten_kernel
-        // clears gctr between them)
-        int* qcnt = b.take<int>((size_t)5 * nqf + 64);
-        okf = qcnt + nqf;
-        int* nex = qcnt + 2 * nqf;
-        int* qover = qcnt + 3 * nqf;
-        int* tdone = qcnt + 4 * nqf;                       // tighten/final incremental state
-        int* gctr = qcnt + 5 * nqf;
-        float* tlk = b.take<float>((size_t)nqf * 64);
-        int* crow = b.take<int>((size_t)nqf * kFgCapQ);
-        float* cu = b.take<float>((size_t)nqf * kFgCapQ);
-        float* cl = b.take<float>((size_t)nqf * kFgCapQ);
-        // every workgroup holds one partly filled chunk at a time: keep room for two per workgroup
-        const int64_t rec_cap = round_up(std::max<int64_t>((int64_t)nqf * kFgRecPerQ, (int64_t)2 * ix->cus * kFgChunk),
-                                         kFgChunk);
-        int4* rec = b.take<int4>((size_t)rec_cap);
-        int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
-        const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
-        int4* rec_dir = b.take<int4>((size_t)dir_cap);
-        float2* pmm = ix->n_multi_tiles ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
-        HIPCHK(launch_query_prep(q + q0 * ix->D, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
-        if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
-          HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf,
-                                    s));
-        FgArgs g;
-        memset(&g, 0, sizeof(g));
-        g.DPB = ix->DPB;
-        g.nq = nqc;
-        g.n_qt = n_qt;
-        fg_groups(n_qt, g.qgroups, g.rgroups);
-        g.qinfo = qinfo;
-        g.order = fg_order();
-        g.dbg = getenv("CWQ_FG_DBG") ? atoi(getenv("CWQ_FG_DBG")) : 0;
-        g.tctr = gctr + 8;
-        g.rf = ix->iso_rf;
-        g.tf = ix->iso_tf;
-        g.pmm = pmm;
-        g.ldq = nqf;
-        g.P = c.P ? c.P : ix->dummy;
-        g.Phi = ib ? c.S_int : nullptr;
-        g.ldP = std::max(ix->NI, 1);
-        g.gamma = (float)fc.gamma;
-        g.eps_n = (float)fc.eps_n;
-        g.slack = (float)fc.slack;
-        // 1. sample pass -> T[q] = K-th largest lower bound over the sample rows
-        if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
-        g.mode = 1;
-        if (g.order == 2) HIPCHK(hipMemsetAsync(g.tctr, 0, 32, s));
-        g.n_rt = n_rts;
-        g.nrows = ix->ld_s;
-        g.rowmap = ix->samp_rows;
-        // large samples: lower bounds reduced to maxima over groups of 4 rows in the
-        // kernel (fgemm_kernel<1>); small ones keep one value per row so that K groups exist
-        g.lb = lb;
-        g.lbg = ix->n_samp >= 64 * K ? 4 : 1;
-        g.ldlb = ix->ld_s / g.lbg;
-        HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
-        HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
-        // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
-        // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is
-        // raised to the K-th largest candidate lower bound, so later phases emit fewer
-        g.mode = 0;
-        g.nrows = ix->NL_iso;
-        g.rowmap = nullptr;
-        g.T = tl + (K - 1);
-        g.ldT = 64;
-        g.rec = rec;
-        g.rec_cap = rec_cap;
-        g.gctr = gctr;
-        g.chunk_fill = chunk_fill;
-        g.qover = qover;
-        g.rec_dir = rec_dir;
-        g.dir_cap = dir_cap;
-        HIPCHK(hipMemsetAsync(qcnt, 0, ((size_t)5 * nqf + 64) * 4, s));
-        int cuts[6] = {0, n_rt, n_rt, n_rt, n_rt, n_rt};
-        const int nph = fg_phase_cuts(n_rt, cuts);
-        ix->n_fg_launch = nph;
-        for (int ph = 0; ph < nph; ++ph) {
-          g.rt_off = cuts[ph];
-          g.n_rt = cuts[ph + 1] - cuts[ph];
-          g.all_uniform = ix->tile_uni_prefix[cuts[ph + 1]] - ix->tile_uni_prefix[cuts[ph]] == g.n_rt &&
-                          !getenv("CWQ_FG_NO_ALLUNI");
-          if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
-          unsigned long long* stamp_d = nullptr;
-          const char* stamp_f = ph == nph - 1 ? getenv("CWQ_FG_STAMP") : nullptr;   // diagnostic builds
-          if (stamp_f) {
-            HIPCHK(hipMalloc(&stamp_d, 1 << 20));
-            HIPCHK(hipMemsetAsync(stamp_d, 0, 1 << 20, s));
-          }
-          g.stamp = stamp_d;
-          HIPCHK(launch_fgemm(Xb, ix->iso_Mb, g, ix->cus, s));
-          if (stamp_f) {
-            std::vector<unsigned long long> hs(1 << 17);
-            HIPCHK(hipMemcpyAsync(hs.data(), stamp_d, 1 << 20, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            HIPCHK(hipFree(stamp_d));
-            g.stamp = nullptr;
-            if (FILE* fo = fopen(stamp_f, "wb")) {
-              fwrite(hs.data(), 8, hs.size(), fo);
-              fclose(fo);
-            }
-          }
-          if (ix->timing) {   // per-launch fgemm time (timing mode synchronises)
-            float e = 0, e0 = 0;
-            HIPCHK(hipEventRecord(ix->ev[6], s));
-            HIPCHK(hipEventSynchronize(ix->ev[6]));
-            HIPCHK(hipEventElapsedTime(&e, ix->ev[5], ix->ev[6]));
-            ix->t_ms[6] += e;
-            if (ph == 0) {
-              HIPCHK(hipEventElapsedTime(&e0, ix->ev[4], ix->ev[5]));
-              ix->t_ms[5] += e0;
-            }
-          }
-          HIPCHK(launch_bucket(rec, gctr, chunk_fill, rec_cap, rec_dir, dir_cap, kFgCapQ, qcnt, qover, crow, cu, cl,
-                               s));
-          if (ph + 1 < nph)
-            HIPCHK(launch_tighten(nqc, K, kFgCapQ, qcnt, qover, cl, tl + (K - 1), 64, tlk, tr, tdone, gctr, s));
-        }
+        IsoFilter fo;
+        if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, K, false, ib, b, fo, s))) return rc;
+        int* qcnt = fo.qcnt;
+        int* nex = fo.nex;
+        okf = fo.okf;
+        float* tl = fo.tl;
+        float* tlk = fo.tlk;
+        int* tr = fo.tr;
+        int* tdone = fo.tdone;
+        int* qover = fo.qover;
+        int* crow = fo.crow;
+        float* cu = fo.cu;
+        float* cl = fo.cl;
         if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
           return rc;
         const IntChain chain = int_chain(ix);
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
                             ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow,
-                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, ib ? &chain : nullptr, s));
+                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, ib ? &chain : nullptr, 0, 0.f, s));
         qcnt_d = qcnt;
         nex_d = nex;
         if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
@@ -1468,32 +1534,40 @@ extern "C" int cwq_node_logprob(cwq_index* ix, const float* q, int64_t nq, int32
   return CWQ_OK;
 }
 
-extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
-                              int32_t* n_found, int64_t* n_calls, void* stream) {
-  if (!ix || (!q && nq > 0) || (nq > 0 && (!nodes || !n_found))) return fail(CWQ_ERR_ARG, "NULL argument");
-  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
-  if (nq == 0) return CWQ_OK;
-  std::lock_guard<std::mutex> lk(ix->mu);
-  DevGuard dg(ix->device);
-  hipStream_t s = (hipStream_t)stream;
-  WsUse wu(ix, s);
-  if (wu.rc) return wu.rc;
+namespace {
+// cwq_categorize body.  allow_filter: the isotropic leaf rows go through the bf16-MFMA
+// filter with the categorize key (run_iso_filter, cat); queries whose candidate lists
+// overflow are re-run with allow_filter = false (the exact scan of every leaf row).
+int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
+                    int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   const int R = std::max(1, std::min(64, ix->NL));
   const bool complete = ix->NL <= R;
   const int64_t cap_list = 1 + (int64_t)ix->NI + R;
-  const int kl = 64, tq = scan_tq(kl);
+  const int kl = 64;
   int rc;
+  const char* ce = getenv("CWQ_CAT_FILTER");
+  const bool filt = allow_filter && use_filter(ix, R) && !(ce && *ce && atoi(ce) == 0);
+  const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
+  const size_t filt_q = filt ? iso_filter_bytes_per_query(ix, n_rt) : 0;
   const int nqb_est = n_qblocks_for(nq, kl);
-  const int max_slabs = (pick_nslab(ix, ix->NL_iso, nqb_est) + pick_nslab(ix, ix->NL_an, nqb_est) + 2) * scan_lists_per_slab(kl);
-  const int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + (size_t)max_slabs * R * 12 + R * 12);
+  auto n_slabs = [&](int nqb) {
+    return filt ? 1 + (pick_nslab(ix, ix->NL_an, nqb) + 1) * scan_lists_per_slab(kl)
+                : (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
+  };
+  const int max_slabs = n_slabs(nqb_est);
+  int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + (size_t)max_slabs * R * 12 + R * 12 + filt_q);
+  if (filt && cq < nq) cq = std::max<int64_t>(kFgTile, cq / kFgTile * kFgTile);   // whole query tiles
+  std::vector<int64_t> fredo;   // queries the filter could not certify
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
     const int nqb = n_qblocks_for(nqc, kl);
-    const int slabs = (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
+    const int slabs = n_slabs(nqb);
+    const int64_t nqf = round_up(nqc, kFgTile);
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
-                                                              (size_t)cap_list * 16 + 8) + 16 * 256;
+                                                              (size_t)cap_list * 16 + 8) + 16 * 256 +
+                  (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
@@ -1509,7 +1583,29 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if ((rc = run_internal(ix, c, s))) return rc;
     int nst = 0;
-    if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s))) return rc;
+    std::vector<char> fbad(nqc, 0);
+    if (filt) {
+      // isotropic rows: the filter with the categorize key -> exact keys in list slot 0;
+      // anisotropic rows: the exact scan into slots 1..
+      IsoFilter fo;
+      if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, R, true, false, b, fo, s))) return rc;
+      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 2, 1)))
+        return rc;
+      HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, kFgCapQ, fo.qcnt, fo.qover, fo.crow, fo.cu, fo.cl,
+                          fo.tl + (R - 1), 64, ix->row_meta, ix->row_par, c.BF ? c.BF : ix->dummy, std::max(ix->NI, 1), 0,
+                          pkey, paux, prow, (int64_t)nst * R, fo.okf, fo.nex, fo.tlk, fo.tr, fo.tdone, nullptr, 1, dfull,
+                          s));
+      std::vector<int> okh(nqc);
+      HIPCHK(hipMemcpyAsync(okh.data(), fo.okf, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (int i = 0; i < nqc; ++i)
+        if (!okh[i]) {
+          fbad[i] = 1;
+          fredo.push_back(q0 + i);
+        }
+    } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s))) {
+      return rc;
+    }
     HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s));
     SimArgs sa;
     memset(&sa, 0, sizeof(sa));
@@ -1550,7 +1646,7 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
     HIPCHK(hipStreamSynchronize(s));
     std::vector<int> redo;
     for (int i = 0; i < nqc; ++i)
-      if (st[i]) redo.push_back(i);
+      if (st[i] && !fbad[i]) redo.push_back(i);   // filter failures are re-run whole below
     if (redo.empty()) continue;
 
     // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
@@ -1609,7 +1705,50 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
       HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
     }
   }
+  if (!fredo.empty()) {
+    // filter overflow: those queries through the exact path, results scattered back
+    const int64_t n = (int64_t)fredo.size();
+    const size_t D = (size_t)ix->D;
+    const size_t o_q = round_up(n * 8, 256), o_nd = o_q + round_up(n * D * 4, 256),
+                 o_f = o_nd + round_up((int64_t)n * k * 8, 256), o_c = o_f + round_up(n * 4, 256),
+                 tot = o_c + round_up(n * 8, 256);
+    if (tot > ix->fb2_size) {
+      if (ix->ws_ev_live) (void)hipEventSynchronize(ix->ws_ev);
+      if (ix->fb2) (void)hipFree(ix->fb2);
+      ix->fb2 = nullptr;
+      ix->fb2_size = 0;
+      if (hipMalloc(&ix->fb2, tot) != hipSuccess) return fail(CWQ_ERR_OOM, "categorize fallback buffers");
+      ix->fb2_size = tot;
+    }
+    char* f = (char*)ix->fb2;
+    int64_t* d_idx = (int64_t*)f;
+    float* qs = (float*)(f + o_q);
+    int64_t* nd = (int64_t*)(f + o_nd);
+    int* fd = (int*)(f + o_f);
+    int64_t* cl = (int64_t*)(f + o_c);
+    HIPCHK(hipMemcpyAsync(d_idx, fredo.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_copy_rows(q, (int64_t)D, d_idx, qs, (int64_t)D, nullptr, n, (int64_t)D, s));
+    if ((rc = categorize_impl(ix, qs, n, k, max_nodes, nd, fd, cl, s, false))) return rc;
+    HIPCHK(launch_copy_rows(nd, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_idx, n, 2 * (int64_t)k, s));
+    HIPCHK(launch_copy_rows(fd, 1, nullptr, n_found, 1, d_idx, n, 1, s));
+    if (n_calls) HIPCHK(launch_copy_rows(cl, 2, nullptr, n_calls, 2, d_idx, n, 2, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
   return CWQ_OK;
+}
+}  // namespace
+
+extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
+                              int32_t* n_found, int64_t* n_calls, void* stream) {
+  if (!ix || (!q && nq > 0) || (nq > 0 && (!nodes || !n_found))) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  if (wu.rc) return wu.rc;
+  return categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
 }
 
 extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order,

@@ -190,6 +190,7 @@ struct FgArgs {
   int order;                              // tile order: 0 static q-fastest, 1 static r-fastest, 2 dynamic
   int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)
   int dbg;                                // ablation (perf experiments only): 1 no operand loads, 2 no epilogue
+  int cat;                                // categorize key: bounds min'ed with P[q][par] (P = BF)
   const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
   const float* T;                         // thresholds, T[q * ldT]
   int64_t ldT;
@@ -301,7 +302,8 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
-                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, hipStream_t s);
+                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
+                        float dconst, hipStream_t s);
 
 // PCA + ICA whitening (cwq_whiten.hip): C[m][n] = sum_k (A[m][k] - ctr[k]) B[n][k] (/ denom[n])
 hipError_t launch_gemm_nt_f32(const float* A, int64_t M, int K, const float* ctr, const float* B, int N,

@@ -157,18 +157,14 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 }
 
 // One prefix_level_kernel step on intervals: parent prefix in [pl, ph], lp' in [lo, hi]
-// -> [lo, hi] <- bounds of fmaf(w, lp', P_parent) as the exact pass computes it (fp64,
-// widened by 2^-22 of the magnitudes for the fp32 fmaf's rounding, rounded outward).
+// -> [lo, hi] <- bounds of fmaf(w, lp', P_parent) as the exact pass computes it.  fp32:
+// each fmaf here and the exact one round by <= 2^-24 of (|P_parent| + |w lp'|), the
+// margin subtraction by 2^-24 of the result; m = 2^-21 of the magnitudes covers all three.
 __device__ __forceinline__ void prefix_step(float pl, float ph, float w, float& lo, float& hi) {
-  const double a = (double)w * (double)lo, b = (double)w * (double)hi;
-  const double wl = fmin(a, b), wh = fmax(a, b);
-  const double m = 0x1p-22 * (fmax(fabs((double)pl), fabs((double)ph)) + fmax(fabs(wl), fabs(wh)));
-  const double l = (double)pl + wl - m, h = (double)ph + wh + m;
-  float fl = (float)l, fh = (float)h;
-  if ((double)fl > l) fl = nextafterf(fl, -CWQ_INF);
-  if ((double)fh < h) fh = nextafterf(fh, CWQ_INF);
-  lo = fl;
-  hi = fh;
+  const float a = w >= 0.f ? lo : hi, b = w >= 0.f ? hi : lo;   // w * [a, b] is ordered
+  const float m = 0x1p-21f * (fmaxf(fabsf(pl), fabsf(ph)) + fabsf(w) * fmaxf(fabsf(lo), fabsf(hi)));
+  lo = fmaf(w, a, pl) - m;
+  hi = fmaf(w, b, ph) + m;
 }
 
 // Internal-node bound operands (launch_int_prep, cwq_internal.h).  One wave per node.
@@ -687,6 +683,42 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // blocks: jb (16 rows) x half (query blocks 0-3 / 4-7): 16 values per lane
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
+    if (MODE == 2) {
+      // internal-node bounds, dense: per 16-query block ib, the wave's 16 x 64 block goes
+      // through LDS so that each store covers 64 consecutive rows of one query (256 B)
+      const int rl = r0 + wr * 64 + lane;   // this lane's row in the store phase
+      const RowF f = rl < a.nrows ? a.rf[rl] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+#pragma unroll 1
+      for (int ib = 0; ib < 8; ++ib) {
+        // acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wsc[(4 * c16 + j) * 64 + jb * 16 + r16] = acc[ib][jb][j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
+        for (int e = 0; e < 16; ++e) {
+          const int ql = wq * 128 + ib * 16 + e;
+          const int q = q0 + ql;
+          if (f.par >= -1 && q < a.nq) {
+            const float d0 = wsc[e * 64 + lane];
+            float lo, hi;
+            if (f.par < 0) {   // the root: its exact prefix
+              lo = hi = s_pl[ql];
+            } else {
+              int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
+              if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
+            }
+            a.lb[(size_t)q * a.ldlb + rl] = lo;
+            a.lb_hi[(size_t)q * a.ldlb + rl] = hi;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();   // reads of this block done before the next dump
+      }
+      goto flush;
+    }
     if (MODE == 1 && a.lbg == 4) {
       // sample pass: lower bounds reduced to row groups of 4 -- rows r16 + 16 jb of this
       // wave's 64-row block, all in one lane -- before the store.  The K-th largest group
@@ -735,6 +767,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             const float pi = (fb.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + fb.par] * fb.invL : 0.f;
             float u;
             fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, fb, pi, a.eps_n, a.slack, u, m);
+            if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, a.P[(size_t)q * a.ldP + fb.par]);
           }
           a.lb[(size_t)q * a.ldlb + g] = m;
         }
@@ -797,6 +830,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 const float pi = (f.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
                 float u;
                 fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f, pi, a.eps_n, a.slack, u, lo);
+                if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, a.P[(size_t)q * a.ldP + f.par]);
               }
               a.lb[(size_t)q * a.ldlb + r] = lo;
             } else if (usable && q < a.nq && (!uni || d0 >= 0.f)) {
@@ -821,6 +855,11 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               }
               float u, lo;
               fg_bounds2(d, ex, qi, f, pi, pl, a.eps_n, a.slack, u, lo);
+              if (a.cat && f.par >= 0) {   // categorize key min(BF[parent], lp)
+                const float bp = a.P[(size_t)q * a.ldP + f.par];
+                u = fminf(u, bp);
+                lo = fminf(lo, bp);
+              }
               if (u >= qi.w) {
                 const int4 rv = make_int4(q, r, __float_as_int(u), __float_as_int(lo));
                 const int slot = atomicAdd(&s_cnt[FG_CSLOT], 1);
@@ -1130,7 +1169,8 @@ hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* q
 // [q/16][v][q%16][16].
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float exact_iso_key(const float* __restrict__ X, const float* __restrict__ Mf, int DP,
-                                               int q, int rr, const RowMeta& md, float pp, float& lp) {
+                                               int q, int rr, const RowMeta& md, float pp, float& lp,
+                                               int cat = 0, float dconst = 0.f) {
   const float* __restrict__ mr = Mf + (size_t)rr * DP;
   const int NV16 = DP / 16;
   const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
@@ -1169,8 +1209,8 @@ __device__ __forceinline__ float exact_iso_key(const float* __restrict__ X, cons
     slice(xg[(size_t)v * kXQ], m4);
   }
   const float S = md.iv * acc;
-  lp = -0.5f * (md.logdet + 0.f + S);
-  return fmaf(pp, md.invL, md.cw * lp);
+  lp = -0.5f * (md.logdet + dconst + S);
+  return cat ? fminf(pp, lp) : fmaf(pp, md.invL, md.cw * lp);   // categorize: pp = BF[parent]
 }
 
 // Raw sum S = sum_d (x_d A_d - B_d)^2 of internal node i for query q in the exact scan's
@@ -1232,7 +1272,8 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
                                                     float* pkey, float* paux, int* prow, int64_t lstride,
                                                     int* ok_flag, int* n_exact, const float* __restrict__ lkb,
                                                     const int* __restrict__ lrb, const int* __restrict__ done,
-                                                    const IntChain chain, int use_chain) {
+                                                    const IntChain chain, int use_chain, int cat,
+                                                    float dconst) {
   __shared__ int s_pend[kWavesPerWG][128];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1280,9 +1321,9 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         const int rr = crow[base + jj];
         const RowMeta md = meta[rr];
         const int p = par[rr];
-        float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;   // exact, or the root's exact prefix below
+        float pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);   // exact (cat: BF)
         if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
-        key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp);
+        key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp, cat, dconst);
         rid = seg_base + rr;
         ++nx;
       }
@@ -1335,11 +1376,12 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
-                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, hipStream_t s) {
+                        const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
+                        float dconst, hipStream_t s) {
   const IntChain ch = chain ? *chain : IntChain{nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
                      crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact,
-                     lkb, lrb, done, ch, chain ? 1 : 0);
+                     lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst);
   return hipGetLastError();
 }
 

@@ -315,3 +315,26 @@ def test_internal_bounds_three_level(gpu, N, D, G1, S, weights):
     finally:
         del os.environ["CWQ_INT_BOUND"]
     assert torch.equal(ids1, ids2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("N,D,G,k", [(60000, 128, 0, 10), (60000, 768, 0, 1), (50000, 96, 300, 10),
+                                     (40000, 64, 2000, 25), (30000, 256, 0, 64)])
+def test_categorize_filter_equals_exact(gpu, N, D, G, k):
+    """Basic query (categorize, A4) with the isotropic leaf rows through the bf16-MFMA
+    filter on the categorize key min(BF[parent], lp): retrieved nodes in pop order, found
+    counts and log_prob call counts identical to the exact scan of every leaf row."""
+    X = gpu.synth.synthetic_corpus(N, D, seed=N + G + k)
+    if G:
+        labels = torch.randint(0, G, (N,), device="cuda:0", generator=torch.Generator(device="cuda:0").manual_seed(5))
+        t = gpu.synth.two_level_synth(X, labels)
+    else:
+        t = gpu.synth.flat_synth(X)
+    ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=k)
+    ix.set_filter(0)
+    ref = ix.categorize(Q, k)
+    ix.set_filter(1)
+    got = ix.categorize(Q, k)
+    ix.set_filter(-1)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
