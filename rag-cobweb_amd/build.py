@@ -53,13 +53,14 @@ def library_id(path=OUT):
     return m.group(1).decode() if m else None
 
 
-def build_library(force=False, verbose=False, jobs=None):
+def build_library(force=False, verbose=False, jobs=None, build_dir=None):
     extra = os.environ.get("CWQ_HIPCC_FLAGS", "").split()   # A/B experiments only
     sid = source_id(extra)
-    if not force and library_id() == sid:
-        return OUT
+    out = OUT
+    if not force and library_id(out) == sid:
+        return out
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    bdir = os.path.join(HERE, "build")
+    bdir = build_dir or os.path.join(HERE, "build")
     os.makedirs(bdir, exist_ok=True)
     common = [hipcc, f"--offload-arch={ARCH}", *FLAGS, *extra, f'-DCWQ_BUILD_ID="{sid}"']
 
@@ -74,12 +75,12 @@ def build_library(force=False, verbose=False, jobs=None):
     n = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 2) // 2), 8)
     with cf.ThreadPoolExecutor(n) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT + ".tmp"]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
