@@ -1004,9 +1004,6 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
   float* paux = b.take<float>((size_t)nq_pad * slabs * K);
   int* prow = b.take<int>((size_t)nq_pad * slabs * K);
-  float* okey = b.take<float>((size_t)nq_pad * K);
-  float* oaux = b.take<float>((size_t)nq_pad * K);
-  int* orow = b.take<int>((size_t)nq_pad * K);
   uint16_t* Xb = b.take<uint16_t>((size_t)nq16 * ix->DPB);
   float4* qinfo = b.take<float4>(nq16);
   int* Tb = b.take<int>((size_t)(K + 1) * nqc);   // [K][nq] blocks + [nq] live threshold
@@ -1027,16 +1024,55 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   int* tr = b.take<int>((size_t)nqc * 64);
   const bool ib = use_int_bounds(ix);
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
-  HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-  if (ib) {
-    if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
-  } else if ((rc = run_internal(ix, c, s, false))) {
-    return rc;
+  // one fused prep launch when the exact internal pass is small (flat trees: the root)
+  bool fused = !ib && ix->NI <= kSbMaxNI && (int)ix->levels.size() <= kSbMaxNI &&
+               ((size_t)ix->NI * (ix->DP / 16) + ix->NI) * 4 <= 65536 && !getenv("CWQ_SB_UNFUSED");
+  SbPrepArgs sp;
+  if (fused) {
+    memset(&sp, 0, sizeof(sp));
+    sp.q = q;
+    sp.nq = nqc;
+    sp.D = ix->D;
+    sp.DP = ix->DP;
+    sp.DPB = ix->DPB;
+    sp.nq_pad = c.nq_pad;
+    sp.nq16 = nq16;
+    sp.X = c.X;
+    sp.Xb = Xb;
+    sp.qinfo = qinfo;
+    sp.c = ix->iso_c;
+    sp.A = ix->int_A;
+    sp.B = ix->int_B;
+    sp.ld = ix->ld_int;
+    sp.NI = ix->NI;
+    sp.par_int = ix->par_int;
+    sp.w_int = ix->w_int;
+    sp.logdet_int = ix->logdet_int;
+    sp.P = c.P;
+    sp.ldP = std::max(ix->NI, 1);
+    sp.qcnt = qcnt;
+    sp.nlev = (int)ix->levels.size();
+    for (int l = 0; l < sp.nlev && fused; ++l) {
+      sp.lv0[l] = ix->levels[l].first;
+      if (l > 0 && ix->levels[l].first != ix->levels[l - 1].second) fused = false;   // BFS: contiguous levels
+    }
+    if (sp.nlev > 0) sp.lv0[sp.nlev] = ix->levels.back().second;
+    if (ix->NI > 0 && (!c.P || sp.nlev == 0 || sp.lv0[0] != 0 || sp.lv0[sp.nlev] != ix->NI)) fused = false;
   }
-  if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
-  HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
-  HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
-  HIPCHK(launch_stream_init(Tb, (K + 1) * nqc, s));
+  if (fused) {
+    HIPCHK(launch_sb_prep(sp, s));
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
+  } else {
+    HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if (ib) {
+      if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
+    } else if ((rc = run_internal(ix, c, s, false))) {
+      return rc;
+    }
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
+    HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
+    HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
+  }
   const FiltConsts fc = filt_consts(ix->DPB);
   StreamArgs a;
   memset(&a, 0, sizeof(a));
@@ -1060,6 +1096,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   // the publishing atomics cost more than the ~3x fewer candidates save -- so off
   a.live_every = 0;
   if (const char* e = getenv("CWQ_STREAM_LIVE")) a.live_every = std::max(0, atoi(e));
+  if (a.live_every > 0) HIPCHK(launch_stream_init(Tb, (K + 1) * nqc, s));   // only the live threshold reads Tb
   a.T = T;
   a.qcnt = qcnt;
   a.qover = qover;
@@ -1095,8 +1132,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                       nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
-  HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
-  HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids, scores, s));
+  HIPCHK(launch_merge_expand(pkey, paux, prow, nqc, nst * K, K, k, ix->sent_ptr, ix->sent_ids, ids, scores, s));
   if ((rc = ix->host_flags((size_t)3 * nqc))) return rc;
   HIPCHK(hipMemcpyAsync(ix->hflags, qcnt, (size_t)3 * nqc * 4, hipMemcpyDeviceToHost, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[3], s));
@@ -1334,9 +1370,6 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
       float* paux = b.take<float>((size_t)nq_pad * slabs * K);
       int* prow = b.take<int>((size_t)nq_pad * slabs * K);
-      float* okey = b.take<float>((size_t)nq_pad * K);
-      float* oaux = b.take<float>((size_t)nq_pad * K);
-      int* orow = b.take<int>((size_t)nq_pad * K);
       int nst = 0;
       int* okf = nullptr;
       int *qcnt_d = nullptr, *nex_d = nullptr;
@@ -1370,9 +1403,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           return rc;
       }
       if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
-      HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * K, K, okey, oaux, orow, s));
-      HIPCHK(launch_expand(okey, orow, nqc, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
-                           scores ? scores + q0 * k : nullptr, s));
+      HIPCHK(launch_merge_expand(pkey, paux, prow, nqc, nst * K, K, k, ix->sent_ptr, ix->sent_ids, ids + q0 * k,
+                                 scores ? scores + q0 * k : nullptr, s));
       if (filt) {
         if ((rc = ix->host_flags((size_t)3 * nqf))) return rc;
         HIPCHK(hipMemcpyAsync(ix->hflags, qcnt_d, (size_t)3 * nqf * 4, hipMemcpyDeviceToHost, s));

@@ -113,6 +113,9 @@ hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int 
                                float* LPF, hipStream_t s);
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
                         float* okey, float* oaux, int* orow, hipStream_t s);
+hipError_t launch_merge_expand(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K, int k,
+                               const int64_t* sent_ptr, const int64_t* sent_ids, int64_t* ids, float* scores,
+                               hipStream_t s);
 hipError_t launch_expand(const float* okey, const int* orow, int nq, int K, int k, const int64_t* sent_ptr,
                          const int64_t* sent_ids, int64_t* ids, float* scores, hipStream_t s);
 hipError_t launch_sort_rows(float* keys, int* rows, int nq, int n, int n_pow2, hipStream_t s);
@@ -132,6 +135,7 @@ constexpr int kFgTile = 256;      // fgemm tile edge (queries and rows); operand
 constexpr int kFgCap = 512;       // candidate records per tile (LDS staging)
 constexpr int kFgChunk = 2048;    // record slots a workgroup claims at a time
 constexpr int kFgCapQ = 4096;     // candidate records per query
+constexpr int kFinalWideMaxQ = 256;   // final_kernel: workgroup per query up to this many queries
 
 // Per filter row (isotropic leaf-class row) constants, 32 B.
 struct RowF {
@@ -220,6 +224,28 @@ struct FgArgs {
 };
 // Small-batch stream filter (cwq_stream.hip): nq <= kStreamMaxQ queries per launch
 constexpr int kStreamMaxQ = 64;
+// small-batch prep (launch_sb_prep): pad + query prep + exact internal pass + counter clear
+constexpr int kSbMaxNI = 64;
+struct SbPrepArgs {
+  const float* q;       // [nq][D] caller queries
+  int nq, D, DP, DPB;
+  int64_t nq_pad, nq16;
+  float* X;             // scan layout, nq_pad rows
+  void* Xb;             // bf16 hi parts [nq16][DPB]
+  float4* qinfo;        // [nq16]
+  const float* c;       // centre (root mean)
+  const float *A, *B;   // internal nodes, dim-major [DP][ld]
+  int64_t ld;
+  int NI;
+  const int* par_int;
+  const float *w_int, *logdet_int;
+  float* P;             // [nq][ldP] exact prefixes
+  int64_t ldP;
+  int* qcnt;            // [5][nq] counters to clear
+  int nlev;
+  int lv0[kSbMaxNI + 1];   // level ranges [lv0[l], lv0[l+1])
+};
+hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s);
 constexpr int kStreamMaxLds = 160 * 1024;
 inline size_t stream_lds_bytes(int nqb, int DPB) { return (size_t)nqb * (DPB / 32) * 64 * 16; }
 struct StreamArgs {

@@ -38,7 +38,9 @@ __device__ __forceinline__ float rl_f(float v, int lane) {
 __device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
 // Shift a per-lane list entry one slot up (slot i receives slot i-1) inside a
-// group of KL lanes.  KL = 16: DPP row_shr:1 (rows of 16 lanes); KL = 64: bpermute.
+// group of KL lanes.  KL = 16: DPP row_shr:1 (rows of 16 lanes); KL = 64: DPP
+// wave_shr:1 (GFX9 whole-wave shift; lane 0 keeps its value, never used as a shifted
+// entry) -- a VALU op instead of a ds_bpermute round trip through the LDS unit.
 template <int KL>
 __device__ __forceinline__ int shift_up(int v);
 template <>
@@ -47,7 +49,7 @@ __device__ __forceinline__ int shift_up<16>(int v) {
 }
 template <>
 __device__ __forceinline__ int shift_up<64>(int v) {
-  return __shfl_up(v, 1, 64);
+  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
 }
 
 // Insert candidate (ck, ca, cr) into the sorted list held by lane group g.
@@ -428,6 +430,86 @@ hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, i
                         float* oaux, int* orow, hipStream_t s) {
   dim3 grid((unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG)), block(256);
   hipLaunchKernelGGL(merge_kernel, grid, block, 0, s, pkey, paux, prow, nq, nent, K, okey, oaux, orow);
+  return hipGetLastError();
+}
+
+// merge_kernel + expand_kernel in one launch (top-k paths): one wave per query merges
+// the per-slab lists, then expands its top rows into sentence ids with the lanes in
+// parallel -- lane i owns list entry i, an exclusive prefix sum of the entries' sentence
+// counts gives each its output slots -- instead of one thread walking the list through
+// dependent loads.  Same ids and order as expand_kernel.
+__global__ __launch_bounds__(256) void merge_expand_kernel(const float* __restrict__ pkey,
+                                                           const float* __restrict__ paux,
+                                                           const int* __restrict__ prow, int nq, int nent, int K,
+                                                           int k, const int64_t* __restrict__ sent_ptr,
+                                                           const int64_t* __restrict__ sent_ids, int64_t* ids,
+                                                           float* scores) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  float lk = -CWQ_INF, la = 0.f;
+  int lr = 0x7fffffff;
+  const size_t base = (size_t)q * nent;
+  if (nent == K) {   // one list (the filter paths): already the sorted top-K
+    if (lane < K) {
+      lk = pkey[base + lane];
+      lr = prow[base + lane];
+    }
+  } else {
+    for (int e0 = 0; e0 < nent; e0 += kWave) {
+      const int e = e0 + lane;
+      float ek = -CWQ_INF, ea = 0.f;
+      int er = 0x7fffffff;
+      if (e < nent) {
+        ek = pkey[base + e];
+        ea = paux[base + e];
+        er = prow[base + e];
+      }
+      const float tk = rl_f(lk, K - 1);
+      const int tr = rl_i(lr, K - 1);
+      const bool c = ek != -CWQ_INF && (ek > tk || (ek == tk && er < tr));
+      uint64_t mask = __ballot(c);
+      while (mask) {
+        const int j = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        list_insert<64>(lk, la, lr, 0, lane, rl_f(ek, j), rl_f(ea, j), rl_i(er, j), K);
+      }
+    }
+  }
+  // entries up to the first empty one (expand_kernel stops there)
+  const bool valid = lane < K && lk != -CWQ_INF && lr != 0x7fffffff;
+  const uint64_t vm = __ballot(valid);
+  const int nvalid = (~vm) ? __builtin_ctzll(~vm) : 64;
+  int64_t s0 = 0;
+  int cnt = 0;
+  if (lane < nvalid) {
+    s0 = sent_ptr[lr];
+    cnt = (int)(sent_ptr[lr + 1] - s0);
+  }
+  int off = cnt;   // inclusive scan
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(off, d, 64);
+    if (lane >= d) off += o;
+  }
+  const int total = __shfl(off, 63, 64);
+  off -= cnt;
+  for (int j = 0; j < cnt && off + j < k; ++j) {
+    ids[(size_t)q * k + off + j] = sent_ids[s0 + j];
+    if (scores) scores[(size_t)q * k + off + j] = lk;
+  }
+  for (int t = total + lane; t < k; t += kWave) {
+    ids[(size_t)q * k + t] = -1;
+    if (scores) scores[(size_t)q * k + t] = -CWQ_INF;
+  }
+}
+
+hipError_t launch_merge_expand(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K, int k,
+                               const int64_t* sent_ptr, const int64_t* sent_ids, int64_t* ids, float* scores,
+                               hipStream_t s) {
+  if (K > kWave) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG)), block(256);
+  hipLaunchKernelGGL(merge_expand_kernel, grid, block, 0, s, pkey, paux, prow, nq, nent, K, k, sent_ptr, sent_ids, ids,
+                     scores);
   return hipGetLastError();
 }
 

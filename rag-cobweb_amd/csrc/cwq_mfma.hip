@@ -52,6 +52,8 @@ typedef __attribute__((address_space(1))) void glb_void;
 
 #define CWQ_INF __builtin_inff()
 
+// whole-wave shift by one lane (lane i <- lane i-1; lane 0 keeps v): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
 __device__ __forceinline__ float rl_f2(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -153,6 +155,87 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
                              float4* qinfo, hipStream_t s) {
   hipLaunchKernelGGL(query_prep_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DPB, nq_pad,
                      (__bf16*)Xb, qinfo);
+  return hipGetLastError();
+}
+
+// Small-batch query prep (the per-call stream path, nq <= kStreamMaxQ, flat trees and
+// trees with few internal nodes): one launch does the work of pad_queries_kernel,
+// query_prep_kernel, the exact internal pass (int_small_kernel + one
+// prefix_level_kernel per level) and the candidate-counter clear.  One 256-thread
+// workgroup per padded query row.  The arithmetic is the same as those kernels':
+// query_prep's sums run in wave 0 with its loop and shuffle order; an internal node's
+// raw sum is its 16-dim fma partials (t = fmaf(x, A, -B), dimension order), computed
+// here one slice per thread, then added in slice order by one thread (acc += part);
+// the prefixes are prefix_level_kernel's fmaf chain, level by level.
+__global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
+  extern __shared__ float s_sb[];   // [NI][NV16] partials, then [NI] prefixes
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t r = blockIdx.x;
+  const bool valid = r < a.nq;
+  const int NV16 = a.DP / 16;
+  // pad_queries_kernel: the scan's interleaved layout [r/kXQ][v][r%kXQ][16]
+  for (int d = tid; d < a.DP; d += 256) {
+    const int64_t o = (((r / kXQ) * NV16 + d / 16) * kXQ + (r % kXQ)) * 16 + (d % 16);
+    a.X[o] = (valid && d < a.D) ? a.q[r * a.D + d] : 0.f;
+  }
+  if (r < a.nq16 && tid < 64) {   // query_prep_kernel (wave 0)
+    double sv = 0.0, slo = 0.0, shi = 0.0;
+    for (int d = lane; d < a.DPB; d += kWave) {
+      const float v = (valid && d < a.D) ? a.q[r * a.D + d] - a.c[d] : 0.f;
+      const __bf16 h = (__bf16)v;
+      const float hf = (float)h;
+      const float lo = v - hf;
+      reinterpret_cast<__bf16*>(a.Xb)[r * a.DPB + d] = h;
+      sv += (double)v * (double)v;
+      slo += (double)lo * (double)lo;
+      shi += (double)hf * (double)hf;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      sv += __shfl_xor(sv, off, 64);
+      slo += __shfl_xor(slo, off, 64);
+      shi += __shfl_xor(shi, off, 64);
+    }
+    if (lane == 0) a.qinfo[r] = make_float4((float)sv, up(sqrt(shi)), up(sqrt(slo)), 0.f);
+  }
+  if (!valid) return;
+  if (tid < 5) a.qcnt[(size_t)tid * a.nq + r] = 0;
+  if (a.NI == 0) return;
+  // internal nodes: partials of (node n, slice v), straight from the caller's query
+  float* part = s_sb;
+  for (int t = tid; t < a.NI * NV16; t += 256) {
+    const int n = t / NV16, v = t - n * NV16;
+    float pp;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int d = v * 16 + j;
+      const float x = d < a.D ? a.q[r * a.D + d] : 0.f;
+      const float tt = fmaf(x, a.A[(size_t)d * a.ld + n], -a.B[(size_t)d * a.ld + n]);
+      pp = (j == 0) ? tt * tt : fmaf(tt, tt, pp);
+    }
+    part[t] = pp;
+  }
+  __syncthreads();
+  float* Pl = s_sb + a.NI * NV16;
+  for (int lv = 0; lv < a.nlev; ++lv) {
+    for (int i = a.lv0[lv] + tid; i < a.lv0[lv + 1]; i += 256) {
+      float acc = 0.f;
+      for (int v = 0; v < NV16; ++v) acc += part[i * NV16 + v];
+      const float lp = -0.5f * (a.logdet_int[i] + acc);
+      const int p = a.par_int[i];
+      const float P = p >= 0 ? fmaf(a.w_int[i], lp, Pl[p]) : a.w_int[i] * lp;
+      Pl[i] = P;
+      a.P[(size_t)r * a.ldP + i] = P;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s) {
+  const size_t lds = ((size_t)a.NI * (a.DP / 16) + a.NI) * 4;
+  if (a.nq <= 0 || a.nq_pad < a.nq16 || a.nq16 < a.nq || a.DP % 16 || a.NI > kSbMaxNI || a.nlev > kSbMaxNI ||
+      lds > 65536)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sb_prep_kernel, dim3((unsigned)a.nq_pad), dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
@@ -1010,8 +1093,8 @@ __device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, floa
   const bool prec = lk > ck || (lk == ck && lr < cr);
   const int pos = __popcll(__ballot(prec));
   if (pos < K) {
-    const float sk = __int_as_float(__shfl_up(__float_as_int(lk), 1, 64));
-    const int sr = __shfl_up(lr, 1, 64);
+    const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
+    const int sr = wave_shr1(lr);
     if (lane == pos) {
       lk = ck;
       lr = cr;
@@ -1343,9 +1426,9 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         const bool prec = lk > ck || (lk == ck && lr < cr);
         const int pos = __popcll(__ballot(prec));
         if (pos < K) {
-          const float sk = __int_as_float(__shfl_up(__float_as_int(lk), 1, 64));
-          const float sa = __int_as_float(__shfl_up(__float_as_int(la), 1, 64));
-          const int sr = __shfl_up(lr, 1, 64);
+          const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
+          const float sa = __int_as_float(wave_shr1(__float_as_int(la)));
+          const int sr = wave_shr1(lr);
           if (lane == pos) {
             lk = ck;
             la = ca;
@@ -1372,6 +1455,146 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
   }
 }
 
+// final for small batches (nq <= kFinalWideMaxQ, the per-call paths): one 512-thread
+// workgroup per query.  The exact keys are the same arithmetic as exact_iso_key, split
+// differently over the threads: the 16-dim partials of up to 64 survivors are computed in
+// parallel (one thread per (survivor, slice) -- every load of a round in flight at once),
+// then lane s of wave 0 adds survivor s's partials in slice order (acc += part, as the
+// scan does), so the keys are bit-identical; the per-lane form pays one row's dependent
+// load chain per round (~33 us of a 1-query call at C3).
+constexpr int kFwThreads = 512;
+__global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
+    const float* __restrict__ X, const float* __restrict__ Mf, int DP, int nq, int K, int capq,
+    const int* __restrict__ qcnt, const int* __restrict__ qover, const int* __restrict__ crow,
+    const float* __restrict__ cu, const float* __restrict__ cl, const float* __restrict__ T, int64_t ldT,
+    const RowMeta* __restrict__ meta, const int* __restrict__ par, const float* __restrict__ P, int64_t ldP,
+    int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
+    const float* __restrict__ lkb, const int* __restrict__ lrb, const int* __restrict__ done, const IntChain chain,
+    int use_chain, int cat, float dconst) {
+  extern __shared__ float s_dyn[];
+  const int NV16 = DP / 16, LDP = NV16 + 1;                  // odd row pitch: conflict-free column reads
+  float* s_part = s_dyn;                                      // [64][LDP]
+  int* s_surv = reinterpret_cast<int*>(s_dyn + 64 * LDP);    // [capq] survivor positions
+  __shared__ int s_rr[64];
+  __shared__ int s_ns;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x;
+  const int n = qcnt[q];
+  const float Tq = T[(size_t)q * ldT];
+  const bool ok = qover[q] == 0 && n >= K && n <= capq && Tq > -CWQ_INF;   // uniform over the block
+  float lk = -CWQ_INF, la = 0.f;
+  int lr = 0x7fffffff, nx = 0;
+  const size_t base = (size_t)q * capq;
+  if (ok) {
+    if (wave == 0) {
+      const int d = done[q];
+      float tk = d ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
+      int tr = d ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
+      for (int j0 = d; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        list64_offer(tk, tr, lane, j < n ? cl[base + j] : -CWQ_INF, j, K);
+      }
+      const float T2 = rl_f2(tk, K - 1);
+      int ns = 0;
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        const bool c = j < n && cu[base + j] >= T2;
+        const uint64_t bm = __ballot(c);
+        if (c) s_surv[ns + __popcll(bm & ((1ull << lane) - 1))] = j;
+        ns += __popcll(bm);
+      }
+      if (lane == 0) s_ns = ns;
+    }
+    __syncthreads();
+    const int ns = s_ns;
+    const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
+    for (int r0 = 0; r0 < ns; r0 += 64) {
+      const int cnt = min(64, ns - r0);
+      RowMeta md;
+      float pp = 0.f;
+      int rr = 0;
+      if (wave == 0 && lane < cnt) {
+        rr = crow[base + s_surv[r0 + lane]];
+        md = meta[rr];
+        const int p = par[rr];
+        pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);
+        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
+        s_rr[lane] = rr;
+      }
+      __syncthreads();   // s_rr visible; the previous round's partials consumed
+      for (int t = tid; t < cnt * NV16; t += kFwThreads) {
+        const int sv = t / NV16, v = t - sv * NV16;
+        const float* __restrict__ mr = Mf + (size_t)s_rr[sv] * DP + v * 16;
+        float4 m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
+        const f32x16 xa = xg[(size_t)v * kXQ];
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float4 t4 = m4[j >> 2];
+          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+          const float tt = xa[j] - mj;
+          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+        }
+        s_part[sv * LDP + v] = part;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const bool act = lane < cnt;
+        float key = -CWQ_INF, lp = 0.f;
+        int rid = 0x7fffffff;
+        if (act) {
+          float acc = 0.f;
+          for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+          const float S = md.iv * acc;
+          lp = -0.5f * (md.logdet + dconst + S);
+          key = cat ? fminf(pp, lp) : fmaf(pp, md.invL, md.cw * lp);
+          rid = seg_base + rr;
+          ++nx;
+        }
+        uint64_t mask = __ballot(act);
+        while (mask) {
+          const int b = __builtin_ctzll(mask);
+          mask &= mask - 1;
+          const float ck = rl_f2(key, b), ca = rl_f2(lp, b);
+          const int cr = __builtin_amdgcn_readlane(rid, b);
+          const bool prec = lk > ck || (lk == ck && lr < cr);
+          const int pos = __popcll(__ballot(prec));
+          if (pos < K) {
+            const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
+            const float sa = __int_as_float(wave_shr1(__float_as_int(la)));
+            const int sr = wave_shr1(lr);
+            if (lane == pos) {
+              lk = ck;
+              la = ca;
+              lr = cr;
+            } else if (lane > pos) {
+              lk = sk;
+              la = sa;
+              lr = sr;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (wave != 0) return;
+  if (lane < K) {
+    const size_t o = (size_t)q * lstride + lane;
+    pkey[o] = ok ? lk : -CWQ_INF;
+    paux[o] = la;
+    prow[o] = ok ? lr : 0x7fffffff;
+  }
+  for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
+  if (lane == 0) {
+    ok_flag[q] = ok ? 1 : 0;
+    if (n_exact) n_exact[q] = nx;
+  }
+}
+
+size_t final_wide_lds(int DP, int capq) { return ((size_t)64 * (DP / 16 + 1) + (size_t)capq) * 4; }
+
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
@@ -1379,6 +1602,17 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
                         float dconst, hipStream_t s) {
   const IntChain ch = chain ? *chain : IntChain{nullptr, nullptr, nullptr, nullptr, nullptr};
+  static const int wide_max = [] {
+    const char* e = getenv("CWQ_FINAL_WIDE");   // largest nq for the workgroup-per-query form
+    return e && *e ? atoi(e) : kFinalWideMaxQ;
+  }();
+  const size_t lds = final_wide_lds(DP, capq);
+  if (nq <= wide_max && lds <= 65536) {
+    hipLaunchKernelGGL(final_wide_kernel, dim3((unsigned)nq), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
+                       qover, crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag,
+                       n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
                      crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact,
                      lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst);
