@@ -168,20 +168,24 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 // here one slice per thread, then added in slice order by one thread (acc += part);
 // the prefixes are prefix_level_kernel's fmaf chain, level by level.
 __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
-  extern __shared__ float s_sb[];   // [NI][NV16] partials, then [NI] prefixes
+  extern __shared__ float s_sb[];   // [DQ] query row, [NI][NV16] partials, [NI] prefixes
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t r = blockIdx.x;
   const bool valid = r < a.nq;
   const int NV16 = a.DP / 16;
+  const int DQ = a.DP > a.DPB ? a.DP : a.DPB;
+  float* xq = s_sb;   // the query row, zero padded: every phase below reads it from LDS
+  for (int d = tid; d < DQ; d += 256) xq[d] = (valid && d < a.D) ? a.q[r * a.D + d] : 0.f;
+  __syncthreads();
   // pad_queries_kernel: the scan's interleaved layout [r/kXQ][v][r%kXQ][16]
   for (int d = tid; d < a.DP; d += 256) {
     const int64_t o = (((r / kXQ) * NV16 + d / 16) * kXQ + (r % kXQ)) * 16 + (d % 16);
-    a.X[o] = (valid && d < a.D) ? a.q[r * a.D + d] : 0.f;
+    a.X[o] = xq[d];
   }
   if (r < a.nq16 && tid < 64) {   // query_prep_kernel (wave 0)
     double sv = 0.0, slo = 0.0, shi = 0.0;
     for (int d = lane; d < a.DPB; d += kWave) {
-      const float v = (valid && d < a.D) ? a.q[r * a.D + d] - a.c[d] : 0.f;
+      const float v = (valid && d < a.D) ? xq[d] - a.c[d] : 0.f;
       const __bf16 h = (__bf16)v;
       const float hf = (float)h;
       const float lo = v - hf;
@@ -201,21 +205,21 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
   if (tid < 5) a.qcnt[(size_t)tid * a.nq + r] = 0;
   if (a.NI == 0) return;
   // internal nodes: partials of (node n, slice v), straight from the caller's query
-  float* part = s_sb;
+  float* part = s_sb + DQ;
   for (int t = tid; t < a.NI * NV16; t += 256) {
     const int n = t / NV16, v = t - n * NV16;
     float pp;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int d = v * 16 + j;
-      const float x = d < a.D ? a.q[r * a.D + d] : 0.f;
+      const float x = xq[d];
       const float tt = fmaf(x, a.A[(size_t)d * a.ld + n], -a.B[(size_t)d * a.ld + n]);
       pp = (j == 0) ? tt * tt : fmaf(tt, tt, pp);
     }
     part[t] = pp;
   }
   __syncthreads();
-  float* Pl = s_sb + a.NI * NV16;
+  float* Pl = part + a.NI * NV16;
   for (int lv = 0; lv < a.nlev; ++lv) {
     for (int i = a.lv0[lv] + tid; i < a.lv0[lv + 1]; i += 256) {
       float acc = 0.f;
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
 }
 
 hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s) {
-  const size_t lds = ((size_t)a.NI * (a.DP / 16) + a.NI) * 4;
+  const size_t lds = ((size_t)std::max(a.DP, a.DPB) + (size_t)a.NI * (a.DP / 16) + a.NI) * 4;
   if (a.nq <= 0 || a.nq_pad < a.nq16 || a.nq16 < a.nq || a.DP % 16 || a.NI > kSbMaxNI || a.nlev > kSbMaxNI ||
       lds > 65536)
     return hipErrorInvalidValue;
@@ -771,7 +775,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       // through LDS so that each store covers 64 consecutive rows of one query (256 B)
       const int rl = r0 + wr * 64 + lane;   // this lane's row in the store phase
       const RowF f = rl < a.nrows ? a.rf[rl] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-#pragma unroll 1
+      // ib unrolled: a dynamically indexed acc[ib] would be copied to scratch memory
+#pragma unroll
       for (int ib = 0; ib < 8; ++ib) {
         // acc[ib][jb][j] = C[query wq*128 + ib*16 + 4*c16 + j][row wr*64 + jb*16 + r16]
 #pragma unroll
@@ -1330,14 +1335,16 @@ __device__ __forceinline__ float exact_aniso_S(const float* __restrict__ X, cons
 
 // Exact path prefix P of internal node p (> 0) from the exact root prefix: the chain of
 // prefix_level_kernel steps P = fmaf(w, lp', P[parent]) recomputed for p's ancestors.
+// The chain is walked top-down by re-walking from p (depth^2 parent loads, no local
+// array: a dynamically indexed one would put every caller on scratch memory).
 __device__ __forceinline__ float exact_prefix(const float* __restrict__ X, const IntChain& ch, int DP, int q, int p,
                                               float proot) {
-  int ids[kMaxChain];
   int n = 0;
-  for (int j = p; j > 0 && n < kMaxChain; j = ch.par_int[j]) ids[n++] = j;
+  for (int j = p; j > 0 && n < kMaxChain; j = ch.par_int[j]) ++n;
   float P = proot;
   for (int t = n - 1; t >= 0; --t) {
-    const int a = ids[t];
+    int a = p;
+    for (int u = 0; u < t; ++u) a = ch.par_int[a];   // the ancestor t levels above p
     const float S = exact_aniso_S(X, ch.Ar, ch.Br, DP, q, a);
     const float lp = -0.5f * (ch.logdet_int[a] + S);
     P = fmaf(ch.w_int[a], lp, P);
@@ -1546,7 +1553,16 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         int rid = 0x7fffffff;
         if (act) {
           float acc = 0.f;
-          for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+          const float* pr = s_part + lane * LDP;
+          int v = 0;
+          for (; v + 8 <= NV16; v += 8) {   // 8 reads in flight, then the adds in slice order
+            float t8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t8[u] = pr[v + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += t8[u];
+          }
+          for (; v < NV16; ++v) acc += pr[v];
           const float S = md.iv * acc;
           lp = -0.5f * (md.logdet + dconst + S);
           key = cat ? fminf(pp, lp) : fmaf(pp, md.invL, md.cw * lp);
