@@ -639,6 +639,13 @@ extern "C" int cwq_index_info(const cwq_index* idx, int64_t* o) {
   return CWQ_OK;
 }
 
+// Scan configuration of one query call (cwq_kernels.hip scan_cfg_begin): fixed from the
+// call's total query count, so every chunk and workspace estimate of the call agrees.
+struct ScanCfgScope {
+  explicit ScanCfgScope(int64_t nq) { scan_cfg_begin(nq); }
+  ~ScanCfgScope() { scan_cfg_end(); }
+};
+
 // ---------------------------------------------------------------------------
 // Query orchestration
 // ---------------------------------------------------------------------------
@@ -658,7 +665,9 @@ struct Chunk {
 int n_qblocks_for(int64_t nq, int kl) {
   const int qpb = scan_queries_per_block(kl);
   const int n = (int)((nq + qpb - 1) / qpb);
-  return scan_xcd_map() ? (int)round_up(n, 8) : n;
+  // XCD-aware mapping needs a multiple of 8 blocks; below 8 the padding blocks would be
+  // 7/8 of the grid and of the slab count chosen for it, so small calls map plainly
+  return scan_xcd_map() && n >= 8 ? (int)round_up(n, 8) : n;
 }
 
 // Choose the slab split of a segment: enough workgroups for >= ~5 waves of the
@@ -1479,6 +1488,7 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   for (int64_t& t : ix->stats) t = 0;
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
   return score_topk_impl(ix, q, nq, k, ids, scores, s, true);
 }
@@ -1518,6 +1528,7 @@ extern "C" int cwq_rank_scores(cwq_index* ix, const float* q, int64_t nq, float*
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
   const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4, false);
   int rc;
@@ -1545,6 +1556,7 @@ extern "C" int cwq_node_logprob(cwq_index* ix, const float* q, int64_t nq, int32
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
   const float dconst = full ? (float)((double)ix->D * (double)logf(2.0f * (float)M_PI)) : 0.f;
   const int64_t cq = chunk_queries(ix, nq, (size_t)ix->NL * 4);
@@ -1780,6 +1792,7 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   DevGuard dg(ix->device);
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
   return categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
 }

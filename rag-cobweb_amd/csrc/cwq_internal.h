@@ -98,6 +98,9 @@ hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_
 // The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
 hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
                        const ScanArgs& a, int nslab, hipStream_t s);
+constexpr int kScanSmallQ = 256;     // calls with at most this many queries use the shared-query scan
+void scan_cfg_begin(int64_t nq);     // scan configuration for the current call (thread-local)
+void scan_cfg_end();
 int scan_tq(int kl);                 // queries per wave for a list width
 int scan_rows_per_tile(int kl);      // rows per workgroup step (64 * rows per lane [* 4 if shared queries])
 int scan_queries_per_block(int kl);  // queries per workgroup

@@ -305,10 +305,30 @@ static const ScanCfg kHotCfgs[] = {
     {16, 2, 16, 1},   // 3
 };
 constexpr int kNumHotCfgs = sizeof(kHotCfgs) / sizeof(kHotCfgs[0]);
-static int hot_cfg() {
+// Configuration of the current query call (scan_cfg_begin/end around each entry point,
+// from its total query count): a few queries leave 3 of 4 waves of a query-per-wave
+// workgroup idle and too few waves per SIMD to cover the scalar query loads, so small
+// calls use the shared-query form (4 waves split the rows of one 16-query block).
+// CWQ_SCAN_CFG forces one configuration for every call.
+static thread_local int tl_cfg = -1;
+static int env_cfg() {
   const char* e = getenv("CWQ_SCAN_CFG");
-  const int v = e ? atoi(e) : 0;
+  if (!e || !*e) return -1;
+  const int v = atoi(e);
   return (v < 0 || v >= kNumHotCfgs) ? 0 : v;
+}
+void scan_cfg_begin(int64_t nq) {
+  static const int small_q = [] {
+    const char* e = getenv("CWQ_SCAN_SMALLQ");
+    return e && *e ? atoi(e) : kScanSmallQ;
+  }();
+  tl_cfg = env_cfg() >= 0 ? env_cfg() : (nq <= small_q ? 3 : 0);
+}
+void scan_cfg_end() { tl_cfg = -1; }
+static int hot_cfg() {
+  if (tl_cfg >= 0) return tl_cfg;
+  const int v = env_cfg();
+  return v < 0 ? 0 : v;
 }
 
 int scan_tq(int kl) { return kl == 16 ? kHotCfgs[hot_cfg()].tq : 16; }
@@ -330,8 +350,10 @@ int scan_lists_per_slab(int kl) { return kl == 16 && kHotCfgs[hot_cfg()].shq ? k
                      a.pkey, a.paux, a.prow, a)
 
 template <bool ISO, int EPI, bool CAT>
-static hipError_t launch_scan_t(int kl, const float* X, const float* A, const float* B, const ScanArgs& a, int nslab,
+static hipError_t launch_scan_t(int kl, const float* X, const float* A, const float* B, const ScanArgs& a0, int nslab,
                                 hipStream_t s) {
+  ScanArgs a = a0;
+  if (a.n_qblocks % 8) a.xcd_map = 0;   // fewer than 8 query blocks: plain mapping (n_qblocks_for)
   dim3 grid((unsigned)(nslab * a.n_qblocks)), block(256);
   if (kl == 16) {
     switch (hot_cfg()) {
