@@ -1644,10 +1644,8 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
                         float dconst, hipStream_t s) {
   const IntChain ch = chain ? *chain : IntChain{nullptr, nullptr, nullptr, nullptr, nullptr};
-  static const int wide_max = [] {
-    const char* e = getenv("CWQ_FINAL_WIDE");   // largest nq for the workgroup-per-query form
-    return e && *e ? atoi(e) : kFinalWideMaxQ;
-  }();
+  const char* we = getenv("CWQ_FINAL_WIDE");   // largest nq for the workgroup-per-query form
+  const int wide_max = we && *we ? atoi(we) : kFinalWideMaxQ;
   const size_t lds = final_wide_lds(DP, capq);
   if (nq <= wide_max && lds <= 65536) {
     hipLaunchKernelGGL(final_wide_kernel, dim3((unsigned)nq), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
