@@ -59,7 +59,9 @@ __device__ __forceinline__ int f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 
-template <int MODE>
+// MQB: query blocks the instantiation holds (1: nq <= 16, the per-call case, fewer live
+// registers; SK_MAXQB otherwise)
+template <int MODE, int MQB>
 __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sq[];   // [nqb][nk][64 lanes][16 B]
   const int lane = threadIdx.x & 63;
@@ -74,11 +76,11 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     *reinterpret_cast<uint4*>(sq + (size_t)f * 16) = v;
   }
   // per-lane query terms for the lane's column (query qb*16 + (lane & 15))
-  float4 qi[SK_MAXQB];
-  float Tq[SK_MAXQB];
-  bool qok[SK_MAXQB];
+  float4 qi[MQB];
+  float Tq[MQB];
+  bool qok[MQB];
 #pragma unroll
-  for (int qb = 0; qb < SK_MAXQB; ++qb) {
+  for (int qb = 0; qb < MQB; ++qb) {
     const int q = qb * 16 + (lane & 15);
     qok[qb] = qb < nqb && q < a.nq;
     qi[qb] = qok[qb] ? a.qinfo[q] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -93,15 +95,15 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   const int64_t gstride = (int64_t)gridDim.x * SK_WAVES;
   const int c16 = lane >> 4, r16 = lane & 15;
   // probe: max of the lower bounds per query over the current group
-  float pmax[SK_MAXQB];
+  float pmax[MQB];
 #pragma unroll
-  for (int qb = 0; qb < SK_MAXQB; ++qb) pmax[qb] = -CWQ_INF;
+  for (int qb = 0; qb < MQB; ++qb) pmax[qb] = -CWQ_INF;
   // parent-prefix cache: pi = P[q][par] * invL changes only with the parent (flat trees:
   // one load per wave)
   int cpar = -3;
-  float cP[SK_MAXQB], cPh[SK_MAXQB];   // lower / upper bound of the parent prefix (equal when exact)
+  float cP[MQB], cPh[MQB];   // lower / upper bound of the parent prefix (equal when exact)
 #pragma unroll
-  for (int qb = 0; qb < SK_MAXQB; ++qb) cP[qb] = cPh[qb] = 0.f;
+  for (int qb = 0; qb < MQB; ++qb) cP[qb] = cPh[qb] = 0.f;
   const float* Pu = a.Phi ? a.Phi : a.P;
   auto panel = [&](int64_t gi) {
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
@@ -111,35 +113,47 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   // k = ks*32 + 8*(lane >> 4)); the next chunk -- after the last one, the first chunk of
   // the wave's next group -- is in flight during this chunk's MFMAs and the epilogue.
   bf16x8 cur[SK_CH], nxt[SK_CH];
+  // row terms of the rows this lane's accumulator columns hold (r0 + 4*c16 + j), one group
+  // ahead like the panel chunks (at D = 256 a group is one chunk, so a load at the group's
+  // start would put its latency on every group)
+  constexpr bool PRE_RF = MQB == 1;
+  RowF rfn[4];
+  auto load_rf = [&](int64_t g) {
+    const int64_t r0n = (MODE == 1 ? g * a.probe_stride : g) * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t r = r0n + 4 * c16 + j;
+      rfn[j] = r < a.nrows ? a.rf[r] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+    }
+  };
   int64_t gi = (int64_t)blockIdx.x * SK_WAVES + wave;
   if (gi < ngroups) {
     const char* src = panel(gi);
 #pragma unroll
     for (int i = 0; i < SK_CH; ++i)
       if (i < nk) cur[i] = *reinterpret_cast<const bf16x8*>(src + i * 64);
+    if (PRE_RF) load_rf(gi);
   }
   int it = 0;
   for (; gi < ngroups; gi += gstride, ++it) {
     // live threshold every `live_every` groups, loaded now and used in the epilogue (the
     // load is in flight with the row panel): T = max(T, Tlive[q])
     const bool live = MODE == 0 && a.live_every > 0 && it % a.live_every == a.live_every - 1;
-    int tlive[SK_MAXQB];
+    int tlive[MQB];
 #pragma unroll
-    for (int qb = 0; qb < SK_MAXQB; ++qb) tlive[qb] = (live && qok[qb]) ? a.Tlive[qb * 16 + r16] : 0x80000000;
+    for (int qb = 0; qb < MQB; ++qb) tlive[qb] = (live && qok[qb]) ? a.Tlive[qb * 16 + r16] : 0x80000000;
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
     const int64_t r0 = grp * 16;   // < nrows rounded up to 16 (probe: grp < ngroups of the panel)
     RowF rf[4];
+    if (!PRE_RF) load_rf(gi);   // registers too tight for a group-ahead copy
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t r = r0 + 4 * c16 + j;
-      rf[j] = r < a.nrows ? a.rf[r] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-    }
+    for (int j = 0; j < 4; ++j) rf[j] = rfn[j];   // PRE_RF: loaded with the group's first chunk
     const char* src = panel(gi);
     const int64_t gn = gi + gstride;
     const char* srcn = gn < ngroups ? panel(gn) : nullptr;
-    f32x4 acc[SK_MAXQB];
+    f32x4 acc[MQB];
 #pragma unroll
-    for (int qb = 0; qb < SK_MAXQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < nk; c0 += SK_CH) {
       if (c0 + SK_CH < nk) {
 #pragma unroll
@@ -149,9 +163,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
         for (int i = 0; i < SK_CH; ++i)
           if (i < nk) nxt[i] = *reinterpret_cast<const bf16x8*>(srcn + i * 64);
+        if (PRE_RF) load_rf(gn);   // the next group's row terms fly with its first chunk
       }
 #pragma unroll
-      for (int qb = 0; qb < SK_MAXQB; ++qb) {
+      for (int qb = 0; qb < MQB; ++qb) {
         if (qb >= nqb) break;
         const char* qs = sq + (((size_t)qb * nk + c0) * 64 + lane) * 16;
 #pragma unroll
@@ -165,7 +180,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
     if (live) {
 #pragma unroll
-      for (int qb = 0; qb < SK_MAXQB; ++qb) Tq[qb] = fmaxf(Tq[qb], ord2f(tlive[qb]));
+      for (int qb = 0; qb < MQB; ++qb) Tq[qb] = fmaxf(Tq[qb], ord2f(tlive[qb]));
     }
     // ---- epilogue: rigorous bounds per (row, query); acc[qb][j] = dot of row
     // r0 + 4*c16 + j with query qb*16 + (lane & 15)
@@ -175,14 +190,14 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       if (rok && rf[j].par != cpar) {
         cpar = rf[j].par;
 #pragma unroll
-        for (int qb = 0; qb < SK_MAXQB; ++qb) {
+        for (int qb = 0; qb < MQB; ++qb) {
           const size_t o = (size_t)(qb * 16 + r16) * a.ldP + cpar;
           cP[qb] = (qok[qb] && cpar >= 0) ? a.P[o] : 0.f;
           cPh[qb] = (qok[qb] && cpar >= 0) ? Pu[o] : 0.f;
         }
       }
 #pragma unroll
-      for (int qb = 0; qb < SK_MAXQB; ++qb) {
+      for (int qb = 0; qb < MQB; ++qb) {
         if (qb >= nqb) break;
         if (!rok || !qok[qb]) continue;
         float u, l;
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
     if (MODE == 1) {   // the group's max lower bound per query -> lb[q][gi]
 #pragma unroll
-      for (int qb = 0; qb < SK_MAXQB; ++qb) {
+      for (int qb = 0; qb < MQB; ++qb) {
         float m = fmaxf(pmax[qb], __shfl_xor(pmax[qb], 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
         if (lane < 16 && qok[qb]) a.lb[(size_t)(qb * 16 + lane) * a.ldlb + gi] = m;
@@ -234,18 +249,24 @@ hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s)
     return hipErrorInvalidValue;
   static bool attr = false;   // dynamic LDS above the 64 KiB default
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_kernel<1>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
-    if (e != hipSuccess) return e;
+    const void* fns[4] = {reinterpret_cast<const void*>(&stream_kernel<0, 1>),
+                          reinterpret_cast<const void*>(&stream_kernel<0, SK_MAXQB>),
+                          reinterpret_cast<const void*>(&stream_kernel<1, 1>),
+                          reinterpret_cast<const void*>(&stream_kernel<1, SK_MAXQB>)};
+    for (const void* f : fns) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
-  if (mode == 1)
-    hipLaunchKernelGGL(stream_kernel<1>, dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
-  else
-    hipLaunchKernelGGL(stream_kernel<0>, dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
+  const dim3 grid((unsigned)n_wg), block(64 * SK_WAVES);
+  if (a.nqb == 1) {
+    if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, 1>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((stream_kernel<0, 1>), grid, block, lds, s, a);
+  } else {
+    if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, SK_MAXQB>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((stream_kernel<0, SK_MAXQB>), grid, block, lds, s, a);
+  }
   return hipGetLastError();
 }
 
