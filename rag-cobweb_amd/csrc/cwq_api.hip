@@ -291,6 +291,12 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   // parent-free), min'ed with BF[parent] in the kernels; usable = not an internal copy.
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   ix->cat_dconst = dfull;
+  // multi-parent tiles keep the pretest up to this many parents (deep trees: ~4 leaves
+  // per parent puts ~64 parents in a 256-row tile); CWQ_FG_MAX_PARENTS overrides
+  const int max_parents = [] {
+    const char* e = getenv("CWQ_FG_MAX_PARENTS");
+    return e && *e ? std::max(1, atoi(e)) : kFgMaxTileParents;
+  }();
   auto tables = [&](bool cat, std::vector<RowF>& rf, std::vector<TileF>& tf) {
     rf.assign(ld, RowF{});
     std::vector<double> gr(ld, 0.0);
@@ -350,7 +356,7 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
       }
       T.par_hi = T.par;
       if (T.uniform && !same_par) {
-        if (plo >= 0 && phi - plo < kFgMaxTileParents && !getenv("CWQ_FG_NO_MULTI")) {
+        if (plo >= 0 && phi - plo < max_parents && !getenv("CWQ_FG_NO_MULTI")) {
           T.uniform = 2;
           T.par = plo;
           T.par_hi = phi;
@@ -788,12 +794,32 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   g.Sroot = Sroot;
   g.root_w = ix->root_w;
   g.root_ld = ix->root_ld;
-  // one pass: the root row gets its exact prefix, rows whose parent is the root their
-  // prefix bounds (fused), deeper rows lp' bounds for the level passes below
-  HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
-  for (size_t lv = 2; lv < ix->levels.size(); ++lv)
-    HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first, ix->levels[lv].second,
-                                ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
+  // One launch per tree level (the root and depth 1 together): each row's prefix bounds
+  // are finished in the epilogue from its parent's, which the previous launch wrote
+  // (prefix_step on intervals), so the bounds are written once and never re-read by a
+  // separate prefix pass.  A row tile straddling two levels is computed by both launches
+  // with identical results.  Measured on balanced trees (1M x 768, 10k queries): branching
+  // 10 / depth 5 internal pass 10.7 -> 10.3 ms, branching 4 / depth 9 36.3 -> 38.7 ms (the
+  // small levels' launches and the parent gathers cost what the prefix passes did), so it
+  // is off by default: CWQ_INT_LEVELS=1 enables it.
+  const char* el = getenv("CWQ_INT_LEVELS");
+  const bool per_level = el && *el && atoi(el) == 1 && ix->levels.size() > 2;
+  if (!per_level) {
+    HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+    for (size_t lv = 2; lv < ix->levels.size(); ++lv)
+      HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first,
+                                  ix->levels[lv].second, ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
+    return CWQ_OK;
+  }
+  g.fuse_prefix = 1;
+  g.order = 0;   // static tile order: no claim counters to reset between the launches
+  for (size_t lv = 1; lv < ix->levels.size(); ++lv) {
+    const int i0 = lv == 1 ? 0 : ix->levels[lv].first, i1 = ix->levels[lv].second;
+    if (i1 <= i0) continue;
+    g.rt_off = i0 / kFgTile;
+    g.n_rt = (i1 - 1) / kFgTile - g.rt_off + 1;
+    HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+  }
   return CWQ_OK;
 }
 

@@ -165,7 +165,7 @@ struct TileF {
   int par_hi;
   float pad1;
 };
-constexpr int kFgMaxTileParents = 64;   // uniform 2 only up to this many parents per tile
+constexpr int kFgMaxTileParents = 257;  // uniform 2 up to this many parents per tile (all: a tile has 256 rows)
 
 // Rigorous bounds l <= key_fp32 <= u of an isotropic row's Fast key from an approximate
 // bf16-MFMA dot product x_hi.mu_hi (error eextra on top of the bf16 split terms; see the
@@ -198,6 +198,7 @@ struct FgArgs {
   int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)
   int dbg;                                // ablation (perf experiments only): 1 no operand loads, 2 no epilogue
   int cat;                                // categorize key: bounds min'ed with P[q][par] (P = BF)
+  int fuse_prefix;                        // mode 2, one launch per tree level: prefix bounds from the parent's
   const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
   const float* T;                         // thresholds, T[q * ldT]
   int64_t ldT;

@@ -798,6 +798,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             } else {
               int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
               if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
+              else if (a.fuse_prefix)   // deeper: the parent's bounds, final since the previous level's launch
+                prefix_step(a.lb[(size_t)q * a.ldlb + f.par], a.lb_hi[(size_t)q * a.ldlb + f.par], f.invL, lo, hi);
             }
             a.lb[(size_t)q * a.ldlb + rl] = lo;
             a.lb_hi[(size_t)q * a.ldlb + rl] = hi;
@@ -907,6 +909,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 } else {
                   int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
                   if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
+                  else if (a.fuse_prefix)
+                    prefix_step(a.lb[(size_t)q * a.ldlb + f.par], a.lb_hi[(size_t)q * a.ldlb + f.par], f.invL, lo, hi);
                 }
                 a.lb[(size_t)q * a.ldlb + r] = lo;
                 a.lb_hi[(size_t)q * a.ldlb + r] = hi;
@@ -1196,34 +1200,38 @@ __global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restric
       pb = max(pb, T.par_hi);
     }
   }
-  if (pb < 0) return;   // no multi-parent tile in the run
-  const int span = pb - pa + 1;
-  const bool staged = span <= kPrSpan;
-  if (staged) {
+  if (pb < 0) return;   // no multi-parent tile in the run (uniform over the block)
+  const int ql = tid % kPrQ, t = t0 + tid / kPrQ;
+  const int q = q0 + ql;
+  bool act = t < t1 && q < nq;
+  TileF T{};
+  if (act) {
+    T = tf[t];
+    act = T.uniform == 2;
+  }
+  float mn = CWQ_INF, mx = -CWQ_INF;
+  // the run's parent range through LDS in windows of kPrSpan parents (coalesced rows)
+  for (int w0 = pa; w0 <= pb; w0 += kPrSpan) {
+    const int span = min(kPrSpan, pb - w0 + 1);
+    __syncthreads();   // the previous window is consumed
     for (int i = tid; i < kPrQ * span; i += 256) {
-      const int ql = i / span, p = pa + (i - ql * span);
-      const int q = q0 + ql;
-      if (q < nq) {
-        s_lo[ql][p - pa] = P[(size_t)q * ldP + p];
-        s_hi[ql][p - pa] = Phi[(size_t)q * ldP + p];
+      const int qq = i / span, p = w0 + (i - qq * span);
+      if (q0 + qq < nq) {
+        s_lo[qq][p - w0] = P[(size_t)(q0 + qq) * ldP + p];
+        s_hi[qq][p - w0] = Phi[(size_t)(q0 + qq) * ldP + p];
       }
     }
     __syncthreads();
+    if (act) {
+      const int p0 = max(T.par, w0), p1 = min(T.par_hi, w0 + span - 1);
+      for (int p = p0; p <= p1; ++p) {
+        const float a = s_lo[ql][p - w0] * T.invL, b = s_hi[ql][p - w0] * T.invL;
+        mn = fminf(mn, fminf(a, b));
+        mx = fmaxf(mx, fmaxf(a, b));
+      }
+    }
   }
-  const int ql = tid % kPrQ, t = t0 + tid / kPrQ;
-  const int q = q0 + ql;
-  if (t >= t1 || q >= nq) return;
-  const TileF T = tf[t];
-  if (T.uniform != 2) return;
-  float mn = CWQ_INF, mx = -CWQ_INF;
-  for (int p = T.par; p <= T.par_hi; ++p) {
-    const float lo = staged ? s_lo[ql][p - pa] : P[(size_t)q * ldP + p];
-    const float hi = staged ? s_hi[ql][p - pa] : Phi[(size_t)q * ldP + p];
-    const float a = lo * T.invL, b = hi * T.invL;
-    mn = fminf(mn, fminf(a, b));
-    mx = fmaxf(mx, fmaxf(a, b));
-  }
-  pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
+  if (act) pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
 }
 
 hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int nq, const TileF* tf, int n_rt,

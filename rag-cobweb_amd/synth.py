@@ -84,3 +84,51 @@ def two_level_synth(X, labels):
     meanSq = torch.cat([r_m2, c_m2, torch.zeros((N, D), device=dev)])   # leaves: count 1, meanSq 0
     return dict(mean=mean, var=var, parent=parent.numpy(), node_of_sentence=node_of_sentence.numpy(),
                 n_clusters=G, count=count, meanSq=meanSq)
+
+
+def balanced_synth(X, branching, depth, seed=0):
+    """A deep tree shaped like a Cobweb hierarchy: the rows are split recursively
+    `depth` times into `branching` groups of (nearly) equal size along a random direction
+    per group (so that siblings are spatially coherent, as Cobweb's concepts are), the
+    last level's groups holding the rows as count-1 leaves.  Node stats by sequential
+    Welford over each node's rows (ascending row index).  BFS order: root, level 1, ...,
+    level `depth`, then the leaves (by parent, then row index).  Empty groups are dropped."""
+    N, D = X.shape
+    dev = X.device
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    rows = torch.arange(N, device=dev)
+    r_cnt, r_mu, r_m2 = welford_groups(X, rows, torch.tensor([0, N], device=dev))
+    means, vars_, parent = [r_mu], [_var_of(r_cnt, r_m2)], [torch.tensor([-1])]
+    off_prev, off = 0, 1                      # BFS offset of the previous / current level
+    gl = torch.zeros(N, dtype=torch.int64, device=dev)
+    for _ in range(depth):
+        ng = int(gl.max()) + 1
+        dirs = torch.randn((ng, D), generator=gen, device=dev)
+        proj = (X * dirs[gl]).sum(1)
+        order = torch.argsort(proj)
+        order = order[torch.argsort(gl[order], stable=True)]    # by group, then projection
+        cnt = torch.bincount(gl, minlength=ng)
+        start = torch.cumsum(cnt, 0) - cnt
+        rank = torch.empty(N, dtype=torch.int64, device=dev)
+        rank[order] = rows - start[gl[order]]
+        chunk = torch.clamp(rank * branching // cnt[gl].clamp(min=1), max=branching - 1)
+        uniq, gl = torch.unique(gl * branching + chunk, sorted=True, return_inverse=True)
+        G = uniq.numel()
+        parent.append((uniq // branching).cpu() + off_prev)    # previous level's group -> its BFS index
+        ordr = torch.argsort(gl * N + rows)                      # by group, then row index
+        gptr = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+        gptr[1:] = torch.cumsum(torch.bincount(gl, minlength=G), 0)
+        cc, mu, m2 = welford_groups(X, ordr, gptr)
+        means.append(mu)
+        vars_.append(_var_of(cc, m2))
+        off_prev, off = off, off + G
+    leaf_order = torch.argsort(gl * N + rows)
+    G = int(gl.max()) + 1
+    parent.append(off_prev + torch.repeat_interleave(torch.arange(G), torch.bincount(gl, minlength=G).cpu()))
+    mean = torch.cat(means + [X[leaf_order]])
+    var = torch.cat(vars_ + [torch.full((N, D), float(PRIOR_VAR), device=dev)])
+    node_of_sentence = torch.empty(N, dtype=torch.int64)
+    node_of_sentence[leaf_order.cpu()] = torch.arange(off, off + N)
+    return dict(mean=mean, var=var, parent=torch.cat(parent).to(torch.int64).numpy(),
+                node_of_sentence=node_of_sentence.numpy(), n_internal=off)

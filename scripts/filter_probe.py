@@ -25,11 +25,16 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1")
     ap.add_argument("--clusters", type=int, default=0, help="0: flat tree; G: root -> G random clusters -> leaves")
+    ap.add_argument("--balanced", default=None, help="B,L: a depth-L tree of branching B (synth.balanced_synth)")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
-    if args.clusters:
+    if args.balanced:
+        b, lv = (int(v) for v in args.balanced.split(","))
+        fs = pkg.synth.balanced_synth(X, b, lv)
+        print(f"balanced tree: branching {b}, depth {lv}: {fs['n_internal']} internal nodes", flush=True)
+    elif args.clusters:
         g = torch.Generator(device=dev)
         g.manual_seed(7)
         labels = torch.randint(0, args.clusters, (args.n,), generator=g, device=dev)

@@ -338,3 +338,22 @@ def test_categorize_filter_equals_exact(gpu, N, D, G, k):
     ix.set_filter(-1)
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("branching,depth", [(4, 6), (3, 8), (10, 3)])
+@pytest.mark.parametrize("levels", ["1", "0"])
+def test_deep_balanced_tree(gpu, branching, depth, levels, monkeypatch):
+    """Deep trees shaped like Cobweb hierarchies (synth.balanced_synth): internal-node
+    bounds one launch per level with fused prefix steps (CWQ_INT_LEVELS=1, default) or one
+    launch + per-level prefix passes (0); multi-parent leaf tiles with up to ~90 parents;
+    ids and scores identical to the exact scan, batch and per-call paths."""
+    monkeypatch.setenv("CWQ_INT_LEVELS", levels)
+    X = gpu.synth.synthetic_corpus(30000, 64, seed=61)
+    t = gpu.synth.balanced_synth(X, branching, depth, seed=62)
+    ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=63)
+    for q in (Q, Q[:3]):
+        ids0, s0, ids1, s1, st = both(ix, q, 10)
+        assert st["filter_used"], st
+        assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    ix.close()
