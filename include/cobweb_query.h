@@ -80,7 +80,8 @@ int cwq_index_destroy(cwq_index* idx);
 
 /* Index facts: out[0]=n_nodes out[1]=dim out[2]=n_sent out[3]=internal nodes
  * out[4]=leaf-class rows out[5]=isotropic rows out[6]=max depth out[7]=device bytes
- * (the handle's own copies; the workspace grows on demand up to ~8 GiB per call).
+ * (the handle's own copies; the workspace grows on demand up to 40% of the free device
+ * memory, 2-48 GiB, per call; CWQ_WS_BUDGET_MB overrides).
  * Device footprint per node row: internal nodes 8*DP B (1/sigma, mu/sigma), isotropic
  * leaf rows 4*DP (dim-major mean) + 4*DP (row-major mean) + 2*DPB (bf16) + 32 B,
  * anisotropic leaf rows 8*DP B; C3 (1M x 768) 7.8 GB, C4 (10M x 1024) 104 GB -- the
