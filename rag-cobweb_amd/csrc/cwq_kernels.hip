@@ -873,8 +873,183 @@ __global__ void simulate_kernel(const SimArgs a) {
   a.status[q] = status;
 }
 
+// The same replay, one wave per query on a 64-ary heap: a pop's sift-down reads a node's
+// 64 children with one coalesced load and picks the first in heap order with a wave
+// reduction, so a pop is ~log64(n) dependent memory round trips instead of log2(n) (the
+// heap of a best-first search over a 1M-leaf tree holds ~10^5 entries); pushes sift up by
+// lane 0.  heap_before is a strict total order (the BFS index breaks every tie), so any
+// correct priority queue pops the same sequence as the binary heap above.
+__device__ __forceinline__ bool wheap_before(float s1, float p1, int t1, float s2, float p2, int t2) {
+  if (s1 != s2) return s1 > s2;
+  if (p1 != p2) return p1 < p2;
+  return t1 < t2;
+}
+
+__device__ void wheap_push(HeapEnt* h, int64_t& n, const HeapEnt& e, int lane) {
+  if (lane == 0) {
+    int64_t i = n;
+    while (i > 0) {
+      const int64_t p = (i - 1) >> 6;
+      const HeapEnt hp = h[p];
+      if (!wheap_before(e.score, e.pscore, e.tb, hp.score, hp.pscore, hp.tb)) break;
+      h[i] = hp;
+      i = p;
+    }
+    h[i] = e;
+  }
+  ++n;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// best (first in heap order) of the lanes' candidates; lanes with ok == false ignored;
+// returns the winning lane (-1 if none)
+__device__ __forceinline__ int wave_best(bool ok, float sc, float ps, int tb) {
+  // lexicographic: max score, then min pscore, then min tb, one ballot round each
+  float m = ok ? sc : -CWQ_INF;
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  bool c = ok && sc == m;
+  if (__ballot(ok) == 0) return -1;
+  float mp = c ? ps : CWQ_INF;
+  for (int off = 32; off > 0; off >>= 1) mp = fminf(mp, __shfl_xor(mp, off, 64));
+  c = c && ps == mp;
+  int mt = c ? tb : 0x7fffffff;
+  for (int off = 32; off > 0; off >>= 1) mt = min(mt, __shfl_xor(mt, off, 64));
+  c = c && tb == mt;
+  const uint64_t bm = __ballot(c);
+  return bm ? __builtin_ctzll(bm) : -1;
+}
+
+__device__ HeapEnt wheap_pop(HeapEnt* h, int64_t& n, int lane) {
+  const HeapEnt top = h[0];
+  --n;
+  const HeapEnt last = h[n];
+  int64_t i = 0;
+  for (;;) {
+    const int64_t c0 = (i << 6) + 1;
+    if (c0 >= n) break;
+    const int64_t c = c0 + lane;
+    const bool ok = c < n;
+    HeapEnt ce = ok ? h[c] : HeapEnt{-CWQ_INF, 0.f, 0x7fffffff, 0};
+    const int b = wave_best(ok, ce.score, ce.pscore, ce.tb);
+    const float bs = __shfl(ce.score, b, 64), bp = __shfl(ce.pscore, b, 64);
+    const int bt = __shfl(ce.tb, b, 64), bn = __shfl(ce.node, b, 64);
+    if (!wheap_before(bs, bp, bt, last.score, last.pscore, last.tb)) break;
+    if (lane == 0) h[i] = HeapEnt{bs, bp, bt, bn};
+    i = c0 + b;
+  }
+  if (n > 0 && lane == 0) h[i] = last;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return top;
+}
+
+__global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
+  int64_t hn = 0;
+  const bool dense = a.R == 0;
+  const float* lk = a.lkey + (size_t)q * a.R;
+  const float* lx = a.laux + (size_t)q * a.R;
+  const int* lw = a.lrow + (size_t)q * a.R;
+  const float tau = (dense || a.complete) ? -CWQ_INF : lk[a.R - 1];
+  const bool exact_all = dense || a.complete || tau == -CWQ_INF;
+  int status = 0, found = 0;
+  int64_t calls = 1, visited = 0;
+  // the list entries this lane holds (LIST mode: R <= 64 rows, checked in parallel)
+  const bool lvalid = !dense && lane < a.R && lk[lane] != -CWQ_INF && lw[lane] != 0x7fffffff;
+  const int lrow_ = lvalid ? lw[lane] : -1;
+  const int lpar_ = lvalid ? a.row_par[lrow_] : -3;
+  const float lsc_ = lvalid ? lx[lane] : 0.f;
+  // entries of the list up to the first empty one (the binary-heap form stops there)
+  const int nvalid = [&] {
+    const uint64_t vm = __ballot(!dense && lane < a.R && !lvalid);
+    const int first_bad = vm ? __builtin_ctzll(vm) : 64;
+    return dense ? 0 : min(first_bad, a.R);
+  }();
+
+  if (a.NI > 0) {
+    wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0}, lane);
+  } else {   // single-node tree: the root is leaf row 0
+    float lp = -CWQ_INF;
+    if (dense) {
+      lp = a.dense_lpf[(size_t)q * a.ldL];
+    } else {
+      const uint64_t bm = __ballot(lane < nvalid && lrow_ == 0);
+      if (bm) lp = __shfl(lsc_, 63 - __builtin_clzll(bm), 64);   // the last match, as the loop above
+    }
+    wheap_push(h, hn, HeapEnt{lp, 0.f, a.row_bfs[0], -1}, lane);
+  }
+
+  while (hn > 0) {
+    const HeapEnt e = wheap_pop(h, hn, lane);
+    ++visited;
+    const bool is_int = e.node >= 0;
+    const int row = is_int ? -1 : -e.node - 1;
+    if (!exact_all) {
+      float b;
+      if (is_int) {
+        b = a.BF[(size_t)q * a.ldI + e.node];
+      } else {
+        const int p = a.row_par[row];
+        b = p >= 0 ? fminf(a.BF[(size_t)q * a.ldI + p], e.score) : e.score;
+      }
+      if (!(b > tau)) {
+        status = 1;
+        break;
+      }
+    }
+    if (visited >= a.max_nodes) break;
+    const bool has_sent = is_int ? a.int_has_sent[e.node] != 0 : (a.row_flags[row] & FLAG_HAS_SENT) != 0;
+    if (has_sent) {
+      if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+      ++found;
+    }
+    if (found == a.k) break;
+    if (is_int) {
+      const int u = e.node;
+      calls += a.int_nchild[u];
+      for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
+        wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c}, lane);
+      if (dense) {
+        for (int pass = 0; pass < 2; ++pass) {
+          const int r0 = pass ? a.int_leaf_b0[u] : a.int_leaf_a0[u];
+          const int r1 = pass ? a.int_leaf_b1[u] : a.int_leaf_a1[u];
+          for (int r = r0; r < r1; ++r)
+            if (!(a.row_flags[r] & FLAG_INT_COPY))
+              wheap_push(h, hn, HeapEnt{a.dense_lpf[(size_t)q * a.ldL + r], e.score, a.row_bfs[r], -(r + 1)}, lane);
+        }
+      } else {
+        // the list rows whose parent is u, in list order
+        uint64_t bm = __ballot(lane < nvalid && lpar_ == u);
+        while (bm) {
+          const int j = __builtin_ctzll(bm);
+          bm &= bm - 1;
+          const int r = __shfl(lrow_, j, 64);
+          wheap_push(h, hn, HeapEnt{__shfl(lsc_, j, 64), e.score, a.row_bfs[r], -(r + 1)}, lane);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    a.n_found[q] = found < a.k ? found : a.k;
+    if (a.n_calls) a.n_calls[q] = calls;
+    a.status[q] = status;
+  }
+}
+
 hipError_t launch_simulate(const SimArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(simulate_kernel, dim3((a.nq + 63) / 64), dim3(64), 0, s, a);
+  const char* e = getenv("CWQ_SIM_BINARY");   // 1: the thread-per-query binary heap
+  if (e && *e && atoi(e) == 1) {
+    hipLaunchKernelGGL(simulate_kernel, dim3((a.nq + 63) / 64), dim3(64), 0, s, a);
+  } else {
+    if (a.R > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(simulate_wave_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -34,12 +34,16 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--clusters", type=int, default=0)
+    ap.add_argument("--balanced", default=None, help="B,L: a depth-L tree of branching B (synth.balanced_synth)")
     ap.add_argument("--rank-queries", type=int, default=64)
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
-    if args.clusters:
+    if args.balanced:
+        b, lv = (int(v) for v in args.balanced.split(","))
+        fs = pkg.synth.balanced_synth(X, b, lv)
+    elif args.clusters:
         g = torch.Generator(device=dev)
         g.manual_seed(7)
         labels = torch.randint(0, args.clusters, (args.n,), generator=g, device=dev)
@@ -51,7 +55,8 @@ def main():
     Q, _ = pkg.synth.synthetic_queries(X, args.queries, seed=1)
     del X
     torch.cuda.empty_cache()
-    tree = f"two-level G={args.clusters}" if args.clusters else "flat"
+    tree = (f"balanced {args.balanced}" if args.balanced else f"two-level G={args.clusters}" if args.clusters
+            else "flat")
     dt, (nodes, found, calls) = timed(lambda: ix.categorize(Q, args.k), args.reps)
     ok = float((found == args.k).float().mean())
     print(f"categorize ({tree}, {args.n}x{args.dim}, k={args.k}): {dt * 1e3:.2f} ms per {args.queries} queries  "

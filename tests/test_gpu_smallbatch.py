@@ -101,3 +101,29 @@ def test_scan_config_independent_of_call_size(gpu):
             assert torch.equal(b[j:j + 1], one[i]), (j, i)
     ix.set_filter(-1)
     ix.close()
+
+
+@pytest.mark.parametrize("tree", ["balanced", "two_level"])
+def test_categorize_replay_wave_vs_binary_heap(gpu, tree, monkeypatch):
+    """The heap replay of the best-first categorize: the wave-per-query 64-ary heap
+    (default) and the thread-per-query binary heap (CWQ_SIM_BINARY=1) pop the same
+    sequence -- retrieved nodes, n_found and log_prob call counts identical, with and
+    without max_nodes cutting the search short, through the filter and the exact scan."""
+    X = gpu.synth.synthetic_corpus(20000, 48, seed=71)
+    if tree == "balanced":
+        t = gpu.synth.balanced_synth(X, 5, 4, seed=72)
+        ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    else:
+        X, ix = two_level(gpu, 20000, 48, 300, 200, seed=73)
+    Q, _ = gpu.synth.synthetic_queries(X, 200, seed=74)
+    for mode in (0, 1):
+        ix.set_filter(mode)
+        for k, mx in ((10, 100000), (3, 50), (20, 1000)):
+            wave = ix.categorize(Q, k, max_nodes=mx)
+            monkeypatch.setenv("CWQ_SIM_BINARY", "1")
+            binary = ix.categorize(Q, k, max_nodes=mx)
+            monkeypatch.delenv("CWQ_SIM_BINARY")
+            for a, b in zip(wave, binary):
+                assert torch.equal(a, b), (mode, k, mx)
+    ix.set_filter(-1)
+    ix.close()
