@@ -6,7 +6,7 @@ GPU (half corpus points + 0.1*N(0,I), half fresh N(0,I); seed 1 + rank), k = 10.
 A step = one libcwq cwq_score_topk call over the batch (scan + path score + top-k
 + merge + sentence ids), inputs resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--preset c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--preset c1|c2|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Multi-GPU (the functions of rag-cobweb_amd/dist.py, covered by tests/test_dist.py on
@@ -48,6 +48,12 @@ def config_label(N, D):
         return "BASELINE configs[2], C3"
     if (N, D) == (10_000_000, 1024):
         return "BASELINE configs[3], C4 per-GPU shard"
+    if (N, D) == (1_500, 384):
+        return "BASELINE configs[0] shape, C1 (synthetic stand-in for the QQP embeddings)"
+    if (N, D) == (100_000, 768):
+        return "BASELINE configs[1] shape, C2 (synthetic stand-in for MS-MARCO 100k)"
+    if (N, D) == (8_800_000, 256):
+        return "BASELINE configs[4] shape, C5 (synthetic stand-in for whitened MS-MARCO 8.8M)"
     return "custom size"
 
 
@@ -127,6 +133,12 @@ PRESETS = {
     "c3": dict(n=1_000_000, dim=768, queries=10_000, strong=False),
     # BASELINE configs[3] (C4): 10M x 1024, 100k queries split over the ranks (strong scaling)
     "c4": dict(n=10_000_000, dim=1024, queries=100_000, strong=True),
+    # the other configs' shapes with N(0,I) stand-ins (no datasets or encoders offline):
+    # C1 QQP 1.5k x 384, 300 queries; C2 MS-MARCO 100k x 768, 1k queries; C5 8.8M x 256
+    # (PCA-whitened MS-MARCO; 10k queries per GPU per step)
+    "c1": dict(n=1_500, dim=384, queries=300, strong=False),
+    "c2": dict(n=100_000, dim=768, queries=1_000, strong=False),
+    "c5": dict(n=8_800_000, dim=256, queries=10_000, strong=False),
 }
 
 

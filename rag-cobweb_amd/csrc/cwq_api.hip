@@ -138,6 +138,7 @@ struct cwq_index {
   std::mutex mu;
   void* ws = nullptr;
   size_t ws_size = 0;
+  size_t ws_budget = 0;   // query-chunk workspace budget, from the free memory at the first call
   hipEvent_t ws_ev = nullptr;
   bool ws_ev_live = false;
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
@@ -916,14 +917,18 @@ int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra, b
   // already held), between 2 and 48 GiB -- one chunk for 10k queries over trees with
   // ~350k internal nodes (whose [lo, hi] prefix matrices alone are 28 GB), which beats two
   // chunks by 11% (balanced 4/9 tree, 1M x 768)
+  // (hipMemGetInfo is a driver query of ~0.3 ms: once per handle, not per call)
   const char* e = getenv("CWQ_WS_BUDGET_MB");
   size_t budget = (size_t)16 << 30;
   if (e && atoll(e) > 0) {
     budget = (size_t)atoll(e) << 20;
+  } else if (ix->ws_budget) {
+    budget = ix->ws_budget;
   } else {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess)
       budget = std::min<size_t>((size_t)48 << 30, std::max<size_t>((size_t)2 << 30, (fr + ix->ws_size) / 5 * 2));
+    const_cast<cwq_index*>(ix)->ws_budget = budget;
   }
   int64_t c = (int64_t)std::max<size_t>(kQPad, budget / std::max<size_t>(per_q, 1));
   c = std::max<int64_t>(kQPad, c / kQPad * kQPad);
@@ -938,14 +943,18 @@ constexpr int kFiltMaxK = 64;         // the filter serves the list-based top-k 
 constexpr int kFgRecPerQ = 512;       // candidate-record slots per query (append buffer)
 constexpr int kFgDirPerQ = 256;       // direct-record slots per query (tiles past kFgCap)
 
-bool use_filter(const cwq_index* ix, int k) {
+// min_rows: the automatic mode's threshold (the batch filter: kFiltMinRows; the per-call
+// stream path pays no batch pipeline and wins from a few hundred rows on -- the exact
+// scan's per-call cost on a 1.5k-row tree is its scalar query-slice latency chain, 0.3 ms)
+constexpr int kStreamMinRows = 512;
+bool use_filter(const cwq_index* ix, int k, int min_rows = kFiltMinRows) {
   if (k > kFiltMaxK || ix->NL_iso == 0 || !ix->iso_Mb) return false;
   int mode = ix->filter;
   if (mode < 0) {
     const char* e = getenv("CWQ_FILTER");
     if (e && *e) mode = atoi(e) ? 1 : 0;
   }
-  if (mode < 0) return ix->NL_iso >= kFiltMinRows;
+  if (mode < 0) return ix->NL_iso >= min_rows;
   return mode == 1;
 }
 
@@ -1369,7 +1378,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                     hipStream_t s, bool allow_filter) {
   const bool general = k > 64;
   const bool filt = !general && allow_filter && use_filter(ix, k);
-  if (filt && use_stream(ix, nq, k)) return stream_topk_impl(ix, q, nq, k, ids, scores, s);
+  if (!general && allow_filter && use_filter(ix, k, kStreamMinRows) && use_stream(ix, nq, k))
+    return stream_topk_impl(ix, q, nq, k, ids, scores, s);
   const int kl = k <= 16 ? 16 : 64;
   const int K = std::min<int>(k, 64);
   const int n_pow2 = (int)std::max<int64_t>(2, 1LL << (int)ceil(log2((double)std::max(ix->NL, 2))));

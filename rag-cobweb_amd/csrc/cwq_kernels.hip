@@ -158,6 +158,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X, 
   }
 
   const int NCH = a.DP / DCH;    // compute chunks
+  const int nvq = __builtin_amdgcn_readfirstlane(min(TQ, a.nq - q0));   // valid queries of this wave (>= 1)
   for (int rt0 = r_begin; rt0 < r_end; rt0 += TILE) {
     const int rt = rt0 + wrow;
     float acc[LPL][TQ];
@@ -190,6 +191,9 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X, 
       for (int v = 0; v < NV; ++v) xa[v] = *reinterpret_cast<const f32x16*>(xgb + boff + v * kXQ * 64);
 #pragma unroll
       for (int qi = 0; qi < TQ; ++qi) {
+        // a partly filled query block (small calls): the padding queries' phases are
+        // skipped -- each one is a scalar-load round trip on the wave's critical path
+        if (qi > 0 && qi >= nvq) continue;
 #pragma unroll
         for (int v = 0; v < NV; ++v) smem_ready(xa[v], boff);
         const int qn = qi + 1 < TQ ? qi + 1 : qi;
