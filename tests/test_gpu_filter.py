@@ -185,6 +185,19 @@ def test_auto_mode_threshold(gpu):
     assert not ix.last_stats()["filter_used"]      # k > 64: exact scan (full ranking path)
 
 
+def test_auto_mode_small_tree(gpu):
+    """Automatic mode on a C1-sized tree (1.5k rows): per-call batches take the stream
+    filter, larger batches the exact scan; the same answers either way."""
+    X = gpu.synth.synthetic_corpus(1500, 384, seed=42)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, 100, seed=43)
+    ids1, s1 = ix.score_topk(Q[:5], 10)
+    assert ix.last_stats()["path"] == "stream"
+    ids2, s2 = ix.score_topk(Q, 10)
+    assert ix.last_stats()["path"] == "scan"
+    assert torch.equal(ids1, ids2[:5]) and torch.equal(s1, s2[:5])
+
+
 @pytest.mark.parametrize("cuts,phases", [("64,256", None), ("8,16,32,64", None), ("1000", None), ("", None),
                                          ("", "0")])
 def test_filter_phase_cuts(gpu, cuts, phases, monkeypatch):
@@ -229,7 +242,8 @@ def test_query_chunking(gpu, filt, monkeypatch):
 
 @pytest.mark.parametrize("N,D,k,nq", [(60000, 768, 10, 1), (60000, 768, 10, 7), (60000, 768, 10, 64),
                                       (40000, 96, 1, 16), (40000, 96, 64, 17), (30000, 1024, 10, 33),
-                                      (30000, 200, 5, 48), (20000, 256, 32, 64)])
+                                      (30000, 200, 5, 48), (20000, 256, 32, 64),
+                                      (600, 384, 10, 1), (1500, 384, 10, 64)])   # small trees (auto: >= 512 rows)
 def test_stream_path_equals_exact_scan(gpu, N, D, k, nq):
     """Small batches (nq <= 64) take the stream filter (cwq_stream.hip): bit-identical to
     the exact scan, with and without the filter's threshold probe finding the targets."""
