@@ -41,22 +41,66 @@ __global__ __launch_bounds__(256) void gemm_nt_f32_kernel(const float* __restric
   const int lr = tid >> 1, lk = (tid & 1) * 8;
   const int64_t am = m0 + lr;
   const int bn = n0 + lr;
-  float ra[8], rb[8];
+  // raw values only: the centring is applied when the registers go to LDS (after the
+  // MFMAs), so the 4 loads of a stage are all in flight at once (computing x - ctr at the
+  // load made the compiler wait for each load in turn: 8 round trips per stage)
+  float4 ra0, ra1, rb0, rb1, rc0, rc1;   // A, B and ctr values of this thread's 8 k
+  const bool vec = (K & 3) == 0;   // 16-B aligned rows
   auto gload = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = k0 + lk + j;
-      const bool kin = k < K;
-      ra[j] = (am < M && kin) ? A[am * K + k] - (ctr ? ctr[k] : 0.f) : 0.f;
-      rb[j] = (bn < N && kin) ? B[(int64_t)bn * K + k] : 0.f;
+    const int kb = k0 + lk;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec && kb + 8 <= K) {
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      auto ld4 = [](const float* p) {
+        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));   // streamed once
+        return make_float4(v[0], v[1], v[2], v[3]);
+      };
+      ra0 = ra1 = rb0 = rb1 = rc0 = rc1 = z;
+      if (am < M) {
+        ra0 = ld4(A + am * K + kb);
+        ra1 = ld4(A + am * K + kb + 4);
+      }
+      if (bn < N) {
+        const v4f* bp = reinterpret_cast<const v4f*>(B + (int64_t)bn * K + kb);
+        const v4f x0 = bp[0], x1 = bp[1];
+        rb0 = make_float4(x0[0], x0[1], x0[2], x0[3]);
+        rb1 = make_float4(x1[0], x1[1], x1[2], x1[3]);
+      }
+      if (ctr) {
+        const v4f* cp = reinterpret_cast<const v4f*>(ctr + kb);
+        const v4f c0 = cp[0], c1 = cp[1];
+        rc0 = make_float4(c0[0], c0[1], c0[2], c0[3]);
+        rc1 = make_float4(c1[0], c1[1], c1[2], c1[3]);
+      }
+    } else {
+      auto ld = [&](const float* base, bool rowok, int k) { return (rowok && k < K) ? base[k] : 0.f; };
+      const float* ar = A + am * K;
+      const float* br = B + (int64_t)bn * K;
+      ra0 = make_float4(ld(ar, am < M, kb), ld(ar, am < M, kb + 1), ld(ar, am < M, kb + 2), ld(ar, am < M, kb + 3));
+      ra1 = make_float4(ld(ar, am < M, kb + 4), ld(ar, am < M, kb + 5), ld(ar, am < M, kb + 6), ld(ar, am < M, kb + 7));
+      rb0 = make_float4(ld(br, bn < N, kb), ld(br, bn < N, kb + 1), ld(br, bn < N, kb + 2), ld(br, bn < N, kb + 3));
+      rb1 = make_float4(ld(br, bn < N, kb + 4), ld(br, bn < N, kb + 5), ld(br, bn < N, kb + 6), ld(br, bn < N, kb + 7));
+      rc0 = ctr ? make_float4(ld(ctr, true, kb), ld(ctr, true, kb + 1), ld(ctr, true, kb + 2), ld(ctr, true, kb + 3)) : z;
+      rc1 = ctr ? make_float4(ld(ctr, true, kb + 4), ld(ctr, true, kb + 5), ld(ctr, true, kb + 6), ld(ctr, true, kb + 7))
+                : z;
     }
   };
-  auto swrite = [&](int b) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      As[b][lk + j][lr] = ra[j];
-      Bs[b][lk + j][lr] = rb[j];
-    }
+  auto swrite = [&](int b, int k0) {
+    // padding (rows past M, k past K) stays exactly 0: x - ctr only where both exist
+    const bool row = am < M;
+    const int kb = k0 + lk;
+    auto put = [&](int j, float av, float cv, float bv) {
+      As[b][lk + j][lr] = (row && kb + j < K) ? av - cv : 0.f;
+      Bs[b][lk + j][lr] = bv;
+    };
+    put(0, ra0.x, rc0.x, rb0.x);
+    put(1, ra0.y, rc0.y, rb0.y);
+    put(2, ra0.z, rc0.z, rb0.z);
+    put(3, ra0.w, rc0.w, rb0.w);
+    put(4, ra1.x, rc1.x, rb1.x);
+    put(5, ra1.y, rc1.y, rb1.y);
+    put(6, ra1.z, rc1.z, rb1.z);
+    put(7, ra1.w, rc1.w, rb1.w);
   };
   f32x16w acc[2][2];
 #pragma unroll
@@ -67,7 +111,7 @@ __global__ __launch_bounds__(256) void gemm_nt_f32_kernel(const float* __restric
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   const int nk = (K + WK - 1) / WK;
   gload(0);
-  swrite(0);
+  swrite(0, 0);
   __syncthreads();
   const int fi = lane & 31, fk = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
@@ -86,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_nt_f32_kernel(const float* __restric
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(b ^ 1);
+    if (kt + 1 < nk) swrite(b ^ 1, (kt + 1) * WK);
     __syncthreads();
   }
   // epilogue: C[i = row m][j = column n]; lane: n = lane&31, m = (e&3) + 8(e>>2) + 4(lane>>5)
