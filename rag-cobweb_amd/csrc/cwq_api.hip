@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -826,14 +827,35 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
 
 IntChain int_chain(const cwq_index* ix) { return IntChain{ix->int_Ar, ix->int_Br, ix->par_int, ix->w_int, ix->logdet_int}; }
 
+// Fast top-K over a small isotropic segment with many queries: the lane-per-query scan
+// (scan_small_kernel).
+bool small_scan_fits(const cwq_index* ix, int K) {   // size limits only (workspace sizing)
+  return ix->NL_iso > 0 && ix->NL_iso <= kSmallScanMaxRows && K <= kSmallScanMaxK;
+}
+bool use_small_scan(const cwq_index* ix, int64_t nq, int K) {
+  if (!small_scan_fits(ix, K) || nq < kSmallScanMinQ) return false;
+  const char* e = getenv("CWQ_SCAN_SMALL");   // 0: never, 1: whenever it applies
+  if (e && *e) return atoi(e) != 0;
+  // by wave counts: the row-sliced scan's slabs are >= 256 rows, so on a small corpus it
+  // has few waves, each waiting on its scalar query loads; the lane-per-query scan wins
+  // with ~0.9x as many waves, or with half as many once it fills the SIMDs
+  // (measured crossover, profiles/r02_small_scan.log)
+  const int nqb = n_qblocks_for(nq, 16);
+  const int64_t nqb_real = (nq + scan_queries_per_block(16) - 1) / scan_queries_per_block(16);
+  const int64_t rs_waves = (int64_t)pick_nslab(ix, ix->NL_iso, nqb) * nqb_real * kWavesPerWG;
+  const int64_t small_waves = (nq + kWave - 1) / kWave * small_scan_slabs(nq, ix->NL_iso);
+  return small_waves * 10 >= rs_waves * 9 || (small_waves * 2 >= rs_waves && small_waves >= 4 * (int64_t)ix->cus);
+}
+
 // One scan over both leaf-row segments.
 // seg_mask: bit 0 = isotropic segment, bit 1 = anisotropic; TOPK lists start at
 // slab_off0 (slots before it are filled by the caller).
 int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
                   float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s,
-                  int seg_mask = 3, int slab_off0 = 0) {
+                  int seg_mask = 3, int slab_off0 = 0, int max_lists = INT_MAX) {
   const int tq = scan_tq(kl);
   const int nqb = n_qblocks_for(c.nq, kl);
+  const bool small = epi == EPI_TOPK && !cat && (seg_mask & 1) && use_small_scan(ix, c.nq, K);
   struct Seg {
     bool iso;
     int n;
@@ -850,12 +872,17 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
     if (segs[i].n == 0) continue;
     const int tile = scan_rows_per_tile(kl);
     const int npad = (int)round_up(segs[i].n, kWave);
+    if (i == 0 && small) {
+      ns[0] = small_scan_slabs(c.nq, segs[0].n);
+      continue;
+    }
     const int n = pick_nslab(ix, segs[i].n, nqb);
     rps[i] = (int)round_up((npad + n - 1) / n, tile);   // slabs hold whole tiles: no row scanned twice
     ns[i] = (npad + rps[i] - 1) / rps[i];
   }
   const int lps = scan_lists_per_slab(kl);
-  const int nslab_total = slab_off0 + (ns[0] + ns[1]) * lps;
+  const int nslab_total = slab_off0 + (small ? ns[0] : ns[0] * lps) + ns[1] * lps;
+  if (nslab_total > max_lists) return CWQ_ERR_ARG;   // internal: the caller's list buffers are too small
   if (nslab_total_out) *nslab_total_out = nslab_total;
   int slab_off = slab_off0;
   for (int i = 0; i < 2; ++i) {
@@ -880,6 +907,11 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
     a.nslab_total = nslab_total;
     a.slab_off = slab_off;
     a.K = K;
+    if (i == 0 && small) {
+      HIPCHK(launch_scan_small(c.X, segs[0].A, a, ns[0], s));
+      slab_off += ns[0];
+      continue;
+    }
     HIPCHK(launch_scan(segs[i].iso, epi, cat, kl, c.X, segs[i].A, segs[i].B, a, ns[i], s));
     slab_off += ns[i] * lps;
   }
@@ -1181,7 +1213,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   HIPCHK(launch_stream(a, 0, ix->cus, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
   int nst = 0;
-  if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1))) return rc;
+  if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1, slabs)))
+    return rc;
   const IntChain chain = int_chain(ix);
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
@@ -1386,8 +1419,11 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   // partial-list entries per query (upper bound over both segments; one list for the filter)
   const int nqb_est = n_qblocks_for(nq, kl);
   auto n_slabs = [&](int nqb) {
+    // a chunk may take either scan (use_small_scan on its own query count): room for both
+    // (small_scan_slabs(1, n) is its largest slab count)
+    const int n_iso = std::max(pick_nslab(ix, ix->NL_iso, nqb), small_scan_fits(ix, K) ? small_scan_slabs(1, ix->NL_iso) : 0);
     return filt ? 1 + (pick_nslab(ix, ix->NL_an, nqb) + 1) * scan_lists_per_slab(kl)
-                : (pick_nslab(ix, ix->NL_iso, nqb) + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
+                : (n_iso + pick_nslab(ix, ix->NL_an, nqb) + 2) * scan_lists_per_slab(kl);
   };
   const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
   const int n_rts = filt ? ix->ld_s / kFgTile : 0;
@@ -1446,7 +1482,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         int* crow = fo.crow;
         float* cu = fo.cu;
         float* cl = fo.cl;
-        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1)))
+        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1, slabs)))
           return rc;
         const IntChain chain = int_chain(ix);
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
@@ -1456,7 +1492,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         nex_d = nex;
         if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
       } else {
-        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s)))
+        if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 3, 0, slabs)))
           return rc;
       }
       if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
@@ -1681,7 +1717,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       // anisotropic rows: the exact scan into slots 1..
       IsoFilter fo;
       if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, R, true, false, b, fo, s))) return rc;
-      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 2, 1)))
+      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 2, 1, slabs)))
         return rc;
       HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, kFgCapQ, fo.qcnt, fo.qover, fo.crow, fo.cu, fo.cl,
                           fo.tl + (R - 1), 64, ix->row_meta, ix->row_par, c.BF ? c.BF : ix->dummy, std::max(ix->NI, 1), 0,
@@ -1695,7 +1731,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           fbad[i] = 1;
           fredo.push_back(q0 + i);
         }
-    } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s))) {
+    } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 3, 0, slabs))) {
       return rc;
     }
     HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s));

@@ -109,6 +109,17 @@ int scan_lists_per_slab(int kl);     // partial top-k lists a workgroup writes p
 int scan_xcd_map();                  // XCD-aware block mapping (CWQ_XCD_MAP, default 1)
 int scan_wgs_per_cu(int kl);         // resident workgroups per CU (occupancy query, cached)
 
+// Small-corpus exact scan (isotropic rows, fast top-K lists of K <= 16): lane = query,
+// blocks of 16 or 32 rows staged in LDS.  For segments of at most kSmallScanMaxRows rows
+// with many queries, where the row-sliced scan has few waves (few slabs per query block)
+// and waits on its scalar query loads.  Writes one list per slab, like the scan
+// (a.slab_off, a.nslab_total).
+constexpr int kSmallScanMaxRows = 16384;  // segment size limit (lists per query <= 128)
+constexpr int kSmallScanMinQ = 64;        // one full wave of queries
+constexpr int kSmallScanMaxK = 16;
+int small_scan_slabs(int64_t nq, int nrows);   // slab count (= lists per query)
+hipError_t launch_scan_small(const float* X, const float* M, const ScanArgs& a, int nslab, hipStream_t s);
+
 hipError_t launch_int_small(const float* X, const float* A, const float* B, int64_t ld, int NI, int DP, int nq,
                             float* out, int64_t ldo, hipStream_t s);
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,

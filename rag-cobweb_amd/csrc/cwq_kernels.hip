@@ -414,6 +414,234 @@ hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, cons
 }
 
 // ---------------------------------------------------------------------------
+// Small-corpus scan (isotropic rows, fast keys, top-K lists): lane = query.
+// The row-sliced scan above splits the rows into slabs of >= 256 rows and gives each
+// wave 16 queries whose slices arrive one scalar load per compute phase; on a corpus of
+// a few thousand rows that is a few slabs per query block, one wave per SIMD, and every
+// phase waits on its load (C1, 1.5k x 384 rows, 300 queries: 0.47 ms).  Here a wave
+// owns 64 queries (one per lane, the 16-dim query slice in VGPRs, loaded once per
+// slice), the workgroup's waves share a block of 16 or 32 rows staged in LDS
+// dim-major ([dim][row]: one ds_read_b128 broadcasts 4 rows' value of a dimension to
+// all lanes), 2 VALU ops per (query, row, dim) as in the scan and in the same order per
+// row: 16-dim fma partials (t = x - mu, part = t*t, then fmaf(t, t, part)), added to the
+// row's sum slice by slice.  Each lane keeps its query's top-16 of the slab in
+// registers (key desc, row asc; the scan's order) and writes the first K.
+// Grid: (slab, query group); block = 64 * W threads (W waves = W * 64 queries).
+// ---------------------------------------------------------------------------
+// Global loads of one LDS stage (CH dims x R rows at row rb, dim stg * CH) into registers:
+// element i = tid + it * nthr of the stage's [dim][row/4] float4 array, it < 4.  Named
+// registers, not an array: a private array live across the stage loop's back edge is
+// promoted to LDS by the compiler.
+struct Pre4 {
+  float4 v0, v1, v2, v3;
+  float4 md;   // stage 0 only: row metadata of row tid < R of the block
+  int par, fl;
+};
+template <int R, int CH>
+__device__ __forceinline__ void small_fetch(Pre4& p, const float* __restrict__ M, int64_t ld, int DP, int rb, int stg,
+                                            int tid, int nthr, const RowMeta* __restrict__ meta,
+                                            const int* __restrict__ par, const int* __restrict__ flags, int nrows) {
+  const int d0 = stg * CH, n4 = min(CH, DP - d0) * (R / 4);
+  auto ld4 = [&](int it) {
+    const int i = tid + it * nthr;
+    const int ic = i < n4 ? i : 0;   // clamped: a valid address; the copy to LDS skips it
+    return *reinterpret_cast<const float4*>(M + (size_t)(d0 + ic / (R / 4)) * ld + rb + (ic % (R / 4)) * 4);
+  };
+  p.v0 = ld4(0);
+  p.v1 = ld4(1);
+  p.v2 = ld4(2);
+  p.v3 = ld4(3);
+  if (stg == 0 && tid < R) {
+    const int r = min(rb + tid, nrows - 1);
+    p.md = reinterpret_cast<const float4*>(meta)[r];
+    p.par = par[r];
+    p.fl = rb + tid < nrows ? flags[r] : 0;
+  }
+}
+
+// WMIN: the launch has >= WMIN waves per workgroup; KM: list slots per lane (>= K)
+template <int R, int WMIN, int KM>
+__global__ __launch_bounds__(512) void scan_small_kernel(const float* __restrict__ X, const float* __restrict__ M,
+                                                         const ScanArgs a) {
+  constexpr int CH = 64;   // dims per LDS stage
+  __shared__ float4 sm4[CH * R / 4];   // [dim][row]
+  __shared__ float4 s_md[R];           // the block's row metadata, parents, flags
+  __shared__ int s_par[R], s_fl[R];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthr = blockDim.x;
+  const int q = (blockIdx.y * (nthr >> 6) + wave) * kWave + lane;
+  const int qq = min(q, a.nq - 1);   // lanes past the last query compute on a valid one
+  const int NV16 = a.DP / 16;
+  const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(qq / kXQ) * NV16 * kXQ + (qq % kXQ);
+
+  float lk[KM], la[KM];
+  int lr[KM];
+#pragma clang loop unroll(full)
+  for (int i = 0; i < KM; ++i) {
+    lk[i] = -CWQ_INF;
+    la[i] = 0.f;
+    lr[i] = 0x7fffffff;
+  }
+  const int r_begin = blockIdx.x * a.rows_per_slab;
+  const int r_end = min(r_begin + a.rows_per_slab, a.nrows);
+  // LDS stages of CH dims x R rows; the next stage's global loads are issued (all at
+  // once, into registers) before the current stage is computed, so they fly under it
+  static_assert(CH * R / 4 <= 4 * kWave * WMIN, "a stage is at most 4 float4 loads per thread");
+  const int nst = (a.DP + CH - 1) / CH;
+  Pre4 pre;
+  f32x16 xq = xg[0];
+  int lastp = -2;   // parent prefix cache: rows of a block mostly share their parent
+  float ppc = 0.f;
+  if (r_begin < r_end) small_fetch<R, CH>(pre, M, a.ld, a.DP, r_begin, 0, tid, nthr, a.meta, a.par, a.flags, a.nrows);
+  for (int r0 = r_begin; r0 < r_end; r0 += R) {
+    float acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = 0.f;
+    for (int stg = 0; stg < nst; ++stg) {
+      const int d0 = stg * CH, nd = min(CH, a.DP - d0);
+      __syncthreads();   // the previous stage's reads are done
+      {
+        const int n4 = nd * (R / 4);
+        if (tid < n4) sm4[tid] = pre.v0;
+        if (tid + nthr < n4) sm4[tid + nthr] = pre.v1;
+        if (tid + 2 * nthr < n4) sm4[tid + 2 * nthr] = pre.v2;
+        if (tid + 3 * nthr < n4) sm4[tid + 3 * nthr] = pre.v3;
+        if (stg == 0 && tid < R) {
+          s_md[tid] = pre.md;
+          s_par[tid] = pre.par;
+          s_fl[tid] = pre.fl;
+        }
+      }
+      __syncthreads();
+      {
+        const bool last = stg + 1 == nst;
+        const int nr = last ? r0 + R : r0;
+        if (nr < r_end) small_fetch<R, CH>(pre, M, a.ld, a.DP, nr, last ? 0 : stg + 1, tid, nthr, a.meta, a.par, a.flags,
+                                            a.nrows);
+      }
+      for (int c = 0; c < nd / 16; ++c) {
+        // the next query slice (wrapping to the next block's first) flies under this one
+        const int gn = d0 / 16 + c + 1 < NV16 ? d0 / 16 + c + 1 : 0;
+        const f32x16 xn = xg[(size_t)gn * kXQ];
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+          float p0, p1, p2, p3;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float4 m = sm4[(c * 16 + j) * (R / 4) + g];
+            const float t0 = xq[j] - m.x, t1 = xq[j] - m.y, t2 = xq[j] - m.z, t3 = xq[j] - m.w;
+            p0 = (j == 0) ? t0 * t0 : fmaf(t0, t0, p0);
+            p1 = (j == 0) ? t1 * t1 : fmaf(t1, t1, p1);
+            p2 = (j == 0) ? t2 * t2 : fmaf(t2, t2, p2);
+            p3 = (j == 0) ? t3 * t3 : fmaf(t3, t3, p3);
+          }
+          acc[g * 4 + 0] += p0;
+          acc[g * 4 + 1] += p1;
+          acc[g * 4 + 2] += p2;
+          acc[g * 4 + 3] += p3;
+        }
+        xq = xn;
+      }
+    }
+    // epilogue: the scan's key arithmetic, then insertion into the lane's list (fully
+    // unrolled: acc[] must stay in registers)
+#pragma clang loop unroll(full)
+    for (int i = 0; i < R; ++i) {
+      const int row = r0 + i;
+      if (row < a.nrows) {   // wave-uniform
+        const float4 m4 = s_md[i];
+        const RowMeta md{m4.x, m4.y, m4.z, m4.w};
+        const int p = __builtin_amdgcn_readfirstlane(s_par[i]);
+        const int fl = __builtin_amdgcn_readfirstlane(s_fl[i]);
+        if (fl & FLAG_HAS_SENT) {
+          const float S = md.iv * acc[i];
+          const float lp = -0.5f * (md.logdet + a.dconst + S);
+          if (p != lastp) {
+            ppc = p >= 0 ? a.P[(size_t)qq * a.ldP + p] : 0.f;
+            lastp = p;
+          }
+          const float pp = ppc;
+          float ck = fmaf(pp, md.invL, md.cw * lp);
+          float ca = lp;
+          int cr = a.seg_base + row;
+#pragma clang loop unroll(full)
+          for (int s = 0; s < KM; ++s) {   // bubble the candidate down the sorted list
+            const bool b = ck > lk[s] || (ck == lk[s] && cr < lr[s]);
+            const float tk = b ? lk[s] : ck, ta = b ? la[s] : ca;
+            const int tr = b ? lr[s] : cr;
+            lk[s] = b ? ck : lk[s];
+            la[s] = b ? ca : la[s];
+            lr[s] = b ? cr : lr[s];
+            ck = tk;
+            ca = ta;
+            cr = tr;
+          }
+        }
+      }
+    }
+  }
+  if (q < a.nq) {
+    const size_t o = ((size_t)q * a.nslab_total + a.slab_off + blockIdx.x) * a.K;
+#pragma clang loop unroll(full)
+    for (int s = 0; s < KM; ++s)
+      if (s < a.K) {
+        a.pkey[o + s] = lk[s];
+        a.paux[o + s] = la[s];
+        a.prow[o + s] = lr[s];
+      }
+  }
+}
+
+// Row block per register pass: 16 rows (more slabs, more waves), 32 only for calls with
+// plenty of (query group, block) pairs (in-process A/B over 1.5k-16k rows, 64-3000
+// queries: 16 is faster or within 7%).
+static int small_scan_rows(int64_t nq, int nrows) {
+  if (const char* e = getenv("CWQ_SMALL_R")) {   // A/B: force 16 or 32
+    const int r = atoi(e);
+    if (r == 16 || r == 32) return r;
+  }
+  const int64_t groups = (nq + kWave - 1) / kWave;
+  const int64_t b32 = std::min<int64_t>(128, (nrows + 31) / 32);
+  return groups * b32 >= 8192 ? 32 : 16;
+}
+
+int small_scan_slabs(int64_t nq, int nrows) {
+  const int64_t groups = (nq + kWave - 1) / kWave;
+  const int R = small_scan_rows(nq, nrows);
+  const int blocks = (nrows + R - 1) / R;
+  const int64_t want = (2048 + groups - 1) / groups;   // ~2 waves per SIMD
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, std::min(128, blocks)));
+}
+
+hipError_t launch_scan_small(const float* X, const float* M, const ScanArgs& a0, int nslab, hipStream_t s) {
+  if (a0.K > kSmallScanMaxK || a0.K < 1 || a0.nq < 1 || (a0.ld & 3) || a0.DP % 16) return hipErrorInvalidValue;
+  ScanArgs a = a0;
+  const int R = small_scan_rows(a.nq, a.nrows);
+  const int blocks = (a.nrows + R - 1) / R;
+  a.rows_per_slab = (blocks + nslab - 1) / nslab * R;
+  // every staged row block lies inside the array: r0 + R <= round_up(nrows, 64) <= ld
+  if ((int64_t)(a.nrows + kWave - 1) / kWave * kWave > a.ld) return hipErrorInvalidValue;
+  const int groups = (a.nq + kWave - 1) / kWave;
+  // waves per workgroup (query groups sharing a staged row block): up to 8, but keep
+  // >= 512 workgroups when the call is small (spread over the CUs' LDS units)
+  int W = std::min(8, groups);
+  while (W > 1 && (int64_t)nslab * ((groups + W - 1) / W) < 512) W = (W + 1) / 2;
+  if (R == 32) W = std::max(W, 2);   // the 32-row form's prefetch registers assume >= 2 waves
+  const int qwg = (groups + W - 1) / W;
+  const dim3 grid((unsigned)nslab, (unsigned)qwg), block(64 * W);
+  const bool k10 = a.K <= 10;   // the default k: 10 list slots per lane instead of 16
+  if (R == 32 && k10)
+    hipLaunchKernelGGL((scan_small_kernel<32, 2, 10>), grid, block, 0, s, X, M, a);
+  else if (R == 32)
+    hipLaunchKernelGGL((scan_small_kernel<32, 2, 16>), grid, block, 0, s, X, M, a);
+  else if (k10)
+    hipLaunchKernelGGL((scan_small_kernel<16, 1, 10>), grid, block, 0, s, X, M, a);
+  else
+    hipLaunchKernelGGL((scan_small_kernel<16, 1, 16>), grid, block, 0, s, X, M, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Merge the per-slab partial lists of one query into its global top-K (K <= 64).
 // One wave per query; the list lives in the wave's 64 lanes.
 // ---------------------------------------------------------------------------

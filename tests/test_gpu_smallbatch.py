@@ -127,3 +127,36 @@ def test_categorize_replay_wave_vs_binary_heap(gpu, tree, monkeypatch):
                 assert torch.equal(a, b), (mode, k, mx)
     ix.set_filter(-1)
     ix.close()
+
+
+def _dup_rows(X, n_dup, seed):
+    """Copies of random corpus rows (exact key ties between distinct rows)."""
+    g = torch.Generator(device=X.device).manual_seed(seed)
+    src = torch.randint(0, X.shape[0], (n_dup,), device=X.device, generator=g)
+    return torch.cat([X, X[src]], 0)
+
+
+@pytest.mark.parametrize("shape", [(1500, 384, "flat"), (5000, 128, "two_level"), (16000, 96, "flat"),
+                                   (3000, 64, "aniso")])
+def test_small_scan_vs_row_sliced_scan(gpu, shape, monkeypatch):
+    """The lane-per-query scan of small isotropic segments (scan_small_kernel) against the
+    row-sliced scan (CWQ_SCAN_SMALL=0): ids and scores bit for bit, k = 1 / 10 / 16 and the
+    list-64 form (k = 20, which keeps the row-sliced scan), 64 ... 1000 queries."""
+    N, D, kind = shape
+    X = gpu.synth.synthetic_corpus(N, D, seed=61)
+    if kind == "flat":
+        X = _dup_rows(X, 64, seed=62)
+        fs = gpu.synth.flat_synth(X)
+        ix = gpu.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device="cuda:0")
+    else:   # hierarchical (parent prefixes in the keys); "aniso": both leaf segments
+        X, ix = two_level(gpu, N, D, 40, 200 if kind == "aniso" else 0, seed=63)
+    Q, _ = gpu.synth.synthetic_queries(X, 1000, seed=64)
+    for nq in (64, 100, 300, 1000):
+        for k in (1, 10, 16, 20):
+            got = run(ix, Q[:nq], k, 0)
+            monkeypatch.setenv("CWQ_SCAN_SMALL", "0")
+            ref = run(ix, Q[:nq], k, 0)
+            monkeypatch.delenv("CWQ_SCAN_SMALL")
+            assert torch.equal(got[0], ref[0]), (nq, k)
+            assert torch.equal(got[1], ref[1]), (nq, k)
+    ix.close()
