@@ -201,6 +201,8 @@ def main():
     ap.add_argument("--no-per-call", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r02_fgemm.json"))
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="rehearsal only: gloo lets several ranks share one GPU (RCCL refuses that)")
     args = ap.parse_args()
     pre = PRESETS[args.preset]
     N = args.n or pre["n"]
@@ -214,10 +216,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.dist_backend == "gloo":   # rehearsal of the N-rank path on fewer GPUs
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     pkg = cobweb_pkg.load()
     pkg.lib()
     D_ = pkg.dist

@@ -1027,8 +1027,16 @@ int fg_order() {   // default: dynamic per-XCD tile claims (measured fastest)
   return e && *e ? atoi(e) : 2;
 }
 
+// XCD split of the tiles: qg query groups x rg row groups (qg * rg = 8).  Default: all 8
+// XCDs split the queries (each keeps its query panels in its L2 and streams every row
+// panel); CWQ_FG_QG = 4 / 2 / 1 caps qg (row panels fetched by fewer XCDs, more query
+// panels per XCD).
 void fg_groups(int n_qt, int& qg, int& rg) {
   qg = n_qt >= 8 ? 8 : n_qt >= 4 ? 4 : n_qt >= 2 ? 2 : 1;
+  if (const char* e = getenv("CWQ_FG_QG")) {
+    const int v = atoi(e);
+    if ((v == 1 || v == 2 || v == 4) && v < qg) qg = v;
+  }
   rg = 8 / qg;
 }
 
