@@ -347,7 +347,7 @@ def main():
                                     f"{Qarg} queries/step/GPU") + f" ({config_label(N, D)})",
                        "preset": args.preset, "corpus": N, "dim": D, "queries_per_step": total_q,
                        "queries_per_gpu": nql, "k": k, "tree": "flat-synth",
-                       "parallelism": f"query-shard x{world}, index broadcast over RCCL" if world > 1
+                       "parallelism": f"query-shard x{world}, index broadcast over " + ("RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)") if world > 1
                        else "single GPU"},
             "roofline": {"bound": "mfma", "pipe": pipe,
                          "achieved": round(achieved_tf, 2), "peak": peak, "unit": "TFLOP/s",

@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.." || exit 1
 LLVM=/opt/rocm/lib/llvm/bin
 tmp=$(mktemp -d)
-for o in rag-cobweb_amd/build/*.o; do
+for o in ${BUILD_DIR:-rag-cobweb_amd/build}/*.o; do
   $LLVM/llvm-objcopy --dump-section=.hip_fatbin=$tmp/fb.bin "$o" 2>/dev/null || continue
   $LLVM/clang-offload-bundler --unbundle --type=o --input=$tmp/fb.bin --targets=hipv4-amdgcn-amd-amdhsa--gfx950 \
     --output=$tmp/k.co 2>/dev/null || continue
