@@ -219,7 +219,9 @@ struct cwq_index {
     if (hflags) (void)hipHostFree(hflags);
     hflags = nullptr;
     hflags_n = 0;
-    if (hipHostMalloc((void**)&hflags, n * sizeof(int), hipHostMallocDefault) != hipSuccess)
+    // coherent (fine-grained) host memory: final_wide_kernel writes the flags of the
+    // per-call path straight into it; the batch paths copy into it
+    if (hipHostMalloc((void**)&hflags, n * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return fail(CWQ_ERR_OOM, "hipHostMalloc failed");
     hflags_n = n;
     return CWQ_OK;
@@ -1224,14 +1226,20 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1, slabs)))
     return rc;
   const IntChain chain = int_chain(ix);
+  if ((rc = ix->host_flags((size_t)3 * nqc))) return rc;
+  // one candidate list per query (no anisotropic rows): final_wide expands the top-K to
+  // sentence ids and writes the host flags itself (no merge launch, no flag copy)
+  const bool ftail = nst == 1 && final_wide_lds(ix->DP, capq) <= 65536 && !getenv("CWQ_FW_UNFUSED");
+  const FwExpand fx{ix->sent_ptr, ix->sent_ids, ids, scores, k, ix->hflags};
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
-                      nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s));
+                      nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s, ftail ? &fx : nullptr));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
-  HIPCHK(launch_merge_expand(pkey, paux, prow, nqc, nst * K, K, k, ix->sent_ptr, ix->sent_ids, ids, scores, s));
-  if ((rc = ix->host_flags((size_t)3 * nqc))) return rc;
-  HIPCHK(hipMemcpyAsync(ix->hflags, qcnt, (size_t)3 * nqc * 4, hipMemcpyDeviceToHost, s));
+  if (!ftail) {
+    HIPCHK(launch_merge_expand(pkey, paux, prow, nqc, nst * K, K, k, ix->sent_ptr, ix->sent_ids, ids, scores, s));
+    HIPCHK(hipMemcpyAsync(ix->hflags, qcnt, (size_t)3 * nqc * 4, hipMemcpyDeviceToHost, s));
+  }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[3], s));
   HIPCHK(hipStreamSynchronize(s));
   std::vector<int64_t> redo;

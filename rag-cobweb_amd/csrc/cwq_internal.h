@@ -339,12 +339,24 @@ hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill
 // (the filter's record and tile-claim counters for the next launch)
 hipError_t launch_tighten(int nq, int K, int capq, const int* qcnt, const int* qover, const float* cl, float* T,
                           int64_t ldT, float* lkb, int* lrb, int* done, int* zero16, hipStream_t s);
+// Fused tail of the per-call path (final_wide_kernel, one candidate list per query): the
+// top-K rows expanded to sentence ids into ids/scores (merge_expand_kernel's work) and the
+// per-query {candidates, ok, exact reranks} written to hflags[0..3nq) (host-mapped).
+struct FwExpand {
+  const int64_t* sent_ptr;
+  const int64_t* sent_ids;
+  int64_t* ids;
+  float* scores;
+  int k;
+  int* hflags;
+};
+size_t final_wide_lds(int DP, int capq);   // dynamic LDS of final_wide_kernel (<= 64 KiB to run)
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
                         const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
-                        float dconst, hipStream_t s);
+                        float dconst, hipStream_t s, const FwExpand* fx = nullptr);
 
 // PCA + ICA whitening (cwq_whiten.hip): C[m][n] = sum_k (A[m][k] - ctr[k]) B[n][k] (/ denom[n])
 hipError_t launch_gemm_nt_f32(const float* A, int64_t M, int K, const float* ctr, const float* B, int N,

@@ -1503,6 +1503,10 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
 // then lane s of wave 0 adds survivor s's partials in slice order (acc += part, as the
 // scan does), so the keys are bit-identical; the per-lane form pays one row's dependent
 // load chain per round (~33 us of a 1-query call at C3).
+// Memory round trips are the cost at one query per call, so the query's counters and the
+// first kFwThreads entries of its candidate lists arrive in ONE round (loaded before the
+// count is known; entries past it are never used), and the survivors' row terms fly with
+// their partials' row loads.  fx (optional): the fused expansion + host flags (FwExpand).
 constexpr int kFwThreads = 512;
 __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const float* __restrict__ X, const float* __restrict__ Mf, int DP, int nq, int K, int capq,
@@ -1511,35 +1515,46 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const RowMeta* __restrict__ meta, const int* __restrict__ par, const float* __restrict__ P, int64_t ldP,
     int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
     const float* __restrict__ lkb, const int* __restrict__ lrb, const int* __restrict__ done, const IntChain chain,
-    int use_chain, int cat, float dconst) {
+    int use_chain, int cat, float dconst, const FwExpand fx) {
   extern __shared__ float s_dyn[];
   const int NV16 = DP / 16, LDP = NV16 + 1;                  // odd row pitch: conflict-free column reads
   float* s_part = s_dyn;                                      // [64][LDP]
   int* s_surv = reinterpret_cast<int*>(s_dyn + 64 * LDP);    // [capq] survivor positions
+  __shared__ float s_wl[kFwThreads], s_wu[kFwThreads];        // candidates 0..kFwThreads-1: l, u, row
+  __shared__ int s_wr[kFwThreads];
   __shared__ int s_rr[64];
   __shared__ int s_ns;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
+  const size_t base = (size_t)q * capq;
+  // ---- one round trip: counters + the first window of the candidate lists ----
   const int n = qcnt[q];
   const float Tq = T[(size_t)q * ldT];
-  const bool ok = qover[q] == 0 && n >= K && n <= capq && Tq > -CWQ_INF;   // uniform over the block
+  const int ov = qover[q];
+  const int d = done[q];
+  if (tid < capq) {
+    s_wl[tid] = cl[base + tid];
+    s_wu[tid] = cu[base + tid];
+    s_wr[tid] = crow[base + tid];
+  }
+  const bool ok = ov == 0 && n >= K && n <= capq && Tq > -CWQ_INF;   // uniform over the block
   float lk = -CWQ_INF, la = 0.f;
   int lr = 0x7fffffff, nx = 0;
-  const size_t base = (size_t)q * capq;
+  __syncthreads();
   if (ok) {
     if (wave == 0) {
-      const int d = done[q];
       float tk = d ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
       int tr = d ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
       for (int j0 = d; j0 < n; j0 += 64) {
         const int j = j0 + lane;
-        list64_offer(tk, tr, lane, j < n ? cl[base + j] : -CWQ_INF, j, K);
+        const float lv = j >= n ? -CWQ_INF : j < kFwThreads ? s_wl[j] : cl[base + j];
+        list64_offer(tk, tr, lane, lv, j, K);
       }
       const float T2 = rl_f2(tk, K - 1);
       int ns = 0;
       for (int j0 = 0; j0 < n; j0 += 64) {
         const int j = j0 + lane;
-        const bool c = j < n && cu[base + j] >= T2;
+        const bool c = j < n && (j < kFwThreads ? s_wu[j] : cu[base + j]) >= T2;
         const uint64_t bm = __ballot(c);
         if (c) s_surv[ns + __popcll(bm & ((1ull << lane) - 1))] = j;
         ns += __popcll(bm);
@@ -1551,18 +1566,19 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
     for (int r0 = 0; r0 < ns; r0 += 64) {
       const int cnt = min(64, ns - r0);
-      RowMeta md;
-      float pp = 0.f;
-      int rr = 0;
       if (wave == 0 && lane < cnt) {
-        rr = crow[base + s_surv[r0 + lane]];
-        md = meta[rr];
-        const int p = par[rr];
-        pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);
-        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
-        s_rr[lane] = rr;
+        const int j = s_surv[r0 + lane];
+        s_rr[lane] = j < kFwThreads ? s_wr[j] : crow[base + j];
       }
       __syncthreads();   // s_rr visible; the previous round's partials consumed
+      // the survivors' row terms (wave 0), in flight with the partials' row loads
+      RowMeta md;
+      int p = -1, rr = 0;
+      if (wave == 0 && lane < cnt) {
+        rr = s_rr[lane];
+        md = meta[rr];
+        p = par[rr];
+      }
       for (int t = tid; t < cnt * NV16; t += kFwThreads) {
         const int sv = t / NV16, v = t - sv * NV16;
         const float* __restrict__ mr = Mf + (size_t)s_rr[sv] * DP + v * 16;
@@ -1579,6 +1595,11 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
         }
         s_part[sv * LDP + v] = part;
+      }
+      float pp = 0.f;
+      if (wave == 0 && lane < cnt) {
+        pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);
+        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
       }
       __syncthreads();
       if (wave == 0) {
@@ -1630,13 +1651,51 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     }
   }
   if (wave != 0) return;
+  for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
+  if (fx.ids) {
+    // merge_expand_kernel's expansion of the (already sorted) top-K rows, in place
+    if (!ok) {
+      lk = -CWQ_INF;
+      lr = 0x7fffffff;
+    }
+    const bool valid = lane < K && lk != -CWQ_INF && lr != 0x7fffffff;
+    const uint64_t vm = __ballot(valid);
+    const int nvalid = (~vm) ? __builtin_ctzll(~vm) : 64;
+    int64_t s0 = 0;
+    int cnt = 0;
+    if (lane < nvalid) {
+      s0 = fx.sent_ptr[lr];
+      cnt = (int)(fx.sent_ptr[lr + 1] - s0);
+    }
+    int off = cnt;   // inclusive scan
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const int o = __shfl_up(off, dd, 64);
+      if (lane >= dd) off += o;
+    }
+    const int total = __shfl(off, 63, 64);
+    off -= cnt;
+    const int k = fx.k;
+    for (int j = 0; j < cnt && off + j < k; ++j) {
+      fx.ids[(size_t)q * k + off + j] = fx.sent_ids[s0 + j];
+      if (fx.scores) fx.scores[(size_t)q * k + off + j] = lk;
+    }
+    for (int t = total + lane; t < k; t += kWave) {
+      fx.ids[(size_t)q * k + t] = -1;
+      if (fx.scores) fx.scores[(size_t)q * k + t] = -CWQ_INF;
+    }
+    if (lane == 0) {
+      fx.hflags[q] = n;
+      fx.hflags[nq + q] = ok ? 1 : 0;
+      fx.hflags[2 * nq + q] = nx;
+    }
+    return;
+  }
   if (lane < K) {
     const size_t o = (size_t)q * lstride + lane;
     pkey[o] = ok ? lk : -CWQ_INF;
     paux[o] = la;
     prow[o] = ok ? lr : 0x7fffffff;
   }
-  for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
   if (lane == 0) {
     ok_flag[q] = ok ? 1 : 0;
     if (n_exact) n_exact[q] = nx;
@@ -1650,17 +1709,19 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,
                         float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
                         const float* lkb, const int* lrb, const int* done, const IntChain* chain, int cat,
-                        float dconst, hipStream_t s) {
+                        float dconst, hipStream_t s, const FwExpand* fx) {
   const IntChain ch = chain ? *chain : IntChain{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const FwExpand fe = fx ? *fx : FwExpand{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
   const char* we = getenv("CWQ_FINAL_WIDE");   // largest nq for the workgroup-per-query form
   const int wide_max = we && *we ? atoi(we) : kFinalWideMaxQ;
   const size_t lds = final_wide_lds(DP, capq);
-  if (nq <= wide_max && lds <= 65536) {
+  if ((fx || nq <= wide_max) && lds <= 65536) {
     hipLaunchKernelGGL(final_wide_kernel, dim3((unsigned)nq), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
                        qover, crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag,
-                       n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst);
+                       n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst, fe);
     return hipGetLastError();
   }
+  if (fx) return hipErrorInvalidValue;   // the fused tail exists in the workgroup-per-query form only
   hipLaunchKernelGGL(final_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, capq, qcnt, qover,
                      crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag, n_exact,
                      lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst);

@@ -19,7 +19,7 @@ import cobweb_pkg  # noqa: E402
 
 def parse(v):
     env = {}
-    for item in v.split(","):
+    for item in v.split("&"):
         item = item.strip()
         if item:
             key, val = item.split("=", 1)
@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", required=True, help="';'-separated variants of ','-separated KEY=VAL")
+    ap.add_argument("--variants", required=True, help="';'-separated variants of '&'-separated KEY=VAL")
     args = ap.parse_args()
     variants = [parse(v) for v in args.variants.split(";")]
     keys = sorted({k for v in variants for k in v})
