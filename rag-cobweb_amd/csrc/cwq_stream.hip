@@ -51,21 +51,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int SK_WAVES = 8;
 constexpr int SK_MAXQB = kStreamMaxQ / 16;   // query blocks of 16
 constexpr int SK_CH = 8;                     // K fragments per chunk (8 x 32 = 256 dims)
-#ifndef SK_NT
-#define SK_NT 0   // row panel read with non-temporal loads (each row is read once per call)
-#endif
-
-// one 16-B panel fragment
-__device__ __forceinline__ bf16x8 panel_load(const char* p) {
-#if SK_NT
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 v = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
-  return __builtin_bit_cast(bf16x8, v);
-#else
-  return *reinterpret_cast<const bf16x8*>(p);
-#endif
-}
-
 // float <-> int order-preserving map for atomicMax on floats
 __device__ __forceinline__ int f2ord(float f) {
   const int i = __float_as_int(f);
@@ -145,7 +130,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     const char* src = panel(gi);
 #pragma unroll
     for (int i = 0; i < SK_CH; ++i)
-      if (i < nk) cur[i] = panel_load(src + i * 64);
+      if (i < nk) cur[i] = *reinterpret_cast<const bf16x8*>(src + i * 64);
     if (PRE_RF) load_rf(gi);
   }
   int it = 0;
@@ -172,11 +157,11 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       if (c0 + SK_CH < nk) {
 #pragma unroll
         for (int i = 0; i < SK_CH; ++i)
-          if (c0 + SK_CH + i < nk) nxt[i] = panel_load(src + (c0 + SK_CH + i) * 64);
+          if (c0 + SK_CH + i < nk) nxt[i] = *reinterpret_cast<const bf16x8*>(src + (c0 + SK_CH + i) * 64);
       } else if (srcn) {
 #pragma unroll
         for (int i = 0; i < SK_CH; ++i)
-          if (i < nk) nxt[i] = panel_load(srcn + i * 64);
+          if (i < nk) nxt[i] = *reinterpret_cast<const bf16x8*>(srcn + i * 64);
         if (PRE_RF) load_rf(gn);   // the next group's row terms fly with its first chunk
       }
 #pragma unroll
