@@ -52,6 +52,11 @@ class TreeFitter:
         self.cap, self.used, self.free = 0, 0, []
         self.count = self.mean = self.meanSq = None
         self._flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._kcap = 0
+        # every launch and copy goes to the stream current at construction (looked up once;
+        # the fitter's callers -- CobwebWrapper's build and add -- do not switch streams)
+        self._s = torch.cuda.current_stream(self.dev)
+        self._sp = ctypes.c_void_p(self._s.cuda_stream)
         self._owned = []
         self._grow(max(64, self._n_nodes() * 2))
         stack = [tree.root]
@@ -99,19 +104,31 @@ class TreeFitter:
             self.meanSq[n.slot] = torch.from_numpy(np.asarray(n.meanSq, F32)).to(self.dev)
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        return self._sp
 
     def _op(self, op, dst, src=-1, x=None):
         check(lib().cwq_fit_node_op(op, _p(self.count), _p(self.mean), _p(self.meanSq), self.D, dst, src,
                                     _p(x) if x is not None else None, _p(self._flag), self._stream()))
 
     def _kl(self, p_slot, x, jobs):
-        jobs = np.ascontiguousarray(np.asarray(jobs, np.int32).reshape(-1, 4))
-        jt = torch.from_numpy(jobs).to(self.dev)
-        out = torch.empty(len(jobs), dtype=torch.float32, device=self.dev)
+        """One cwq_fit_kl launch over `jobs` (4 ints each); the jobs go up and the results
+        come back through persistent pinned buffers: one stream sync per call."""
+        jobs = np.asarray(jobs, np.int32).reshape(-1)
+        n = jobs.size // 4
+        if n > self._kcap:
+            self._kcap = max(n, 2 * self._kcap)
+            self._jobs_h = torch.empty(4 * self._kcap, dtype=torch.int32, pin_memory=True)
+            self._jobs_d = torch.empty(4 * self._kcap, dtype=torch.int32, device=self.dev)
+            self._out_h = torch.empty(self._kcap, dtype=torch.float32, pin_memory=True)
+            self._out_d = torch.empty(self._kcap, dtype=torch.float32, device=self.dev)
+            self._jobs_np, self._out_np = self._jobs_h.numpy(), self._out_h.numpy()
+        self._jobs_np[:4 * n] = jobs
+        self._jobs_d[:4 * n].copy_(self._jobs_h[:4 * n], non_blocking=True)
         check(lib().cwq_fit_kl(_p(self.count), _p(self.mean), _p(self.meanSq), self.D, _p(x), float(self.pv),
-                               int(p_slot), _p(jt), len(jobs), _p(out), self._stream()))
-        return out.cpu().numpy()
+                               int(p_slot), _p(self._jobs_d), n, _p(self._out_d), self._sp))
+        self._out_h[:n].copy_(self._out_d[:n], non_blocking=True)
+        self._s.synchronize()
+        return self._out_np[:n].copy()
 
     def _new_node(self):
         n = Node(self.D)
