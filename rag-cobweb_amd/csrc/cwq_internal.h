@@ -262,7 +262,11 @@ struct SbPrepArgs {
 };
 hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s);
 constexpr int kStreamMaxLds = 160 * 1024;
-inline size_t stream_lds_bytes(int nqb, int DPB) { return (size_t)nqb * (DPB / 32) * 64 * 16; }
+constexpr int kStreamChunk = 8;   // K fragments (of 32 dims) per stream-kernel load chunk
+// query fragments in LDS, K padded with zero fragments to whole chunks
+inline size_t stream_lds_bytes(int nqb, int DPB) {
+  return (size_t)nqb * ((DPB / 32 + kStreamChunk - 1) / kStreamChunk * kStreamChunk) * 64 * 16;
+}
 struct StreamArgs {
   int DPB, nq, nqb;            // queries, 16-query blocks (nqb * 16 >= nq)
   int64_t nrows;               // isotropic filter rows

@@ -31,8 +31,10 @@
 // A fragments (16 B per lane, the row panel is row-major [row][DPB]) are loaded straight
 // into registers -- each row is used by one wave only, so there is nothing to share
 // through LDS -- and v_mfma_f32_16x16x32_bf16 (rows x 16 queries) runs once per fragment
-// and query block.  The MFMA work is ~5% of the pass time at 64 queries; the pass is
-// bound by HBM (24 KB in flight per wave, 192 KB per CU).
+// and query block.  Chunks of 8 fragments alternate between two register buffers (the
+// next chunk's 8 KB per wave in flight while the current one is multiplied), so the pass
+// is bound by HBM: C3 nq=1 272 us (5.8 TB/s), nq=64 297 us (was 389 us with one buffer
+// and a register copy per chunk that drained every load).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -50,7 +52,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int SK_WAVES = 8;
 constexpr int SK_MAXQB = kStreamMaxQ / 16;   // query blocks of 16
-constexpr int SK_CH = 8;                     // K fragments per chunk (8 x 32 = 256 dims)
+constexpr int SK_CH = kStreamChunk;         // K fragments per chunk (8 x 32 = 256 dims)
 // float <-> int order-preserving map for atomicMax on floats
 __device__ __forceinline__ int f2ord(float f) {
   const int i = __float_as_int(f);
@@ -66,12 +68,14 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nk = a.DPB / 32;
+  const int nkp = (nk + SK_CH - 1) / SK_CH * SK_CH;   // K padded to whole chunks (zero fragments)
   const int nqb = a.nqb;
   // ---- stage the queries' bf16 fragments (B operand: k = 8*(l>>4).., query = l&15) ----
-  for (int f = threadIdx.x; f < nqb * nk * 64; f += blockDim.x) {
-    const int l = f & 63, ks = (f >> 6) % nk, qb = (f >> 6) / nk;
+  for (int f = threadIdx.x; f < nqb * nkp * 64; f += blockDim.x) {
+    const int l = f & 63, ks = (f >> 6) % nkp, qb = (f >> 6) / nkp;
     const int q = qb * 16 + (l & 15);
-    const uint4 v = *reinterpret_cast<const uint4*>(a.Xb + ((size_t)q * a.DPB + ks * 32 + 8 * (l >> 4)));
+    const uint4 v = ks < nk ? *reinterpret_cast<const uint4*>(a.Xb + ((size_t)q * a.DPB + ks * 32 + 8 * (l >> 4)))
+                            : make_uint4(0u, 0u, 0u, 0u);
     *reinterpret_cast<uint4*>(sq + (size_t)f * 16) = v;
   }
   // per-lane query terms for the lane's column (query qb*16 + (lane & 15))
@@ -108,81 +112,89 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
     return reinterpret_cast<const char*>(a.Mb) + ((size_t)(grp * 16 + r16) * a.DPB + 8 * c16) * 2;
   };
-  // K runs in chunks of SK_CH fragments (16 B per lane each: row r0 + (lane & 15),
-  // k = ks*32 + 8*(lane >> 4)); the next chunk -- after the last one, the first chunk of
-  // the wave's next group -- is in flight during this chunk's MFMAs and the epilogue.
-  bf16x8 cur[SK_CH], nxt[SK_CH];
-  // row terms of the rows this lane's accumulator columns hold (r0 + 4*c16 + j), one group
-  // ahead like the panel chunks (at D = 256 a group is one chunk, so a load at the group's
-  // start would put its latency on every group)
-  constexpr bool PRE_RF = MQB == 1;
-  RowF rfn[4];
-  auto load_rf = [&](int64_t g) {
+  // row terms of the rows this lane's accumulator columns hold (r0 + 4*c16 + j)
+  auto load_rf = [&](RowF (&dst)[4], int64_t g) {
     const int64_t r0n = (MODE == 1 ? g * a.probe_stride : g) * 16;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t r = r0n + 4 * c16 + j;
-      rfn[j] = r < a.nrows ? a.rf[r] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+      dst[j] = r < a.nrows ? a.rf[r] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
     }
   };
   int64_t gi = (int64_t)blockIdx.x * SK_WAVES + wave;
-  if (gi < ngroups) {
-    const char* src = panel(gi);
+  if (gi >= ngroups) return;   // no barrier follows
+  // K runs in chunks of SK_CH fragments (16 B per lane each: row r0 + (lane & 15),
+  // k = ks*32 + 8*(lane >> 4)) over the wave's whole (group, chunk) sequence.  Two
+  // register buffers alternate chunk by chunk: the loads of the next chunk (after a
+  // group's last chunk, the first chunk of the wave's next group) go into one while the
+  // MFMAs consume the other.  No buffer is ever copied: a copy of registers whose loads
+  // are still in flight makes the compiler wait for every load (vmcnt(0)) before the
+  // chunk's MFMAs, which left one chunk in flight per wave and the pass at 0.67 of HBM.
+  // For the same reason nothing between a chunk's loads and its MFMAs is conditional:
+  // a partial last chunk re-reads its last fragment (a cache hit) and multiplies the
+  // extra copies by the zero query fragments of the LDS padding, and the wave's last
+  // step re-reads its current chunk.
+  bf16x8 bA[SK_CH], bB[SK_CH];
+  auto issue = [&](bf16x8 (&b)[SK_CH], const char* p, int nfr) {
 #pragma unroll
-    for (int i = 0; i < SK_CH; ++i)
-      if (i < nk) cur[i] = *reinterpret_cast<const bf16x8*>(src + i * 64);
-    if (PRE_RF) load_rf(gi);
-  }
-  int it = 0;
-  for (; gi < ngroups; gi += gstride, ++it) {
-    // live threshold every `live_every` groups, loaded now and used in the epilogue (the
-    // load is in flight with the row panel): T = max(T, Tlive[q])
-    const bool live = MODE == 0 && a.live_every > 0 && it % a.live_every == a.live_every - 1;
-    int tlive[MQB];
+    for (int i = 0; i < SK_CH; ++i) b[i] = *reinterpret_cast<const bf16x8*>(p + min(i, nfr - 1) * 64);
+  };
+  f32x4 acc[MQB];
+#pragma unroll
+  for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&b)[SK_CH], int c0) {
+#pragma unroll
+    for (int qb = 0; qb < MQB; ++qb) {
+      if (qb >= nqb) break;
+      const char* qs = sq + (((size_t)qb * nkp + c0) * 64 + lane) * 16;
+#pragma unroll
+      for (int i = 0; i < SK_CH; ++i)
+        acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[i], *reinterpret_cast<const bf16x8*>(qs + i * 1024),
+                                                          acc[qb], 0, 0, 0);
+    }
+  };
+  issue(bA, panel(gi), min(SK_CH, nk));
+  // the group's row terms are loaded at its start and used at its end (in flight with
+  // its chunks)
+  RowF rf[4];
+  load_rf(rf, gi);
+  int tlive[MQB];
+  bool live = false;
+  auto load_live = [&](int it) {
+    // live threshold every `live_every` groups, loaded at the group's start and used in
+    // its epilogue: T = max(T, Tlive[q])
+    live = MODE == 0 && a.live_every > 0 && it % a.live_every == a.live_every - 1;
 #pragma unroll
     for (int qb = 0; qb < MQB; ++qb) tlive[qb] = (live && qok[qb]) ? a.Tlive[qb * 16 + r16] : 0x80000000;
-    const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
-    const int64_t r0 = grp * 16;   // < nrows rounded up to 16 (probe: grp < ngroups of the panel)
-    RowF rf[4];
-    if (!PRE_RF) load_rf(gi);   // registers too tight for a group-ahead copy
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rf[j] = rfn[j];   // PRE_RF: loaded with the group's first chunk
-    const char* src = panel(gi);
-    const int64_t gn = gi + gstride;
-    const char* srcn = gn < ngroups ? panel(gn) : nullptr;
-    f32x4 acc[MQB];
-#pragma unroll
-    for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c0 = 0; c0 < nk; c0 += SK_CH) {
-      if (c0 + SK_CH < nk) {
-#pragma unroll
-        for (int i = 0; i < SK_CH; ++i)
-          if (c0 + SK_CH + i < nk) nxt[i] = *reinterpret_cast<const bf16x8*>(src + (c0 + SK_CH + i) * 64);
-      } else if (srcn) {
-#pragma unroll
-        for (int i = 0; i < SK_CH; ++i)
-          if (i < nk) nxt[i] = *reinterpret_cast<const bf16x8*>(srcn + i * 64);
-        if (PRE_RF) load_rf(gn);   // the next group's row terms fly with its first chunk
-      }
-#pragma unroll
-      for (int qb = 0; qb < MQB; ++qb) {
-        if (qb >= nqb) break;
-        const char* qs = sq + (((size_t)qb * nk + c0) * 64 + lane) * 16;
-#pragma unroll
-        for (int i = 0; i < SK_CH; ++i)
-          if (c0 + i < nk)
-            acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[i], *reinterpret_cast<const bf16x8*>(qs + i * 1024),
-                                                              acc[qb], 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < SK_CH; ++i) cur[i] = nxt[i];
+  };
+  int it = 0;
+  load_live(it);
+  int c0 = 0;
+  // one chunk: the next chunk's loads go into `oth`, the MFMAs consume `cur`; at a
+  // group's last chunk the epilogue runs and the wave moves to its next group.  Returns
+  // false after the wave's last group.  The loop below alternates step(bA, bB) and
+  // step(bB, bA), so which buffer is in flight is static in the code.
+  auto step = [&](const bf16x8 (&cur)[SK_CH], bf16x8 (&oth)[SK_CH]) -> bool {
+    int64_t gn = gi;
+    int cn = c0 + SK_CH;
+    if (cn >= nk) {
+      gn = gi + gstride;
+      cn = 0;
     }
+    const bool more = gn < ngroups;
+    issue(oth, more ? panel(gn) + cn * 64 : panel(gi) + c0 * 64, more ? min(SK_CH, nk - cn) : min(SK_CH, nk - c0));
+    mma(cur, c0);
+    if (cn != 0) {
+      c0 = cn;
+      return true;
+    }
+    // ---- group gi done.  Epilogue: rigorous bounds per (row, query); acc[qb][j] = dot
+    // of row r0 + 4*c16 + j with query qb*16 + (lane & 15)
+    const int64_t r0 = (MODE == 1 ? gi * a.probe_stride : gi) * 16;
     if (live) {
 #pragma unroll
       for (int qb = 0; qb < MQB; ++qb) Tq[qb] = fmaxf(Tq[qb], ord2f(tlive[qb]));
     }
-    // ---- epilogue: rigorous bounds per (row, query); acc[qb][j] = dot of row
-    // r0 + 4*c16 + j with query qb*16 + (lane & 15)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool rok = rf[j].par >= -1;
@@ -237,6 +249,16 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         pmax[qb] = -CWQ_INF;
       }
     }
+    if (!more) return false;
+    gi = gn;
+    c0 = 0;
+    load_rf(rf, gi);
+    load_live(++it);
+#pragma unroll
+    for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return true;
+  };
+  while (step(bA, bB) && step(bB, bA)) {
   }
 }
 
