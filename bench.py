@@ -40,6 +40,7 @@ import cobweb_pkg  # noqa: E402
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (no sparsity)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_CLOCK_GHZ = 2.4       # MI355X_MICROARCH.md: max clock (the dense peaks assume it)
 
 
 def config_label(N, D):
@@ -308,15 +309,16 @@ def main():
         launches = 1
     achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
     bytes_q = 8.0 * (N + 1) * D + 8.0 * 2 * N + 4.0 * D + 12.0 * k   # SURVEY §8(d) bytes per query
-    traffic = None
+    traffic = clk = None
     if os.path.exists(args.pmc_file):
         try:
             pm = json.load(open(args.pmc_file))
             if pm.get("workload") == [N, D, nql, k] and pm.get("kernel") == kname.split(" ")[0]:
                 # per step (the launches of one call), like `achieved`
                 traffic = pm.get("hbm_bytes_per_launch")
+                clk = pm.get("effective_clock_ghz")   # GRBM_GUI_ACTIVE / kernel time, same PMC run
         except Exception:
-            traffic = None
+            traffic = clk = None
 
     rec_l2 = rec_ip = rec_tgt = None
     if rank == 0 and args.recall_queries > 0:
@@ -354,7 +356,12 @@ def main():
                          "frac": round(achieved_tf / peak, 4), "traffic": traffic,
                          "kernel": kname, "kernel_ms": round(kern_ms, 3), "launches_per_step": launches,
                          "avg_launch_ms": round(kern_ms / launches, 3),
-                         "call_ms": round(call_ms, 3), "flops_per_step": flops_launch, "phases_ms": phases},
+                         "call_ms": round(call_ms, 3), "flops_per_step": flops_launch, "phases_ms": phases,
+                         # the dense peak assumes the 2.4 GHz peak clock; under this load the chip
+                         # holds the PMC-measured clock, so this is the fraction of what it can issue
+                         "clock_ghz_held": clk,
+                         "frac_at_held_clock": (round(achieved_tf / (peak * clk / PEAK_CLOCK_GHZ), 4)
+                                                if clk and pipe.startswith("bf16") else None)},
             "filter": {k_: st[k_] for k_ in ("filter_used", "fallback_queries", "candidates", "exact_reranks",
                                               "sample_rows")},
             # the reference algorithm reads every node's mean+var once per query; a batch
