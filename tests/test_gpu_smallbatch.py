@@ -160,3 +160,25 @@ def test_small_scan_vs_row_sliced_scan(gpu, shape, monkeypatch):
             assert torch.equal(got[0], ref[0]), (nq, k)
             assert torch.equal(got[1], ref[1]), (nq, k)
     ix.close()
+
+
+# the stream pass loads K in 8-fragment chunks with the LDS query image zero-padded to
+# whole chunks: dims whose fragment count is not a multiple of 8, and an LDS image at the
+# 160 KiB limit (D = 1100: 35 fragments -> 40, 4 query blocks = 160 KiB; D = 1300: 41 -> 48,
+# stream up to 3 query blocks, the batch filter above)
+@pytest.mark.parametrize("N,D,nqs", [(20000, 300, (1, 17, 64)), (20000, 1100, (1, 64)),
+                                     (20000, 1300, (33, 48, 64))])
+def test_stream_chunk_padding_vs_exact(gpu, N, D, nqs):
+    X = gpu.synth.synthetic_corpus(N, D, seed=41)
+    fs = gpu.synth.flat_synth(X)
+    ix = gpu.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, max(nqs), seed=42)
+    dpb = max(96, (D + 31) // 32 * 32)
+    nkp = (dpb // 32 + 7) // 8 * 8
+    for nq in nqs:
+        ref = run(ix, Q[:nq], 10, 0)
+        got = run(ix, Q[:nq], 10, 1)
+        if ((nq + 15) // 16) * nkp * 1024 <= 160 * 1024:
+            assert got[2]["path"] == "stream", (nq, got[2])
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), (D, nq)
+    ix.close()
