@@ -1123,7 +1123,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
   // one fused prep launch when the exact internal pass is small (flat trees: the root)
   bool fused = !ib && ix->NI <= kSbMaxNI && (int)ix->levels.size() <= kSbMaxNI &&
-               ((size_t)std::max(ix->DP, ix->DPB) + (size_t)ix->NI * (ix->DP / 16) + ix->NI) * 4 <= 65536 &&
+               ((size_t)2 * std::max(ix->DP, ix->DPB) + (size_t)ix->NI * (ix->DP / 16) + ix->NI) * 4 <= 65536 &&
                !getenv("CWQ_SB_UNFUSED");
   SbPrepArgs sp;
   if (fused) {

@@ -168,14 +168,19 @@ hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, 
 // here one slice per thread, then added in slice order by one thread (acc += part);
 // the prefixes are prefix_level_kernel's fmaf chain, level by level.
 __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
-  extern __shared__ float s_sb[];   // [DQ] query row, [NI][NV16] partials, [NI] prefixes
+  extern __shared__ float s_sb[];   // [DQ] query row, [DQ] centre, [NI][NV16] partials, [NI] prefixes
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t r = blockIdx.x;
   const bool valid = r < a.nq;
   const int NV16 = a.DP / 16;
   const int DQ = a.DP > a.DPB ? a.DP : a.DPB;
   float* xq = s_sb;   // the query row, zero padded: every phase below reads it from LDS
-  for (int d = tid; d < DQ; d += 256) xq[d] = (valid && d < a.D) ? a.q[r * a.D + d] : 0.f;
+  float* cq = s_sb + DQ;   // the centre, staged with the row (a global load inside the bf16
+                           // prep loop below was one dependent round trip per iteration)
+  for (int d = tid; d < DQ; d += 256) {
+    xq[d] = (valid && d < a.D) ? a.q[r * a.D + d] : 0.f;
+    cq[d] = d < a.D ? a.c[d] : 0.f;
+  }
   __syncthreads();
   // pad_queries_kernel: the scan's interleaved layout [r/kXQ][v][r%kXQ][16]
   for (int d = tid; d < a.DP; d += 256) {
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
   if (r < a.nq16 && tid < 64) {   // query_prep_kernel (wave 0)
     double sv = 0.0, slo = 0.0, shi = 0.0;
     for (int d = lane; d < a.DPB; d += kWave) {
-      const float v = (valid && d < a.D) ? xq[d] - a.c[d] : 0.f;
+      const float v = (valid && d < a.D) ? xq[d] - cq[d] : 0.f;
       const __bf16 h = (__bf16)v;
       const float hf = (float)h;
       const float lo = v - hf;
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
   if (tid < 5) a.qcnt[(size_t)tid * a.nq + r] = 0;
   if (a.NI == 0) return;
   // internal nodes: partials of (node n, slice v), straight from the caller's query
-  float* part = s_sb + DQ;
+  float* part = s_sb + 2 * DQ;
   for (int t = tid; t < a.NI * NV16; t += 256) {
     const int n = t / NV16, v = t - n * NV16;
     float pp;
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
 }
 
 hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s) {
-  const size_t lds = ((size_t)std::max(a.DP, a.DPB) + (size_t)a.NI * (a.DP / 16) + a.NI) * 4;
+  const size_t lds = ((size_t)2 * std::max(a.DP, a.DPB) + (size_t)a.NI * (a.DP / 16) + a.NI) * 4;
   if (a.nq <= 0 || a.nq_pad < a.nq16 || a.nq16 < a.nq || a.DP % 16 || a.NI > kSbMaxNI || a.nlev > kSbMaxNI ||
       lds > 65536)
     return hipErrorInvalidValue;
