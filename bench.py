@@ -85,7 +85,13 @@ def cpu_baseline(X_host, root_mean, root_var, Q_host, k, sample_all, sample_1t, 
     T = O.TorchFastIndex.flat(root_mean, root_var, X_host)
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    n_all = min(aff, omp) if omp > 0 else aff          # the box caps this process at OMP_NUM_THREADS
+    # SURVEY §8(d) asks for len(sched_getaffinity) threads.  The GPU pool gives each
+    # one-GPU job a CPU share, exports it as OMP_NUM_THREADS and asks jobs to size their
+    # thread pools to it (affinity lists the whole machine's CPUs), so the all-cores leg
+    # runs at that share when the variable is set
+    n_all = min(aff, omp) if omp > 0 else aff
+    cap_reason = (f"capped at the pool's per-job CPU share OMP_NUM_THREADS={omp} (affinity lists {aff} CPUs of "
+                  f"the whole machine)" if 0 < omp < aff else f"all {aff} affinity CPUs")
     prev = torch.get_num_threads()
     legs, agree = {}, 0
     for name, threads, sample in (("all", n_all, sample_all), ("1t", 1, sample_1t)):
@@ -108,7 +114,7 @@ def cpu_baseline(X_host, root_mean, root_var, Q_host, k, sample_all, sample_1t, 
     return {"value": main["queries_per_s"], "unit": "queries/s", "cores": main["threads"], "kind": "port",
             "sample": f"reference op sequence in torch-CPU (oracle.TorchFastIndex, CobwebWrapper.py:222-257) on the "
                       f"full flat-synth {N}x{D} tree, one query per call; {legs['all']['queries'] if 'all' in legs else 0} "
-                      f"queries at {n_all} threads (affinity {aff} cpus, OMP_NUM_THREADS {omp or 'unset'}) and "
+                      f"queries at {n_all} threads ({cap_reason}) and "
                       f"{legs['1t']['queries'] if '1t' in legs else 0} at 1 thread; CPU: {cpu_model()}; GPU top-{k} "
                       f"identical on {agree}/{min(len(ids_gpu), legs['all']['queries'] if 'all' in legs else 0)}",
             "legs": legs}
@@ -197,7 +203,7 @@ def main():
     ap.add_argument("--strong", action="store_true", default=None, help="split --queries over the ranks")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--cpu-sample", type=int, default=20, help="CPU baseline queries at all host threads")
-    ap.add_argument("--cpu-sample-1t", type=int, default=4, help="CPU baseline queries at 1 thread")
+    ap.add_argument("--cpu-sample-1t", type=int, default=20, help="CPU baseline queries at 1 thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-call", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
@@ -233,9 +239,14 @@ def main():
     # ---- tree: synthesised on rank 0, broadcast over RCCL (dist.broadcast_tree) ----
     t0 = time.perf_counter()
     root_mu = None
+    def dev_used():
+        fr, tot = torch.cuda.mem_get_info(dev)
+        return tot - fr
+
     if rank == 0:
         X = pkg.synth.synthetic_corpus(N, D, seed=0, device=dev)
-        tree = pkg.synth.flat_synth(X)
+        # variances in compact form: one scalar per leaf (prior_var), the root's row in full
+        tree = pkg.synth.flat_synth(X, compact=True)
         mean, var, parent, nos = tree["mean"], tree["var"], tree["parent"], tree["node_of_sentence"]
         root_mu = tree["root"][1]
         del tree, X
@@ -247,13 +258,16 @@ def main():
     if world > 1:
         dist.barrier()
         t1 = time.perf_counter()
-        mean, var, parent, nos = D_.broadcast_tree(mean, var, parent, nos, src=0, device=dev, stats=bstats)
+        mean, var, parent, nos = D_.broadcast_tree(mean, var, parent, nos, src=0, device=dev, stats=bstats,
+                                                   compact=True)
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t1
     t1 = time.perf_counter()
     index = pkg.index.CobwebIndex(mean, var, parent, nos, device=dev)
     torch.cuda.synchronize()
     t_index = time.perf_counter() - t1
+    torch.cuda.empty_cache()
+    used_create = dev_used()              # caller's mean + compact var + the index's own copies
     X = mean[1:]                          # leaf means are the corpus rows
     root_var_host = var[0].cpu().numpy() if rank == 0 else None
     del var
@@ -320,6 +334,13 @@ def main():
         except Exception:
             traffic = clk = None
 
+    torch.cuda.empty_cache()
+    used_steady = dev_used()              # + the handle's workspace after the timed calls
+    mem = {"index_bytes": index.info["device_bytes"], "device_used_after_index_create": used_create,
+           "device_used_after_timed_steps": used_steady, "device_total": torch.cuda.mem_get_info(dev)[1],
+           "note": "device-wide used bytes (mem_get_info) on this rank; the caller's mean stays resident (the "
+                   "queries and the recall ground truth are drawn from it)"}
+
     rec_l2 = rec_ip = rec_tgt = None
     if rank == 0 and args.recall_queries > 0:
         tg = targets if q_lo == 0 else targets[:0]
@@ -373,6 +394,7 @@ def main():
             "recall@10": {"vs_flat_l2": rec_l2, "vs_flat_ip": rec_ip, "target_in_top10": rec_tgt,
                           "n_queries": min(args.recall_queries, nql)},
             "cpu_baseline": base,
+            "memory_bytes_rank0": mem,
             "setup_s": {"synth": round(t_synth, 3), "rccl_broadcast": round(t_bcast, 3),
                         "rccl_broadcast_bytes": bstats.get("bytes"), "index_build": round(t_index, 3)},
         }

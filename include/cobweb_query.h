@@ -76,6 +76,23 @@ int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean
                      const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
                      const double* level_w, int32_t n_w, void* stream, cwq_index** out);
 
+/*
+ * cwq_index_create with the variances in compact form (same index, same results).
+ * In the reference every count-1 leaf has var = meanSq/1 + prior_var = prior_var in all
+ * D dimensions (CobwebTorchTree.py:336-342, CobwebWrapper.py:186-203), so a flat 10M x
+ * 1024 tree's _node_vars is 41 GB of one repeated value.  Here:
+ *   var_row   device [n_nodes] fp32: the variance of node i in every dimension, for the
+ *             nodes NOT listed in an_nodes
+ *   an_nodes  host [n_an] int64: the nodes whose variances differ across dimensions
+ *             (internal nodes, leaves holding several points), each listed once
+ *   an_var    device [n_an*dim] fp32: their compute_var rows, in an_nodes order
+ * Other arguments as cwq_index_create.  The caller may free every input on return.
+ */
+int cwq_index_create_cv(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var_row,
+                        const int64_t* an_nodes, int64_t n_an, const float* an_var, const int64_t* parent,
+                        const int64_t* node_of_sentence, int64_t n_sent, const double* level_w, int32_t n_w,
+                        void* stream, cwq_index** out);
+
 int cwq_index_destroy(cwq_index* idx);
 
 /* Index facts: out[0]=n_nodes out[1]=dim out[2]=n_sent out[3]=internal nodes

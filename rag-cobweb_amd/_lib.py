@@ -27,6 +27,8 @@ SIGNATURES = {
     "cwq_build_id": (_c.c_char_p, []),
     "cwq_last_error": (_c.c_char_p, []),
     "cwq_index_create": (_c.c_int, [_c.c_int, _I64, _I32, _P, _P, _P, _P, _I64, _P, _I32, _P, _c.POINTER(_P)]),
+    "cwq_index_create_cv": (_c.c_int, [_c.c_int, _I64, _I32, _P, _P, _P, _I64, _P, _P, _P, _I64, _P, _I32, _P,
+                                       _c.POINTER(_P)]),
     "cwq_index_destroy": (_c.c_int, [_P]),
     "cwq_index_info": (_c.c_int, [_P, _P]),
     "cwq_score_topk": (_c.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
@@ -76,7 +78,8 @@ def lib():
             L = load_library(LIB_PATH)
             if not os.environ.get("CWQ_LIB"):
                 from .build import source_id
-                got, want = L.cwq_build_id().decode(), source_id()
+                # the same extra flags build_library() stamps into the id (CWQ_HIPCC_FLAGS)
+                got, want = L.cwq_build_id().decode(), source_id(os.environ.get("CWQ_HIPCC_FLAGS", "").split())
                 if got != want:
                     raise ImportError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
                                       f"rebuild it with __graft_entry__.build()")

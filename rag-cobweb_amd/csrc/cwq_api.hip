@@ -199,7 +199,13 @@ struct cwq_index {
   }
   // end of a query call: the workspace is busy until the work queued on s so far is done
   int ws_end(hipStream_t s) {
-    if (hipEventRecord(ws_ev, s) != hipSuccess) return fail(CWQ_ERR_HIP, "hipEventRecord failed");
+    if (!ws_ev) return fail(CWQ_ERR_HIP, "workspace event missing");
+    if (hipEventRecord(ws_ev, s) != hipSuccess) {
+      // the event no longer marks this call's work: wait for it here instead
+      ws_ev_live = false;
+      (void)hipStreamSynchronize(s);
+      return fail(CWQ_ERR_HIP, "hipEventRecord failed");
+    }
     ws_ev_live = true;
     return CWQ_OK;
   }
@@ -234,7 +240,9 @@ struct WsUse {
   hipStream_t s;
   int rc;
   WsUse(cwq_index* i, hipStream_t st) : ix(i), s(st) { rc = ix->ws_begin(s); }
-  ~WsUse() { (void)ix->ws_end(s); }
+  ~WsUse() {
+    if (rc == CWQ_OK) (void)ix->ws_end(s);   // ws_begin failed: nothing was queued on s
+  }
 };
 
 #ifndef CWQ_BUILD_ID
@@ -414,16 +422,12 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
 
 }  // namespace
 
-extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var,
-                                const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
-                                const double* level_w, int32_t n_w, void* stream, cwq_index** out) {
-  if (!out) return fail(CWQ_ERR_ARG, "out is NULL");
-  *out = nullptr;
-  if (n_nodes <= 0 || dim <= 0 || !mean || !var || !parent) return fail(CWQ_ERR_ARG, "empty tree or NULL inputs");
-  if (n_nodes >= (int64_t)INT32_MAX / 2) return fail(CWQ_ERR_ARG, "too many nodes");
-  if (n_sent < 0 || (n_sent > 0 && !node_of_sentence)) return fail(CWQ_ERR_ARG, "bad sentence map");
-  DevGuard dg(device);
-  hipStream_t s = (hipStream_t)stream;
+namespace {
+// cwq_index_create / cwq_index_create_cv: `var` is either the full [n_nodes][D] array or
+// the compact per-node form (VarSrc); both give the same index.
+int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mean, const VarSrc& var,
+                      const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent, const double* level_w,
+                      int32_t n_w, hipStream_t s, cwq_index** out) {
 
   // ---- structure (host) ----
   if (parent[0] != -1) return fail(CWQ_ERR_ARG, "parent[0] must be -1 (root first, BFS order)");
@@ -627,6 +631,59 @@ extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const 
   HIPCHK(hipStreamSynchronize(s));
   *out = ix.release();
   return CWQ_OK;
+}
+
+int create_args_ok(int64_t n_nodes, int32_t dim, const float* mean, const int64_t* parent,
+                   const int64_t* node_of_sentence, int64_t n_sent, cwq_index** out) {
+  if (!out) return fail(CWQ_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n_nodes <= 0 || dim <= 0 || !mean || !parent) return fail(CWQ_ERR_ARG, "empty tree or NULL inputs");
+  if (n_nodes >= (int64_t)INT32_MAX / 2) return fail(CWQ_ERR_ARG, "too many nodes");
+  if (n_sent < 0 || (n_sent > 0 && !node_of_sentence)) return fail(CWQ_ERR_ARG, "bad sentence map");
+  return CWQ_OK;
+}
+}  // namespace
+
+extern "C" int cwq_index_create(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var,
+                                const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent,
+                                const double* level_w, int32_t n_w, void* stream, cwq_index** out) {
+  int rc = create_args_ok(n_nodes, dim, mean, parent, node_of_sentence, n_sent, out);
+  if (rc) return rc;
+  if (!var) return fail(CWQ_ERR_ARG, "var is NULL");
+  DevGuard dg(device);
+  const VarSrc vs{var, nullptr, nullptr, nullptr};
+  return index_create_impl(device, n_nodes, dim, mean, vs, parent, node_of_sentence, n_sent, level_w, n_w,
+                           (hipStream_t)stream, out);
+}
+
+extern "C" int cwq_index_create_cv(int device, int64_t n_nodes, int32_t dim, const float* mean, const float* var_row,
+                                   const int64_t* an_nodes, int64_t n_an, const float* an_var, const int64_t* parent,
+                                   const int64_t* node_of_sentence, int64_t n_sent, const double* level_w, int32_t n_w,
+                                   void* stream, cwq_index** out) {
+  int rc = create_args_ok(n_nodes, dim, mean, parent, node_of_sentence, n_sent, out);
+  if (rc) return rc;
+  if (!var_row || n_an < 0 || (n_an > 0 && (!an_nodes || !an_var))) return fail(CWQ_ERR_ARG, "bad compact var");
+  std::vector<int> an_map(n_nodes, -1);
+  for (int64_t j = 0; j < n_an; ++j) {
+    const int64_t nd = an_nodes[j];
+    if (nd < 0 || nd >= n_nodes) return fail(CWQ_ERR_ARG, "an_nodes out of range");
+    if (an_map[nd] >= 0) return fail(CWQ_ERR_ARG, "an_nodes lists a node twice");
+    an_map[nd] = (int)j;
+  }
+  DevGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+  int* d_map = nullptr;
+  if (hipMalloc(&d_map, (size_t)n_nodes * sizeof(int)) != hipSuccess)
+    return fail(CWQ_ERR_OOM, "hipMalloc failed (compact var map)");
+  if (hipMemcpyAsync(d_map, an_map.data(), (size_t)n_nodes * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) {
+    (void)hipFree(d_map);
+    return fail(CWQ_ERR_HIP, "compact var map upload failed");
+  }
+  const VarSrc vs{nullptr, var_row, d_map, an_var};
+  rc = index_create_impl(device, n_nodes, dim, mean, vs, parent, node_of_sentence, n_sent, level_w, n_w, s, out);
+  (void)hipStreamSynchronize(s);   // the build kernels read the map (an error path may return early)
+  (void)hipFree(d_map);
+  return rc;
 }
 
 extern "C" int cwq_index_destroy(cwq_index* idx) {
@@ -884,7 +941,9 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
   }
   const int lps = scan_lists_per_slab(kl);
   const int nslab_total = slab_off0 + (small ? ns[0] : ns[0] * lps) + ns[1] * lps;
-  if (nslab_total > max_lists) return CWQ_ERR_ARG;   // internal: the caller's list buffers are too small
+  if (nslab_total > max_lists)
+    return fail(CWQ_ERR_ARG, "internal: partial-list buffer too small (" + std::to_string(nslab_total) +
+                                 " lists needed, " + std::to_string(max_lists) + " allocated)");
   if (nslab_total_out) *nslab_total_out = nslab_total;
   int slab_off = slab_off0;
   for (int i = 0; i < 2; ++i) {

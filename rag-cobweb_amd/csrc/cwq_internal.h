@@ -83,17 +83,34 @@ struct SimArgs {
   int64_t* out_nodes; int* n_found; int64_t* n_calls; int* status;
 };
 
+// Node variances read by the index build.  Full: [n_nodes][D] rows (compute_var of every
+// node, CobwebWrapper.py:186-203).  Compact (cwq_index_create_cv): one scalar per node --
+// a node whose D variances are one repeated value, as every count-1 leaf's are
+// (var = prior_var, CobwebTorchTree.py:336-342) -- plus full rows for the nodes listed in
+// an_map (an_map[node] >= 0: that node's row of an_var).  Both give the same values.
+struct VarSrc {
+  const float* full;     // [n_nodes][D], or nullptr (compact)
+  const float* row;      // compact: [n_nodes]
+  const int* an_map;     // compact: [n_nodes], row of an_var or -1
+  const float* an_var;   // compact: [n_an][D]
+  __device__ __forceinline__ float at(int64_t node, int d, int D) const {
+    if (full) return full[node * D + d];
+    const int m = an_map[node];
+    return m >= 0 ? an_var[(int64_t)m * D + d] : row[node];
+  }
+};
+
 // ---- launchers (cwq_kernels.hip) ----
 hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s);
 // rows of `words` 4-byte words: dst[di ? di[i] : i] = src[si ? si[i] : i] (strides in words)
 hipError_t launch_copy_rows(const void* src, int64_t src_stride_w, const int64_t* src_idx, void* dst,
                             int64_t dst_stride_w, const int64_t* dst_idx, int64_t n, int64_t words, hipStream_t s);
-hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s);
+hipError_t launch_iso_flags(const VarSrc& var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s);
 // mode 0: dst = mean, 1: dst = 1/sqrt(var), 2: dst = mean/sqrt(var)
-hipError_t launch_gather_T(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n, int mode,
+hipError_t launch_gather_T(const float* mean, const VarSrc& var, int D, const int64_t* nodes, int64_t n, int mode,
                            float* dst, int64_t ld, int DP, hipStream_t s);
-hipError_t launch_logdet(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
-hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
+hipError_t launch_logdet(const VarSrc& var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
+hipError_t launch_inv_var0(const VarSrc& var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
 
 // The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
 hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
@@ -313,7 +330,7 @@ hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp,
 // its RowF {R0 = M_n, beta, delta, rn2 = c_n, hs = wmax, hl = logdet, invL = level weight
 // w_int, par = parent internal id (-1 root, -2 padding)}, and row-major
 // fp32 copies Ar = A, Br = mean * A (bit-identical to the exact scan's int_A / int_B).
-hipError_t launch_int_prep(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n,
+hipError_t launch_int_prep(const float* mean, const VarSrc& var, int D, const int64_t* nodes, int64_t n,
                            const float* c, const float* logdet, const int* par_int, const float* w_int, int DP, int DPB2,
                            int64_t ld, void* Mb2, RowF* rf, float* Ar, float* Br, float gamma, hipStream_t s);
 // Queries for the internal bounds: a = [x'^2, x'] bf16 hi [nq_pad][DPB2], qinfo =

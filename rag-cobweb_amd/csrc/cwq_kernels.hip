@@ -1331,20 +1331,19 @@ hipError_t launch_copy_rows(const void* src, int64_t src_stride_w, const int64_t
 }
 
 // flags[r] = 1 when var[node[r], :] is one value repeated (bitwise).
-__global__ void iso_flags_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
-                                 int* flags) {
+__global__ void iso_flags_kernel(const VarSrc var, int D, const int64_t* __restrict__ nodes, int64_t n, int* flags) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
   if (r >= n) return;
-  const float* v = var + nodes[r] * (int64_t)D;
-  const float v0 = v[0];
+  const int64_t nd = nodes[r];
+  const float v0 = var.at(nd, 0, D);
   bool same = true;
-  for (int d = lane; d < D; d += kWave) same &= (__float_as_uint(v[d]) == __float_as_uint(v0));
+  for (int d = lane; d < D; d += kWave) same &= (__float_as_uint(var.at(nd, d, D)) == __float_as_uint(v0));
   const bool all = __all(same);
   if (lane == 0) flags[r] = all ? 1 : 0;
 }
 
-hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s) {
+hipError_t launch_iso_flags(const VarSrc& var, int D, const int64_t* nodes, int64_t n, int* flags, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(iso_flags_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, var, D, nodes, n, flags);
   return hipGetLastError();
@@ -1352,8 +1351,8 @@ hipError_t launch_iso_flags(const float* var, int D, const int64_t* nodes, int64
 
 // dst[d * ld + r] = f(mean[node[r], d], var[node[r], d]); zero padding for
 // d >= D or r >= n.  64x64 tile transpose through LDS (both sides coalesced).
-__global__ __launch_bounds__(256) void gather_T_kernel(const float* __restrict__ mean, const float* __restrict__ var,
-                                                       int D, const int64_t* __restrict__ nodes, int64_t n, int mode,
+__global__ __launch_bounds__(256) void gather_T_kernel(const float* __restrict__ mean, const VarSrc var, int D,
+                                                       const int64_t* __restrict__ nodes, int64_t n, int mode,
                                                        float* dst, int64_t ld, int DP) {
   __shared__ float tile[64][65];
   const int64_t r0 = (int64_t)blockIdx.y * 64;
@@ -1364,11 +1363,12 @@ __global__ __launch_bounds__(256) void gather_T_kernel(const float* __restrict__
     const int d = d0 + tx;
     float v = 0.f;
     if (r < n && d < D) {
-      const int64_t o = nodes[r] * (int64_t)D + d;
+      const int64_t nd = nodes[r];
+      const int64_t o = nd * (int64_t)D + d;
       if (mode == 0) {
         v = mean[o];
       } else {
-        const float is = 1.0f / sqrtf(var[o]);
+        const float is = 1.0f / sqrtf(var.at(nd, d, D));
         v = mode == 1 ? is : mean[o] * is;
       }
     }
@@ -1382,7 +1382,7 @@ __global__ __launch_bounds__(256) void gather_T_kernel(const float* __restrict__
   }
 }
 
-hipError_t launch_gather_T(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n, int mode,
+hipError_t launch_gather_T(const float* mean, const VarSrc& var, int D, const int64_t* nodes, int64_t n, int mode,
                            float* dst, int64_t ld, int DP, hipStream_t s) {
   if (ld <= 0) return hipSuccess;
   dim3 grid((unsigned)((DP + 63) / 64), (unsigned)((ld + 63) / 64));
@@ -1391,31 +1391,29 @@ hipError_t launch_gather_T(const float* mean, const float* var, int D, const int
 }
 
 // logdet[r] = sum_d log(var[node[r], d]); fp32 logs (as torch.log), fp64 sum.
-__global__ void logdet_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
-                              float* out) {
+__global__ void logdet_kernel(const VarSrc var, int D, const int64_t* __restrict__ nodes, int64_t n, float* out) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
   if (r >= n) return;
-  const float* v = var + nodes[r] * (int64_t)D;
+  const int64_t nd = nodes[r];
   double s = 0.0;
-  for (int d = lane; d < D; d += kWave) s += (double)logf(v[d]);
+  for (int d = lane; d < D; d += kWave) s += (double)logf(var.at(nd, d, D));
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if (lane == 0) out[r] = (float)s;
 }
 
-hipError_t launch_logdet(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
+hipError_t launch_logdet(const VarSrc& var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(logdet_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, var, D, nodes, n, out);
   return hipGetLastError();
 }
 
-__global__ void inv_var0_kernel(const float* __restrict__ var, int D, const int64_t* __restrict__ nodes, int64_t n,
-                                float* out) {
+__global__ void inv_var0_kernel(const VarSrc var, int D, const int64_t* __restrict__ nodes, int64_t n, float* out) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-    out[r] = 1.0f / var[nodes[r] * (int64_t)D];
+    out[r] = 1.0f / var.at(nodes[r], 0, D);
 }
 
-hipError_t launch_inv_var0(const float* var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
+hipError_t launch_inv_var0(const VarSrc& var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(inv_var0_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, var, D,
                      nodes, n, out);

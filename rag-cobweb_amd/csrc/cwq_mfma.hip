@@ -260,7 +260,7 @@ __device__ __forceinline__ void prefix_step(float pl, float ph, float w, float& 
 }
 
 // Internal-node bound operands (launch_int_prep, cwq_internal.h).  One wave per node.
-__global__ void int_prep_kernel(const float* __restrict__ mean, const float* __restrict__ var, int D,
+__global__ void int_prep_kernel(const float* __restrict__ mean, const VarSrc var, int D,
                                 const int64_t* __restrict__ nodes, int64_t n, const float* __restrict__ c,
                                 const float* __restrict__ logdet, const int* __restrict__ par_int,
                                 const float* __restrict__ w_int, int DP, int DPB2, int64_t ld, __bf16* Mb2, RowF* rf,
@@ -276,7 +276,7 @@ __global__ void int_prep_kernel(const float* __restrict__ mean, const float* __r
     float v = 0.f;
     if (ok) {
       const int64_t o = nodes[r] * (int64_t)D + d;
-      const float A = 1.0f / sqrtf(var[o]);      // as gather_T_kernel (the exact scan's A)
+      const float A = 1.0f / sqrtf(var.at(nodes[r], d, D));   // as gather_T_kernel (the exact scan's A)
       const float w = A * A;
       const float mu = mean[o];
       const float mc = mu - c[d];
@@ -328,7 +328,7 @@ __global__ void int_prep_kernel(const float* __restrict__ mean, const float* __r
   }
 }
 
-hipError_t launch_int_prep(const float* mean, const float* var, int D, const int64_t* nodes, int64_t n,
+hipError_t launch_int_prep(const float* mean, const VarSrc& var, int D, const int64_t* nodes, int64_t n,
                            const float* c, const float* logdet, const int* par_int, const float* w_int, int DP, int DPB2,
                            int64_t ld, void* Mb2, RowF* rf, float* Ar, float* Br, float gamma, hipStream_t s) {
   if (ld <= 0) return hipSuccess;

@@ -25,24 +25,28 @@ def _default_device():
     return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
-def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None, stats=None):
+def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None, stats=None, compact=False):
     """Broadcast a BFS-flattened tree from `src`.  Non-src ranks pass None for the
     arrays; every rank returns (mean, var, parent, node_of_sentence) with mean/var
     on `device` (the RCCL buffers) and the small structure arrays as numpy.
 
     `var` travels compressed: a row whose D values are one value repeated (every
     count-1 leaf: var = prior_var exactly, CobwebTorchTree.py:336-342) is sent as that
-    scalar, and only the other rows are sent in full.  The receivers rebuild var
-    bit for bit.  For a flat-synth tree that is N+1 scalars + one row instead of
-    (N+1) x D floats (3.07 GB at C3).  `stats` (dict) receives the bytes sent."""
+    scalar, and only the other rows are sent in full.  For a flat-synth tree that is
+    N+1 scalars + one row instead of (N+1) x D floats (3.07 GB at C3).  `var` may be
+    given as an index.CompactVar already.  compact=False: every rank returns the full
+    [Nn, D] var, rebuilt bit for bit; compact=True: every rank returns the CompactVar
+    (cwq_index_create_cv builds from it directly: no [Nn, D] array on any rank -- 41 GB
+    at C4).  `stats` (dict) receives the bytes sent."""
+    from .index import CompactVar
     rank, ws = world()
     dev = torch.device(device) if device is not None else _default_device()
     if rank == src:
         mean = torch.as_tensor(mean, dtype=torch.float32).to(dev).contiguous()
-        var = torch.as_tensor(var, dtype=torch.float32).to(dev).contiguous()
-        bits = var.view(torch.int32)
-        iso = (bits == bits[:, :1]).all(1)
-        an_idx = torch.nonzero(~iso).squeeze(1).to(torch.int64)
+        cv = var if isinstance(var, CompactVar) else CompactVar.from_full(torch.as_tensor(var).to(dev))
+        v0 = torch.as_tensor(cv.row, dtype=torch.float32).to(dev).contiguous()
+        an_idx = torch.as_tensor(cv.an_nodes, dtype=torch.int64).to(dev).contiguous()
+        an_rows = torch.as_tensor(cv.an_var, dtype=torch.float32).to(dev).contiguous()
         meta = torch.tensor([mean.shape[0], mean.shape[1], len(node_of_sentence), an_idx.numel()], dtype=torch.int64)
     else:
         meta = torch.zeros(4, dtype=torch.int64)
@@ -50,8 +54,6 @@ def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None, stat
     dist.broadcast(meta, src)
     n_nodes, dim, n_sent, n_an = (int(v) for v in meta.tolist())
     if rank == src:
-        v0 = var[:, 0].contiguous()
-        an_rows = var[an_idx].contiguous()
         par = torch.as_tensor(np.asarray(parent, np.int64)).to(dev)
         nos = torch.as_tensor(np.asarray(node_of_sentence, np.int64)).to(dev)
     else:
@@ -66,10 +68,13 @@ def broadcast_tree(mean, var, parent, node_of_sentence, src=0, device=None, stat
         if t.numel():
             dist.broadcast(t, src)
             sent += t.numel() * t.element_size()
-    if rank != src:
-        var = v0[:, None].expand(n_nodes, dim).contiguous()
-        if n_an:
-            var[an_idx] = an_rows
+    cv = CompactVar(v0, an_idx.cpu(), an_rows)
+    if compact:
+        var = cv
+    elif rank != src or isinstance(var, CompactVar):
+        var = cv.full()
+    else:
+        var = torch.as_tensor(var, dtype=torch.float32).to(dev).contiguous()
     if stats is not None:
         stats["bytes"] = sent
         stats["var_rows_sent"] = n_an
@@ -140,7 +145,7 @@ class ShardedCobwebIndex:
 
     def __init__(self, mean=None, var=None, parent=None, node_of_sentence=None, level_weights=None, src=0):
         from .index import CobwebIndex
-        mean, var, parent, nos = broadcast_tree(mean, var, parent, node_of_sentence, src=src)
+        mean, var, parent, nos = broadcast_tree(mean, var, parent, node_of_sentence, src=src, compact=True)
         self.index = CobwebIndex(mean, var, parent, nos, level_weights, device=mean.device)
 
     def score_topk(self, queries, k):

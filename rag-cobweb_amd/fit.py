@@ -123,10 +123,11 @@ class TreeFitter:
             self._out_d = torch.empty(self._kcap, dtype=torch.float32, device=self.dev)
             self._jobs_np, self._out_np = self._jobs_h.numpy(), self._out_h.numpy()
         self._jobs_np[:4 * n] = jobs
-        self._jobs_d[:4 * n].copy_(self._jobs_h[:4 * n], non_blocking=True)
-        check(lib().cwq_fit_kl(_p(self.count), _p(self.mean), _p(self.meanSq), self.D, _p(x), float(self.pv),
-                               int(p_slot), _p(self._jobs_d), n, _p(self._out_d), self._sp))
-        self._out_h[:n].copy_(self._out_d[:n], non_blocking=True)
+        with torch.cuda.stream(self._s):   # both copies on the stream the kernel runs on
+            self._jobs_d[:4 * n].copy_(self._jobs_h[:4 * n], non_blocking=True)
+            check(lib().cwq_fit_kl(_p(self.count), _p(self.mean), _p(self.meanSq), self.D, _p(x), float(self.pv),
+                                   int(p_slot), _p(self._jobs_d), n, _p(self._out_d), self._sp))
+            self._out_h[:n].copy_(self._out_d[:n], non_blocking=True)
         self._s.synchronize()
         return self._out_np[:n].copy()
 

@@ -35,10 +35,54 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+class CompactVar:
+    """Node variances in compact form (cwq_index_create_cv): `row[i]` is node i's variance
+    in every dimension -- every count-1 leaf has var = prior_var exactly
+    (CobwebTorchTree.py:336-342) -- except for the nodes `an_nodes` (int64, ascending),
+    whose full rows are `an_var` [n_an, D].  A flat 10M x 1024 tree's variances are 40 MB
+    this way instead of 41 GB."""
+
+    def __init__(self, row, an_nodes, an_var):
+        self.row = row
+        self.an_nodes = an_nodes
+        self.an_var = an_var
+
+    @property
+    def shape(self):
+        return (int(self.row.shape[0]), int(self.an_var.shape[1]))
+
+    @classmethod
+    def from_full(cls, var):
+        """Compress a full [Nn, D] variance tensor (bitwise: a row counts as one value
+        only when all D values have the same bits)."""
+        var = torch.as_tensor(var, dtype=torch.float32)
+        bits = var.view(torch.int32)
+        iso = (bits == bits[:, :1]).all(1)
+        an = torch.nonzero(~iso).squeeze(1).to(torch.int64)
+        return cls(var[:, 0].contiguous(), an, var[an].contiguous())
+
+    def full(self):
+        """The [Nn, D] array it stands for (tests / small trees)."""
+        n, d = self.shape
+        out = self.row[:, None].expand(n, d).clone()
+        if self.an_nodes.numel():
+            out[self.an_nodes.to(out.device)] = self.an_var.to(out.device)
+        return out
+
+    def __getitem__(self, i):   # one node's variance row (bench's root var, small reads)
+        i = int(i)
+        hit = (self.an_nodes == i).nonzero()
+        if hit.numel():
+            return self.an_var[int(hit[0, 0])]
+        return self.row[i].expand(self.shape[1])
+
+
 class CobwebIndex:
     """Immutable flattened tree on one GPU.
 
-    mean, var          [Nn, D] float32 (torch on any device, or numpy), BFS order
+    mean               [Nn, D] float32 (torch on any device, or numpy), BFS order
+    var                [Nn, D] float32, or a CompactVar (one scalar per node with full rows
+                       only where the D variances differ)
     parent             [Nn] int64, parent[0] = -1, non-decreasing (BFS)
     node_of_sentence   [n_sent] int64, node holding each sentence id (-1: none)
     level_weights      per-depth weights (CobwebWrapper.py:153-168)
@@ -48,9 +92,18 @@ class CobwebIndex:
         self.device = _dev(device)
         L = self._L = lib()   # the handle belongs to the library that created it
         mean = torch.as_tensor(mean, dtype=torch.float32).to(self.device).contiguous()
-        var = torch.as_tensor(var, dtype=torch.float32).to(self.device).contiguous()
-        if mean.shape != var.shape or mean.dim() != 2:
-            raise ValueError("mean and var must both be [n_nodes, dim]")
+        compact = isinstance(var, CompactVar)
+        if compact:
+            vrow = torch.as_tensor(var.row, dtype=torch.float32).to(self.device).contiguous()
+            an_nodes = np.ascontiguousarray(np.asarray(torch.as_tensor(var.an_nodes).cpu(), dtype=np.int64))
+            an_var = torch.as_tensor(var.an_var, dtype=torch.float32).to(self.device).contiguous()
+            if (mean.dim() != 2 or vrow.shape != (mean.shape[0],) or an_var.dim() != 2
+                    or an_var.shape != (an_nodes.size, mean.shape[1])):
+                raise ValueError("compact var: row [n_nodes], an_var [n_an, dim] for mean [n_nodes, dim]")
+        else:
+            var = torch.as_tensor(var, dtype=torch.float32).to(self.device).contiguous()
+            if mean.shape != var.shape or mean.dim() != 2:
+                raise ValueError("mean and var must both be [n_nodes, dim]")
         parent = np.ascontiguousarray(np.asarray(parent, dtype=np.int64))
         nos = np.ascontiguousarray(np.asarray(node_of_sentence, dtype=np.int64))
         w = np.ascontiguousarray(np.asarray(
@@ -60,10 +113,18 @@ class CobwebIndex:
         self.level_weights = [float(x) for x in w]
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(L.cwq_index_create(self.device.index, self.n_nodes, self.dim, _ptr(mean), _ptr(var),
-                                     parent.ctypes.data_as(ctypes.c_void_p), nos.ctypes.data_as(ctypes.c_void_p),
-                                     self.n_sent, w.ctypes.data_as(ctypes.c_void_p), w.size,
-                                     _stream(self.device), ctypes.byref(h)))
+            if compact:
+                check(L.cwq_index_create_cv(self.device.index, self.n_nodes, self.dim, _ptr(mean), _ptr(vrow),
+                                            an_nodes.ctypes.data_as(ctypes.c_void_p), an_nodes.size, _ptr(an_var),
+                                            parent.ctypes.data_as(ctypes.c_void_p),
+                                            nos.ctypes.data_as(ctypes.c_void_p), self.n_sent,
+                                            w.ctypes.data_as(ctypes.c_void_p), w.size, _stream(self.device),
+                                            ctypes.byref(h)))
+            else:
+                check(L.cwq_index_create(self.device.index, self.n_nodes, self.dim, _ptr(mean), _ptr(var),
+                                         parent.ctypes.data_as(ctypes.c_void_p), nos.ctypes.data_as(ctypes.c_void_p),
+                                         self.n_sent, w.ctypes.data_as(ctypes.c_void_p), w.size,
+                                         _stream(self.device), ctypes.byref(h)))
         self._h = h
         self.info = self._info()
 

@@ -16,7 +16,7 @@ Outputs are the BFS-ordered arrays `CobwebIndex` takes.
 """
 import torch
 
-from .index import welford_groups
+from .index import CompactVar, welford_groups
 from .tree import PRIOR_VAR
 
 
@@ -43,15 +43,21 @@ def _var_of(count, meanSq):
     return meanSq / count[:, None] + float(PRIOR_VAR)
 
 
-def flat_synth(X):
+def flat_synth(X, compact=False):
     """root + N leaves.  Returns dict(mean, var, parent, node_of_sentence) with the
-    BFS order [root, leaf 0, ..., leaf N-1]."""
+    BFS order [root, leaf 0, ..., leaf N-1].  compact=True: var as a CompactVar (the
+    leaves' prior_var as one scalar each, the root's row in full) -- the same index,
+    without the [N+1, D] variance array."""
     N, D = X.shape
     order = torch.arange(N, device=X.device, dtype=torch.int64)
     gptr = torch.tensor([0, N], device=X.device, dtype=torch.int64)
     cnt, mu, m2 = welford_groups(X, order, gptr)
     mean = torch.cat([mu, X])
-    var = torch.cat([_var_of(cnt, m2), torch.full((N, D), float(PRIOR_VAR), device=X.device)])
+    if compact:
+        var = CompactVar(torch.full((N + 1,), float(PRIOR_VAR), device=X.device),
+                         torch.zeros(1, dtype=torch.int64), _var_of(cnt, m2))
+    else:
+        var = torch.cat([_var_of(cnt, m2), torch.full((N, D), float(PRIOR_VAR), device=X.device)])
     parent = torch.zeros(N + 1, dtype=torch.int64)
     parent[0] = -1
     nos = torch.arange(1, N + 1, dtype=torch.int64)

@@ -74,3 +74,33 @@ def test_flatten_matches_oracle(pkg):
 def test_prior_var_matches_reference_bits(pkg):
     g = load_golden("g1_hier_d32")
     assert np.float32(pkg.PRIOR_VAR).tobytes() == np.float32(g["prior_var"]).tobytes()
+
+
+def test_compact_var_create_error_path(pkg):
+    """cwq_index_create_cv validates before any device work."""
+    L = pkg.lib()
+    h = ctypes.c_void_p()
+    rc = L.cwq_index_create_cv(0, 0, 4, None, None, None, 0, None, None, None, 0, None, 0, None, ctypes.byref(h))
+    assert rc == pkg._lib.CWQ_ERR_ARG and b"empty" in L.cwq_last_error()
+    parent = np.array([-1, 0], np.int64)
+    an = np.array([5], np.int64)
+    rc = L.cwq_index_create_cv(0, 2, 4, ctypes.c_void_p(16), ctypes.c_void_p(16), an.ctypes.data_as(ctypes.c_void_p),
+                               1, ctypes.c_void_p(16), parent.ctypes.data_as(ctypes.c_void_p), None, 0, None, 0, None,
+                               ctypes.byref(h))
+    assert rc == pkg._lib.CWQ_ERR_ARG and b"an_nodes out of range" in L.cwq_last_error()
+
+
+def test_compact_var_roundtrip_cpu(pkg):
+    """CompactVar.from_full keeps one scalar per row whose D values share their bits and the
+    other rows in full; full() rebuilds the array bit for bit (the broadcast / index form)."""
+    import torch
+    rng = np.random.default_rng(0)
+    var = np.full((50, 7), pkg.PRIOR_VAR, np.float32)
+    var[0] = rng.random(7).astype(np.float32) + 0.1
+    var[13, 2] = np.float32(0.5)
+    var[20] = np.float32(-0.0)          # one value repeated (bits), even a signed zero
+    cv = pkg.index.CompactVar.from_full(torch.from_numpy(var))
+    assert cv.an_nodes.tolist() == [0, 13] and cv.shape == (50, 7)
+    assert torch.equal(cv.full().view(torch.int32), torch.from_numpy(var).view(torch.int32))
+    np.testing.assert_array_equal(cv[13].numpy(), var[13])
+    np.testing.assert_array_equal(cv[7].numpy(), var[7])

@@ -112,7 +112,11 @@ def _bench_path_worker(rank, ws, port, result_path, strong):
         else:
             args = (None, None, None, None)
         st = {}
-        mean, var, parent, nos = D.broadcast_tree(*args, device="cpu", stats=st)
+        # bench.py's form: the variances stay compact on every rank (no [Nn, D] array)
+        mean, cvar, parent, nos = D.broadcast_tree(*args, device="cpu", stats=st, compact=True)
+        assert isinstance(cvar, cobweb_pkg.load().index.CompactVar)
+        assert cvar.row.shape == (301,) and cvar.an_var.shape == (2, 24)   # root + the anisotropic row
+        var = cvar.full()
         idx = O.FlatIndex(mean.numpy(), var.numpy(), parent, [[0, int(s)] for s in nos])
 
         def scorer(qs, k):
