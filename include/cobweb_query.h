@@ -179,6 +179,10 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  * scan (candidate list overflow / no threshold), filter used (0 exact scan, 1 batch
  * MFMA filter, 2 small-batch stream filter), mean candidate records per query, mean
  * exact reranks per query, threshold-sample rows].
+ * After cwq_categorize, cwq_last_stats reports instead: [queries, queries re-run with
+ * every leaf row materialised (DENSE), queries re-run after a filter list overflow,
+ * queries resolved by counting over the bottleneck order, queries resolved by the heap
+ * replay, 0].
  */
 int cwq_set_filter(cwq_index* idx, int mode);
 int cwq_last_stats(cwq_index* idx, int64_t* out6);

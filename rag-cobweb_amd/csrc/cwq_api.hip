@@ -91,6 +91,7 @@ struct cwq_index {
   float *logdet_int = nullptr, *w_int = nullptr;
   int *par_int = nullptr, *int_child_begin = nullptr, *int_child_end = nullptr, *int_nchild = nullptr;
   int *int_bfs = nullptr, *int_has_sent = nullptr;
+  bool any_int_sent = false;   // an internal node holds sentences (categorize: heap replay only)
   int *int_leaf_a0 = nullptr, *int_leaf_a1 = nullptr, *int_leaf_b0 = nullptr, *int_leaf_b1 = nullptr;
   int64_t *sent_ptr = nullptr, *sent_ids = nullptr;
   int* row_of_sent = nullptr;
@@ -603,6 +604,7 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   if ((rc = ix->upload(&ix->int_nchild, inch, s))) return rc;
   if ((rc = ix->upload(&ix->int_bfs, ibfs, s))) return rc;
   if ((rc = ix->upload(&ix->int_has_sent, ihs, s))) return rc;
+  for (int v : ihs) ix->any_int_sent = ix->any_int_sent || v != 0;
   if ((rc = ix->upload(&ix->int_leaf_a0, la0, s))) return rc;
   if ((rc = ix->upload(&ix->int_leaf_a1, la1, s))) return rc;
   if ((rc = ix->upload(&ix->int_leaf_b0, lb0, s))) return rc;
@@ -1843,6 +1845,17 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     sa.n_found = n_found + q0;
     sa.n_calls = n_calls ? n_calls + q0 : nullptr;
     sa.status = status;
+    sa.par_int = ix->par_int;
+    // the pop sequence by counting over the bottleneck order (cat_count_kernel); the
+    // queries it cannot certify go through the heap replay (CWQ_CAT_COUNT=0: replay all)
+    const char* cce = getenv("CWQ_CAT_COUNT");
+    const bool by_count = ix->NI > 0 && !ix->any_int_sent && !(cce && *cce && atoi(cce) == 0);
+    if (by_count) {
+      HIPCHK(launch_cat_count(sa, s));
+      sa.pre_status = 1;
+    }
+    std::vector<int> cst(by_count ? nqc : 0);
+    if (by_count) HIPCHK(hipMemcpyAsync(cst.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(launch_simulate(sa, s));
     std::vector<int> st(nqc);
     HIPCHK(hipMemcpyAsync(st.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1850,6 +1863,11 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     std::vector<int> redo;
     for (int i = 0; i < nqc; ++i)
       if (st[i] && !fbad[i]) redo.push_back(i);   // filter failures are re-run whole below
+    for (int i = 0; i < nqc; ++i) {
+      if (by_count && cst[i] == 0 && !fbad[i]) ++ix->stats[3];
+      else if (!fbad[i]) ++ix->stats[4];
+    }
+    ix->stats[1] += (int64_t)redo.size();
     if (redo.empty()) continue;
 
     // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
@@ -1908,6 +1926,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
     }
   }
+  ix->stats[2] += (int64_t)fredo.size();
   if (!fredo.empty()) {
     // filter overflow: those queries through the exact path, results scattered back
     const int64_t n = (int64_t)fredo.size();
@@ -1948,11 +1967,14 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   if (nq == 0) return CWQ_OK;
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
+  for (int64_t& t : ix->stats) t = 0;
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
   ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
-  return categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
+  const int rc = categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
+  ix->stats[0] = nq;
+  return rc;
 }
 
 extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order,

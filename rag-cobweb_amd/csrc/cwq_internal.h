@@ -81,6 +81,8 @@ struct SimArgs {
   const int* row_par; const int* row_bfs; const int* row_flags;
   HeapEnt* heap; int64_t heap_cap;
   int64_t* out_nodes; int* n_found; int64_t* n_calls; int* status;
+  const int* par_int;  // parent internal id of every internal node (cat_count_kernel)
+  int pre_status;      // simulate: skip the queries whose status the count pass already set to 0
 };
 
 // Node variances read by the index build.  Full: [n_nodes][D] rows (compute_var of every
@@ -158,6 +160,9 @@ hipError_t launch_node_lp(const float* S_int, int64_t ldI, const float* S_leaf, 
                           const int* node_src, const float* logdet_int, const float* logdet_row, float dconst,
                           int64_t n_nodes, float* out, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, hipStream_t s);
+// Categorize by counting (cat_count_kernel): resolves a query's pop sequence from the
+// bottleneck order (status 0), or leaves it to the heap replay (status 2).
+hipError_t launch_cat_count(const SimArgs& a, hipStream_t s);
 hipError_t launch_welford_groups(const float* X, int D, const int64_t* order, const int64_t* gptr, int64_t n_groups,
                                  float* count, float* mean, float* meanSq, hipStream_t s);
 

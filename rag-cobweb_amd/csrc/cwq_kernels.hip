@@ -1182,6 +1182,7 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= a.nq) return;
+  if (a.pre_status && a.status[q] == 0) return;   // resolved by cat_count_kernel
   HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
   int64_t hn = 0;
   const bool dense = a.R == 0;
@@ -1272,6 +1273,328 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
     if (a.n_calls) a.n_calls[q] = calls;
     a.status[q] = status;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Categorize by counting (LIST mode).  Pops come out in non-increasing path bottleneck
+// b (cwq_internal.h / DESIGN §4.7: a node with larger b is always popped before one
+// with smaller b), so for a value G every node with b > G is popped before every node
+// with b <= G, and the nodes with b == G (a "group") are popped consecutively, in an
+// order only the heap keys inside the group decide.  The query's search therefore is:
+//   * the nodes with b > G, as a SET: their count (pop positions) and the sum of their
+//     children counts (log_prob calls), by one pass over the internal nodes' b;
+//   * the group at G replayed exactly with the heap keys (-lp, parent lp, BFS index);
+// where G is the group holding the pop that ends the search: the k-th retrieval
+// (a leaf of the top-R list: G = its b) or, when max_nodes comes first, the
+// (max_nodes - 1)-th pop (G = the (max_nodes - 1)-th largest b, radix select over the
+// internal nodes' b and the list keys).  Same outputs as simulate_wave_kernel; a
+// query it cannot certify (a group over kCcMaxGroup nodes, retrieved leaves sharing a
+// b, G at or below the list's R-th key, internal nodes holding sentences) gets status
+// 2 and goes to the heap replay.  One 256-thread workgroup per query.
+// ---------------------------------------------------------------------------
+constexpr int kCcThreads = 256;
+constexpr int kCcMaxGroup = 512;
+
+__device__ __forceinline__ uint32_t ord_u32(float v) {   // float order -> unsigned order
+  const uint32_t b = __float_as_uint(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord_f32(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ __launch_bounds__(kCcThreads) void cat_count_kernel(const SimArgs a) {
+  __shared__ float s_lk[64], s_lx[64];
+  __shared__ int s_lr[64], s_lp[64], s_lf[64], s_lb[64];
+  __shared__ int s_hist[2048];
+  __shared__ float s_gs[kCcMaxGroup], s_gp[kCcMaxGroup];
+  __shared__ int s_gt[kCcMaxGroup], s_gn[kCcMaxGroup], s_gpar[kCcMaxGroup], s_gst[kCcMaxGroup];
+  __shared__ int s_ng, s_over, s_sel, s_red_i[kCcThreads / 64];
+  __shared__ long long s_red_l[kCcThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x;
+  if (q >= a.nq) return;
+  const float* BF = a.BF + (size_t)q * a.ldI;
+  const float* LPF = a.LPF + (size_t)q * a.ldI;
+  const int NI = a.NI, R = a.R;
+  const float* lk = a.lkey + (size_t)q * R;
+  // ---- the top-R leaf list (entries up to the first empty one, as the replay) ----
+  if (wave == 0) {
+    const bool lvalid = lane < R && lk[lane] != -CWQ_INF && a.lrow[(size_t)q * R + lane] != 0x7fffffff;
+    s_lk[lane] = lvalid ? lk[lane] : -CWQ_INF;
+    s_lx[lane] = lvalid ? a.laux[(size_t)q * R + lane] : 0.f;
+    const int r = lvalid ? a.lrow[(size_t)q * R + lane] : -1;
+    s_lr[lane] = r;
+    s_lp[lane] = r >= 0 ? a.row_par[r] : -3;
+    s_lf[lane] = r >= 0 ? a.row_flags[r] : 0;
+    s_lb[lane] = r >= 0 ? a.row_bfs[r] : 0;
+    const uint64_t bad = __ballot(lane < R && !lvalid);
+    if (lane == 0) {
+      s_sel = bad ? __builtin_ctzll(bad) : min(R, 64);   // nvalid
+      s_ng = 0;
+      s_over = 0;
+    }
+  }
+  __syncthreads();
+  const int nvalid = s_sel;
+  const float tau = a.complete ? -CWQ_INF : s_lk[R - 1 < 63 ? R - 1 : 63];
+  const int64_t M = a.max_nodes - 1;   // pops 1..M are processed (pop max_nodes breaks first)
+  // G candidate 1: b of the k-th retrieval of the list (list order = b order)
+  int kidx = -1;
+  {
+    int cnt = 0;
+    for (int j = 0; j < nvalid; ++j)
+      if (s_lf[j] & FLAG_HAS_SENT)
+        if (++cnt == a.k) {
+          kidx = j;
+          break;
+        }
+  }
+  auto block_sum_l = [&](long long v) -> long long {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) s_red_l[wave] = v;
+    __syncthreads();
+    long long t = 0;
+    for (int w = 0; w < kCcThreads / 64; ++w) t += s_red_l[w];
+    return t;
+  };
+  // count / children sum of the internal nodes with b > G; collect the group b == G
+  auto count_pass = [&](float G, long long& cnt, long long& sumc) {
+    __syncthreads();
+    if (tid == 0) s_ng = 0;
+    __syncthreads();
+    long long c = 0, sc = 0;
+    for (int i = tid; i < NI; i += kCcThreads) {
+      const float v = BF[i];
+      if (v > G) {
+        ++c;
+        sc += a.int_nchild[i];
+      } else if (v == G) {
+        const int slot = atomicAdd(&s_ng, 1);
+        if (slot < kCcMaxGroup) s_gn[slot] = i;
+      }
+    }
+    cnt = block_sum_l(c);
+    sumc = block_sum_l(sc);
+  };
+  int status = 2;
+  float G = 0.f;
+  long long C = 0, S = 0;
+  bool have = false;
+  if (kidx >= 0 && s_lk[kidx] > tau) {
+    G = s_lk[kidx];
+    count_pass(G, C, S);
+    for (int j = 0; j < nvalid; ++j) C += s_lk[j] > G ? 1 : 0;
+    have = C < M;   // else max_nodes cuts earlier: select below
+  }
+  if (!have) {
+    // the M-th largest b among the internal nodes and the list (above the k-th retrieval's
+    // group when there is one): radix select, 11 + 11 + 10 bits
+    const bool lim = kidx >= 0 && s_lk[kidx] > tau;
+    const float up = lim ? s_lk[kidx] : CWQ_INF;
+    long long total = 0;
+    {
+      long long c = 0;
+      for (int i = tid; i < NI; i += kCcThreads) c += (BF[i] < up || !lim) ? 1 : 0;
+      total = block_sum_l(c);
+      for (int j = 0; j < nvalid; ++j) total += (s_lk[j] < up || !lim) ? 1 : 0;
+    }
+    if (total < M) {
+      // fewer nodes than max_nodes: the search would exhaust the heap -- only exact when
+      // every leaf is in the list and the k-th retrieval does not exist (else covered above)
+      if (!lim && a.complete) {
+        G = -CWQ_INF;   // every node popped: "group" below everything, nothing to replay
+        long long c = 0, sc = 0;
+        for (int i = tid; i < NI; i += kCcThreads) {
+          ++c;
+          sc += a.int_nchild[i];
+        }
+        C = block_sum_l(c) + nvalid;
+        S = block_sum_l(sc);
+        have = true;
+        status = 3;   // marker: exhausted
+      }
+    } else {
+      uint32_t prefix = 0, pmask = 0;
+      long long need = M;
+      const int shifts[3] = {21, 10, 0};
+      const int widths[3] = {11, 11, 10};
+      for (int pass = 0; pass < 3; ++pass) {
+        const int sh = shifts[pass], nb = 1 << widths[pass];
+        for (int b = tid; b < 2048; b += kCcThreads) s_hist[b] = 0;
+        __syncthreads();
+        for (int i = tid; i < NI + nvalid; i += kCcThreads) {
+          const float v = i < NI ? BF[i] : s_lk[i - NI];
+          if (lim && !(v < up)) continue;
+          const uint32_t u = ord_u32(v);
+          if ((u & pmask) != prefix) continue;
+          atomicAdd(&s_hist[(u >> sh) & (nb - 1)], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          long long acc = 0;
+          int b = nb - 1;
+          for (; b > 0; --b) {
+            if (acc + s_hist[b] >= need) break;
+            acc += s_hist[b];
+          }
+          s_sel = b;
+          s_red_l[0] = acc;
+        }
+        __syncthreads();
+        const int b = s_sel;
+        need -= s_red_l[0];
+        prefix |= (uint32_t)b << sh;
+        pmask |= (uint32_t)(nb - 1) << sh;
+        __syncthreads();
+      }
+      G = ord_f32(prefix);
+      if (G > tau || a.complete) {
+        count_pass(G, C, S);
+        for (int j = 0; j < nvalid; ++j) C += s_lk[j] > G ? 1 : 0;
+        have = true;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- outputs: retrievals above G (list order; their b must be distinct), then the
+  // group at G replayed with the heap keys by wave 0 ----
+  if (have && wave == 0) {
+    int found = 0;
+    long long calls = 1 + S;
+    bool ok = s_ng <= kCcMaxGroup;
+    float prev = CWQ_INF;
+    for (int j = 0; j < nvalid && ok; ++j) {
+      if (!(s_lk[j] > G)) break;
+      if (s_lf[j] & FLAG_HAS_SENT) {
+        if (s_lk[j] == prev) ok = false;   // two retrievals in one group above G: replay decides
+        prev = s_lk[j];
+        if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = s_lb[j];
+        ++found;
+      }
+    }
+    if (found >= a.k && status != 3) ok = false;   // cannot happen: the k-th retrieval is in the group
+    if (ok && status != 3) {
+      // the group: internal members (collected) + list rows with b == G
+      int ng = s_ng;
+      for (int j = 0; j < nvalid; ++j)
+        if (s_lk[j] == G) {
+          if (ng >= kCcMaxGroup) {
+            ok = false;
+            break;
+          }
+          if (lane == 0) s_gn[ng] = -(s_lr[j] + 1);
+          ng++;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (ok) {
+        // member keys; s_gpar = the parent's member slot (-1: an origin, pushed at the start);
+        // s_gst: 0 waiting, 1 in the heap, 2 popped
+        for (int m = lane; m < ng; m += 64) {
+          const int nd = s_gn[m];
+          int p;
+          if (nd >= 0) {
+            s_gs[m] = LPF[nd];
+            p = a.par_int[nd];
+            s_gt[m] = a.int_bfs[nd];
+          } else {
+            const int r = -nd - 1;
+            p = a.row_par[r];
+            int j = 0;
+            while (j < nvalid && s_lr[j] != r) ++j;
+            s_gs[m] = s_lx[j];
+            s_gt[m] = a.row_bfs[r];
+          }
+          s_gp[m] = p >= 0 ? LPF[p] : 0.f;
+          int ps = -1;
+          if (p >= 0 && BF[p] == G)
+            for (int m2 = 0; m2 < ng; ++m2)
+              if (s_gn[m2] == p) ps = m2;
+          s_gpar[m] = ps;
+          s_gst[m] = ps < 0 ? 1 : 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        long long pos = C;   // pops before the group
+        bool done = false;
+        while (!done) {
+          // best member in the heap: max score, then min parent score, then min BFS index
+          int best = -1;
+          float bs = -CWQ_INF, bp = CWQ_INF;
+          int bt = 0x7fffffff;
+          for (int m = lane; m < ng; m += 64)
+            if (s_gst[m] == 1) {
+              const float sc = s_gs[m], ps = s_gp[m];
+              const int tb = s_gt[m];
+              if (best < 0 || sc > bs || (sc == bs && (ps < bp || (ps == bp && tb < bt)))) {
+                best = m;
+                bs = sc;
+                bp = ps;
+                bt = tb;
+              }
+            }
+          const int w = [&] {   // wave argmin in heap order
+            float m = best >= 0 ? bs : -CWQ_INF;
+            for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+            bool c = best >= 0 && bs == m;
+            if (__ballot(best >= 0) == 0) return -1;
+            float mp = c ? bp : CWQ_INF;
+            for (int off = 32; off > 0; off >>= 1) mp = fminf(mp, __shfl_xor(mp, off, 64));
+            c = c && bp == mp;
+            int mt = c ? bt : 0x7fffffff;
+            for (int off = 32; off > 0; off >>= 1) mt = min(mt, __shfl_xor(mt, off, 64));
+            c = c && bt == mt;
+            const uint64_t bm = __ballot(c);
+            return bm ? __builtin_ctzll(bm) : -1;
+          }();
+          if (w < 0) {   // the group ran out before the search ended: not certified
+            ok = false;
+            break;
+          }
+          const int m = __shfl(best, w, 64);
+          ++pos;
+          if (pos >= a.max_nodes) break;   // visited >= max_nodes: not processed
+          const int nd = s_gn[m];
+          if (lane == 0) s_gst[m] = 2;
+          if (nd < 0) {
+            const int r = -nd - 1;
+            if (a.row_flags[r] & FLAG_HAS_SENT) {
+              if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = s_gt[m];
+              ++found;
+              if (found == a.k) done = true;
+            }
+          } else {
+            calls += a.int_nchild[nd];
+            for (int m2 = lane; m2 < ng; m2 += 64)
+              if (s_gpar[m2] == m) s_gst[m2] = 1;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+      }
+    }
+    if (ok) {
+      status = 0;
+      if (lane == 0) {
+        a.n_found[q] = found < a.k ? found : a.k;
+        if (a.n_calls) a.n_calls[q] = calls;
+      }
+    } else {
+      status = 2;
+    }
+  }
+  if (tid == 0) a.status[q] = have ? status : 2;
+}
+
+hipError_t launch_cat_count(const SimArgs& a, hipStream_t s) {
+  if (a.R <= 0 || a.R > 64 || a.NI <= 0 || !a.par_int) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cat_count_kernel, dim3((unsigned)a.nq), dim3(kCcThreads), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_simulate(const SimArgs& a, hipStream_t s) {

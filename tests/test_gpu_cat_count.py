@@ -1,0 +1,90 @@
+"""Basic categorize by counting (cat_count_kernel) == the exact heap replay.
+
+The counting path resolves a query from the bottleneck order: every node with path
+bottleneck b > G is popped before any node with b <= G, so the search up to
+the group G that ends it is a SET (a count and a children sum over the internal nodes),
+and only the group at G is replayed with the heap keys of CobwebTorchTree.py:243-285.
+Here it must give exactly what the full heap replay gives (CWQ_CAT_COUNT=0): retrieved
+nodes in pop order, n_found, log_prob call counts -- on two-level and deep trees, with
+max_nodes cutting before / inside / after the retrievals, k from 1 to 64, perturbed
+queries (a leaf closer than its parent: b ties along the path) and duplicated rows
+(retrievals sharing one b: left to the replay).  The G1/G2/G4/G5 reference goldens go
+through the counting path in tests/test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg
+
+
+def _both(ix, Q, k, max_nodes):
+    os.environ["CWQ_CAT_COUNT"] = "0"
+    try:
+        ref = ix.categorize(Q, k, max_nodes)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["CWQ_CAT_COUNT"]
+    got = ix.categorize(Q, k, max_nodes)
+    torch.cuda.synchronize()
+    st = ix.last_categorize_stats()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    return st
+
+
+def _trees(pkg):
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(21)
+    X = pkg.synth.synthetic_corpus(60_000, 48, seed=22)
+    X[1000:1010] = X[2000]                                   # duplicated rows: equal b among retrievals
+    lab = torch.randint(0, 600, (X.shape[0],), generator=g, device="cuda:0")
+    yield "two-level G=600", pkg.synth.two_level_synth(X, lab), X
+    lab = torch.randint(0, 20_000, (X.shape[0],), generator=g, device="cuda:0")
+    yield "two-level G=20000", pkg.synth.two_level_synth(X, lab), X
+    yield "balanced 4/6", pkg.synth.balanced_synth(X, 4, 6), X
+    yield "balanced 10/3", pkg.synth.balanced_synth(X, 10, 3), X
+
+
+def test_count_equals_replay(gpu):
+    totals = {"by_count": 0, "by_replay": 0}
+    for name, t, X in _trees(gpu):
+        ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+        Q, _ = gpu.synth.synthetic_queries(X, 512, seed=23)
+        Q[5] = X[2000]                                       # exactly on the duplicated row
+        Q[6] = X[1000] + 1e-3
+        n_int = ix.info["internal_nodes"]
+        for k, mx in [(10, 100000), (1, 100000), (64, 100000), (10, n_int // 2), (10, n_int + 5), (5, 7),
+                      (10, 2), (64, n_int + 40)]:
+            st = _both(ix, Q, k, mx)
+            totals["by_count"] += st["by_count"]
+            totals["by_replay"] += st["by_replay"]
+        ix.close()
+    # the counting path must carry the bulk of the queries
+    assert totals["by_count"] > 0.8 * (totals["by_count"] + totals["by_replay"]), totals
+
+
+def test_count_flat_tree_and_small(gpu):
+    X = gpu.synth.synthetic_corpus(30_000, 32, seed=31)
+    t = gpu.synth.flat_synth(X)
+    ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=32)
+    for k, mx in [(10, 100000), (64, 100000), (10, 5), (10, 1), (1, 2)]:
+        st = _both(ix, Q, k, mx)
+        assert st["by_count"] >= 0.9 * Q.shape[0], st
+    ix.close()
+    # a tree smaller than the list (every leaf in it): the search exhausts the heap
+    t = gpu.synth.two_level_synth(X[:40].contiguous(), torch.arange(40, device="cuda:0") % 3)
+    ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    for k, mx in [(10, 100000), (39, 100000), (40, 100000), (41, 100000), (10, 3)]:
+        if k <= 64:
+            _both(ix, Q[:50], k, mx)
+    ix.close()
