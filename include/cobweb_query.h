@@ -229,6 +229,40 @@ int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_
                     const float* x, int32_t* flag, void* stream);
 
 /*
+ * Device-resident incremental fit (F1): CobwebTorchTree.cobweb's insert loop
+ * (CobwebTorchTree.py:143-233; CobwebTorchNode.py:57-85, 374-666) run entirely on the
+ * GPU -- the tree (statistics, parent links, ordered child lists) in device memory, one
+ * workgroup per handle inserting the rows in order, every decision on the device, the
+ * reference's random() draws from Python's MT19937 stream run on the device.  Builds the
+ * same trees as the host-driven cwq_fit_kl / cwq_fit_node_op path (fit.py).  dim <= 1024.
+ *   cwq_fit_create   a handle with room for cap_nodes nodes
+ *   cwq_fit_load     the tree in slots 0..n_nodes-1: parent (host, -1 at the root),
+ *                    children in list order as CSR (host child_ptr [n+1], child_idx),
+ *                    count / mean / meanSq (host, [n], [n*dim]); mt_state (host [625]) =
+ *                    Python's random.getstate()[1] (624 words + index)
+ *   cwq_fit_insert   X (device [n*dim]): the rows inserted in order; leaf_out (device
+ *                    [n] int32) = the slot of the node each row ended in (ifit's return
+ *                    value).  info (host int64[4]) = {rows done, random() draws, status,
+ *                    slots in use}; status 1: the node pool / child arena needs room --
+ *                    export, load into a larger handle and insert the remaining rows
+ *   cwq_fit_export   out2 = {slots in use, root}; parent (-2: a node a split removed),
+ *                    child CSR, count, mean, meanSq (host, [cap] / [cap*dim]) and the
+ *                    random() state after the draws (host [625])
+ *   cwq_mt19937_draw n draws of Python's random.random() from state625 (host; updates it)
+ */
+typedef struct cwq_fit cwq_fit;
+int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t cap_nodes, cwq_fit** out);
+int cwq_fit_destroy(cwq_fit* h);
+int cwq_fit_load(cwq_fit* h, int32_t n_nodes, int32_t root, const int32_t* parent, const int32_t* child_ptr,
+                 const int32_t* child_idx, const float* count, const float* mean, const float* meanSq,
+                 const uint32_t* mt_state, void* stream);
+int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* leaf_out, int64_t* info, void* stream);
+int cwq_fit_export(cwq_fit* h, int32_t* out2, int32_t* parent, int32_t* child_ptr, int32_t* child_idx, float* count,
+                   float* mean, float* meanSq, uint32_t* mt_state, void* stream);
+const char* cwq_fit_last_error(void);
+int cwq_mt19937_draw(uint32_t* state625, int64_t n, double* out);
+
+/*
  * PCA + ICA whitening transform (F4).  Replaces PCAICAWhiteningModel.transform
  * (src/whitening/pca_ica.py:30-51), the embedding normalisation of the "PCA + ICA"
  * benchmark rows and of config C5:

@@ -43,6 +43,13 @@ SIGNATURES = {
     "cwq_fit_kl": (_c.c_int, [_P, _P, _P, _I32, _P, _c.c_float, _I32, _P, _I32, _P, _P]),
     "cwq_fit_node_op": (_c.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "cwq_welford_groups": (_c.c_int, [_P, _I64, _I32, _P, _P, _I64, _P, _P, _P, _P]),
+    "cwq_fit_create": (_c.c_int, [_c.c_int, _I32, _c.c_float, _I32, _c.POINTER(_P)]),
+    "cwq_fit_destroy": (_c.c_int, [_P]),
+    "cwq_fit_load": (_c.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwq_fit_insert": (_c.c_int, [_P, _P, _I64, _P, _P, _P]),
+    "cwq_fit_export": (_c.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwq_fit_last_error": (_c.c_char_p, []),
+    "cwq_mt19937_draw": (_c.c_int, [_P, _I64, _P]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,850 @@
+// libcwq: device-resident incremental fit (ifit) -- the whole insert loop
+// of CobwebTorchTree.cobweb (CobwebTorchTree.py:143-233) on the GPU, with no host
+// round trip per insert or per level.
+//
+// The tree lives in device memory: a pool of node statistics (count, mean, meanSq =
+// Welford M2, CobwebTorchNode.py:31-68), parent links and per-node child lists in list
+// order (slabs of an arena; append at the end, remove with the tail shifted left, as
+// Python's list.append / list.remove).  One 1024-thread workgroup runs the inserts in
+// order; per tree level it computes every child's KL terms (one wave per child), then
+// one thread makes the reference's scalar decisions in its float32 op order:
+//   two_best_children (CobwebTorchNode.py:374-420): gain = p1*KL(c+x || P+x) -
+//     p2*KL(c || P+x), sorted by (gain, count, random()) descending;
+//   pu_for_insert / pu_for_new_child / pu_for_merge / pu_for_split (:422-650), each a
+//     sequential float32 sum over the children (Python's `score += ...`);
+//   get_best_operation (CobwebTorchTree.py:287-372 via fit.py): max of (pu, random(), name);
+// and applies best / new / merge / split / fringe split / exact-match increment to the
+// device tree.  random() is Python's own MT19937 stream (genrand_res53), run on the
+// device from the state the host hands over (random.getstate()) and handed back after,
+// so the draws -- b per level for the child sort, then best, new, [merge], [split] --
+// are the reference's.  KL (compute_score, CobwebTorchTree.py:344-364) per element in
+// the reference's fp32 op order (contraction off), the two D-sums in fp64 per lane
+// (lane stride 64) then a butterfly, rounded once -- exactly cwq_fit_kl's arithmetic,
+// so this and the host-driven fitter (fit.py TreeFitter.ifit) build identical trees.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/cobweb_query.h"
+
+namespace cwq {
+
+// ---------------------------------------------------------------------------
+// MT19937 with Python's random.random() (genrand_res53): state = 624 words + index
+// ---------------------------------------------------------------------------
+constexpr int kMtN = 624, kMtM = 397;
+__host__ __device__ inline uint32_t mt_u32(uint32_t* mt, int& idx) {
+  if (idx >= kMtN) {
+    int kk = 0;
+    uint32_t y;
+    for (; kk < kMtN - kMtM; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + kMtM] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    for (; kk < kMtN - 1; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + (kMtM - kMtN)] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    y = (mt[kMtN - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+    mt[kMtN - 1] = mt[kMtM - 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    idx = 0;
+  }
+  uint32_t y = mt[idx++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+__host__ __device__ inline double mt_random(uint32_t* mt, int& idx) {
+  const uint32_t a = mt_u32(mt, idx) >> 5, b = mt_u32(mt, idx) >> 6;
+  return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+
+// ---------------------------------------------------------------------------
+// Device tree
+// ---------------------------------------------------------------------------
+struct FitDev {
+  int D;
+  float pv;
+  int cap;                      // node slots
+  float *count, *mean, *meanSq; // [cap], [cap][D]
+  int *parent, *ccnt, *ccap;    // [cap]
+  int64_t* coff;                // [cap] child slab offset in the arena
+  int* arena;
+  int64_t arena_cap;
+  int* ctrl;                    // [0] used [2] root [3] status [4] mt index
+  int64_t* ctrl64;              // [0] arena_top [1] rows done [2] randoms drawn
+  uint32_t* mt;                 // [624]
+  float *kres, *gain, *tall, *tins, *ncv;   // per-level scratch [cap]
+  int* jobs;                    // [cap] split job nodes
+};
+
+constexpr int kFdThreads = 1024;
+constexpr int kFdWaves = kFdThreads / 64;
+constexpr int kFdMaxD = 1024;   // 7 D-vectors + the MT state stay within 64 KiB of LDS
+constexpr int kFdChunk = 1024;
+enum { FD_OK = 0, FD_ROOM = 1, FD_FULL = 2 };
+
+struct FdShared {
+  float x[kFdMaxD], mu2[kFdMaxD], v2[kFdMaxD], lv2[kFdMaxD];
+  float muP[kFdMaxD], vP[kFdMaxD], lvP[kFdMaxD];
+  uint32_t mt[kMtN];
+  float cg[kFdChunk], cn[kFdChunk];
+  int ci[8];
+  float cf[8];
+  double cr[2];   // random() of "best" and "new"
+  int flag;
+};
+
+#pragma clang fp contract(off)
+
+// WG-wide node operations (every thread calls; barriers inside)
+__device__ void fd_zero(const FitDev& f, int s) {
+#pragma clang fp contract(off)
+  for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
+    f.mean[(size_t)s * f.D + d] = 0.f;
+    f.meanSq[(size_t)s * f.D + d] = 0.f;
+  }
+  if (threadIdx.x == 0) f.count[s] = 0.f;
+  __syncthreads();
+}
+
+// increment_counts (CobwebTorchNode.py:57-68)
+__device__ void fd_increment(const FitDev& f, int s, const float* x) {
+#pragma clang fp contract(off)
+  const float cd = f.count[s];
+  for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
+    const size_t o = (size_t)s * f.D + d;
+    const float cnt = cd + 1.0f;
+    const float delta = x[d] - f.mean[o];
+    const float m = f.mean[o] + delta / cnt;
+    f.meanSq[o] = f.meanSq[o] + delta * (x[d] - m);
+    f.mean[o] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) f.count[s] = cd + 1.0f;
+  __syncthreads();
+}
+
+// update_counts_from_node (CobwebTorchNode.py:70-85)
+__device__ void fd_combine(const FitDev& f, int dst, int src) {
+#pragma clang fp contract(off)
+  const float cd = f.count[dst], cs = f.count[src];
+  for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
+    const size_t o = (size_t)dst * f.D + d, os = (size_t)src * f.D + d;
+    const float delta = f.mean[os] - f.mean[o];
+    const float tot = cd + cs;
+    f.meanSq[o] = (f.meanSq[o] + f.meanSq[os]) + (delta * delta) * ((cd * cs) / tot);
+    f.mean[o] = (cd * f.mean[o] + cs * f.mean[os]) / tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) f.count[dst] = cd + cs;
+  __syncthreads();
+}
+
+// is_exact_match (CobwebTorchNode.py:652-666, torch.isclose defaults)
+__device__ bool fd_exact(const FitDev& f, FdShared& sh, int s) {
+#pragma clang fp contract(off)
+  if (threadIdx.x == 0) sh.flag = 1;
+  __syncthreads();
+  const float cd = f.count[s];
+  bool ok = true;
+  for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
+    const size_t o = (size_t)s * f.D + d;
+    const float sd = sqrtf(f.meanSq[o] / cd);
+    if (!(fabsf(sd) <= 1e-8f)) ok = false;
+    if (!(fabsf(sh.x[d] - f.mean[o]) <= 1e-8f + 1e-5f * fabsf(f.mean[o]))) ok = false;
+  }
+  if (!ok) sh.flag = 0;
+  __syncthreads();
+  const bool r = sh.flag != 0;
+  __syncthreads();
+  return r;
+}
+
+// thread 0; -1: pool full.  Slots are never reused within a load (a node freed by a split
+// keeps its slot, marked parent = -2), so the host maps every slot it loaded to the same
+// node object afterwards; slot numbers never enter a decision.
+__device__ int fd_alloc(const FitDev& f) {
+  if (f.ctrl[0] >= f.cap) return -1;
+  const int s = f.ctrl[0]++;
+  f.parent[s] = -1;
+  f.ccnt[s] = 0;
+  f.ccap[s] = 0;
+  f.coff[s] = 0;
+  return s;
+}
+
+// a new zeroed node (WG-wide); s_out via LDS
+__device__ int fd_new_node(const FitDev& f, FdShared& sh) {
+  if (threadIdx.x == 0) {
+    sh.ci[0] = fd_alloc(f);
+    if (sh.ci[0] < 0) f.ctrl[3] = FD_FULL;
+  }
+  __syncthreads();
+  const int s = sh.ci[0];
+  __syncthreads();
+  if (s >= 0) fd_zero(f, s);
+  return s;
+}
+
+// children[p].append(c)
+__device__ void fd_append(const FitDev& f, FdShared& sh, int p, int c) {
+  if (threadIdx.x == 0) {
+    sh.ci[1] = 0;
+    if (f.ccnt[p] == f.ccap[p]) {   // grow: a new slab of twice the capacity at the arena top
+      const int nc = f.ccap[p] < 4 ? 4 : 2 * f.ccap[p];
+      const int64_t off = f.ctrl64[0];
+      if (off + nc > f.arena_cap) {
+        f.ctrl[3] = FD_FULL;
+      } else {
+        f.ctrl64[0] = off + nc;
+        sh.ci[1] = 1;
+        sh.ci[2] = (int)(f.coff[p] >> 32);
+        sh.ci[3] = (int)(f.coff[p] & 0xffffffff);
+        f.coff[p] = off;
+        f.ccap[p] = nc;
+      }
+    }
+  }
+  __syncthreads();
+  if (sh.ci[1]) {   // move the list into the new slab
+    const int64_t old = ((int64_t)sh.ci[2] << 32) | (uint32_t)sh.ci[3];
+    const int64_t nw = f.coff[p];
+    const int n = f.ccnt[p];
+    for (int i = threadIdx.x; i < n; i += kFdThreads) f.arena[nw + i] = f.arena[old + i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && f.ctrl[3] != FD_FULL) {
+    f.arena[f.coff[p] + f.ccnt[p]] = c;
+    f.ccnt[p] = f.ccnt[p] + 1;
+  }
+  __syncthreads();
+}
+
+// children[p].remove(c): first occurrence, the tail shifted left by one
+__device__ void fd_remove(const FitDev& f, FdShared& sh, int p, int c) {
+  const int n = f.ccnt[p];
+  const int64_t base = f.coff[p];
+  if (threadIdx.x == 0) sh.ci[4] = n;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += kFdThreads)
+    if (f.arena[base + i] == c) atomicMin(&sh.ci[4], i);
+  __syncthreads();
+  const int j = sh.ci[4];
+  __syncthreads();
+  if (j >= n) return;
+  for (int c0 = j; c0 < n - 1; c0 += kFdThreads) {
+    const int i = c0 + threadIdx.x;
+    const int v = i < n - 1 ? f.arena[base + i + 1] : 0;
+    __syncthreads();
+    if (i < n - 1) f.arena[base + i] = v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) f.ccnt[p] = n - 1;
+  __syncthreads();
+}
+
+// KL(cand || ref) of one wave: per-lane fp64 sums over d = lane, lane + 64, ..., then the
+// butterfly, then (sa + sb - D) / 2 in fp32 -- cwq_fit_kl's arithmetic
+__device__ __forceinline__ float fd_kl_finish(double sa, double sb, int D) {
+#pragma clang fp contract(off)
+  for (int off = 32; off > 0; off >>= 1) {
+    sa += __shfl_xor(sa, off, 64);
+    sb += __shfl_xor(sb, off, 64);
+  }
+  float score = (float)sa;
+  score = score + (float)sb;
+  score = score - (float)D;
+  score = score / 2.0f;
+  return score;
+}
+
+__device__ __forceinline__ void fd_insert_mv(float c, float m, float m2, float x, float pv, float& mo, float& vo) {
+#pragma clang fp contract(off)
+  const float cnt = c + 1.0f;
+  const float delta = x - m;
+  const float mm = m + delta / cnt;
+  const float mm2 = m2 + delta * (x - mm);
+  mo = mm;
+  vo = mm2 / cnt + pv;
+}
+
+// (gain, count, random) descending; ties keep list order (Python's stable sort)
+__device__ __forceinline__ bool fd_rel_before(float g1, float n1, double r1, int i1, float g2, float n2, double r2,
+                                              int i2) {
+  if (g1 != g2) return g1 > g2;
+  if (n1 != n2) return n1 > n2;
+  if (r1 != r2) return r1 > r2;
+  return i1 < i2;
+}
+
+__global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, const float* __restrict__ X, int64_t n,
+                                                                int* leaf_out) {
+#pragma clang fp contract(off)
+  extern __shared__ char fd_smem[];
+  FdShared& sh = *reinterpret_cast<FdShared*>(fd_smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int D = f.D;
+  const float pv = f.pv;
+  for (int i = tid; i < kMtN; i += kFdThreads) sh.mt[i] = f.mt[i];
+  int mt_idx = f.ctrl[4];   // thread 0's copy is the live one
+  double drawn = 0;
+  __syncthreads();
+  int64_t row = f.ctrl64[1];
+  for (; row < n; ++row) {
+    // room for one more insert: arena below half, a few free slots (host compacts/grows)
+    if (f.ctrl64[0] > f.arena_cap / 2 || f.ctrl[0] + 64 > f.cap) {
+      if (tid == 0) f.ctrl[3] = FD_ROOM;
+      break;
+    }
+    for (int d = tid; d < D; d += kFdThreads) sh.x[d] = X[row * D + d];
+    __syncthreads();
+    int cur = f.ctrl[2];
+    int leaf = -1;
+    while (cur >= 0) {
+      const int b = f.ccnt[cur];
+      if (b == 0) {
+        // leaf: exact match or the empty root -> increment (CobwebTorchTree.py:184-188)
+        if (f.count[cur] == 0.f || fd_exact(f, sh, cur)) {
+          fd_increment(f, cur, sh.x);
+          leaf = cur;
+          break;
+        }
+        // fringe split (:190-204): new = copy of cur in cur's place, cur and a new leaf under it
+        const int nw = fd_new_node(f, sh);
+        if (nw < 0) break;
+        const int gp = f.parent[cur];
+        if (tid == 0) f.parent[nw] = gp;
+        __syncthreads();
+        fd_combine(f, nw, cur);
+        if (tid == 0) f.parent[cur] = nw;
+        __syncthreads();
+        fd_append(f, sh, nw, cur);
+        if (gp >= 0) {
+          fd_remove(f, sh, gp, cur);
+          fd_append(f, sh, gp, nw);
+        } else if (tid == 0) {
+          f.ctrl[2] = nw;
+        }
+        __syncthreads();
+        fd_increment(f, nw, sh.x);
+        const int ch = fd_new_node(f, sh);
+        if (ch < 0) break;
+        if (tid == 0) f.parent[ch] = nw;
+        __syncthreads();
+        fd_increment(f, ch, sh.x);
+        fd_append(f, sh, nw, ch);
+        leaf = ch;
+        break;
+      }
+      // ---- internal node: the CU terms of every operation ----
+      const float cP = f.count[cur];
+      for (int d = tid; d < D; d += kFdThreads) {   // P + x (mean_var_insert of the parent)
+        float m, v;
+        fd_insert_mv(cP, f.mean[(size_t)cur * D + d], f.meanSq[(size_t)cur * D + d], sh.x[d], pv, m, v);
+        sh.mu2[d] = m;
+        sh.v2[d] = v;
+        sh.lv2[d] = logf(v);
+      }
+      __syncthreads();
+      const int64_t cbase = f.coff[cur];
+      // per child: U = KL(c + x || P + x), T = KL(c || P + x); the new leaf's KL(new || P + x)
+      for (int j = wave; j <= b; j += kFdWaves) {
+        double sU = 0.0, tU = 0.0, sT = 0.0, tT = 0.0;
+        if (j < b) {
+          const int c = f.arena[cbase + j];
+          const float cc = f.count[c];
+          for (int d = lane; d < D; d += 64) {
+            const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
+            const float mu2 = sh.mu2[d], v2 = sh.v2[d], lv2 = sh.lv2[d];
+            float mu1, v1;
+            fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
+            {
+              const float a = lv2 - logf(v1);
+              const float df = mu1 - mu2;
+              const float bb = (v1 + df * df) / v2;
+              sU += (double)a;
+              tU += (double)bb;
+            }
+            mu1 = m;
+            v1 = m2 / cc + pv;
+            {
+              const float a = lv2 - logf(v1);
+              const float df = mu1 - mu2;
+              const float bb = (v1 + df * df) / v2;
+              sT += (double)a;
+              tT += (double)bb;
+            }
+          }
+          const float U = fd_kl_finish(sU, tU, D), T = fd_kl_finish(sT, tT, D);
+          if (lane == 0) {
+            f.kres[2 * j] = U;
+            f.kres[2 * j + 1] = T;
+          }
+        } else {
+          for (int d = lane; d < D; d += 64) {
+            const float mu1 = sh.x[d], v1 = 0.f + pv;
+            const float a = sh.lv2[d] - logf(v1);
+            const float df = mu1 - sh.mu2[d];
+            const float bb = (v1 + df * df) / sh.v2[d];
+            sU += (double)a;
+            tU += (double)bb;
+          }
+          const float K = fd_kl_finish(sU, tU, D);
+          if (lane == 0) f.kres[2 * b] = K;
+        }
+      }
+      __syncthreads();
+      // fp32 terms per child (parallel; numpy's elementwise float32 ops of fit.py)
+      const float nP1 = cP + 1.0f;
+      for (int j = tid; j < b; j += kFdThreads) {
+        const int c = f.arena[cbase + j];
+        const float nc = f.count[c];
+        const float U = f.kres[2 * j], T = f.kres[2 * j + 1];
+        const float p1 = (nc + 1.0f) / nP1, p2 = nc / nP1;
+        f.gain[j] = p1 * U - p2 * T;
+        f.tall[j] = p2 * T;
+        f.tins[j] = p1 * U;
+        f.ncv[j] = nc;
+      }
+      __syncthreads();
+      // two_best_children: one random() per child, in list order (chunks staged in LDS)
+      int i1 = -1, i2 = -1;
+      float g1 = 0.f, n1 = 0.f, g2 = 0.f, n2 = 0.f;
+      double r1 = 0.0, r2 = 0.0;
+      for (int c0 = 0; c0 < b; c0 += kFdChunk) {
+        const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
+        for (int j = tid; j < m; j += kFdThreads) {
+          sh.cg[j] = f.gain[c0 + j];
+          sh.cn[j] = f.ncv[c0 + j];
+        }
+        __syncthreads();
+        if (tid == 0) {
+          for (int j = 0; j < m; ++j) {
+            const double r = mt_random(sh.mt, mt_idx);
+            drawn += 1;
+            const float g = sh.cg[j], nn = sh.cn[j];
+            const int id = c0 + j;
+            if (i1 < 0 || fd_rel_before(g, nn, r, id, g1, n1, r1, i1)) {
+              i2 = i1; g2 = g1; n2 = n1; r2 = r1;
+              i1 = id; g1 = g; n1 = nn; r1 = r;
+            } else if (i2 < 0 || fd_rel_before(g, nn, r, id, g2, n2, r2, i2)) {
+              i2 = id; g2 = g; n2 = nn; r2 = r;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      // pu sums (sequential float32, list order) and the operation choice: thread 0
+      if (tid == 0) {
+        float s_all = 0.f, s_ins = 0.f, s_keep = 0.f;
+        bool first_all = true, first_ins = true, first_keep = true;
+        for (int j = 0; j < b; ++j) {
+          const float ta = f.tall[j];
+          const float ti = j == i1 ? f.tins[j] : ta;
+          s_all = first_all ? ta : s_all + ta;
+          first_all = false;
+          s_ins = first_ins ? ti : s_ins + ti;
+          first_ins = false;
+          if (j != i1 && j != i2) {
+            s_keep = first_keep ? ta : s_keep + ta;
+            first_keep = false;
+          }
+        }
+        const float knew = f.kres[2 * b];
+        const float pu_best = s_ins / (float)b;
+        const float pu_new = (s_all + (1.0f / nP1) * knew) / (float)(b + 1);
+        const double r_best = mt_random(sh.mt, mt_idx), r_new = mt_random(sh.mt, mt_idx);
+        drawn += 2;
+        sh.ci[0] = f.arena[cbase + i1];
+        sh.ci[1] = i2 >= 0 ? f.arena[cbase + i2] : -1;
+        sh.ci[2] = i1;
+        sh.ci[3] = i2;
+        sh.ci[5] = (b > 2 && i2 >= 0) ? 1 : 0;          // merge applies
+        sh.ci[6] = f.ccnt[sh.ci[0]] > 0 ? 1 : 0;        // split applies
+        sh.cf[0] = pu_best;
+        sh.cf[1] = pu_new;
+        sh.cf[2] = s_keep;
+        sh.cr[0] = r_best;
+        sh.cr[1] = r_new;
+      }
+      __syncthreads();
+      const int b1 = sh.ci[0], b2 = sh.ci[1];
+      const bool do_merge = sh.ci[5] != 0, do_split = sh.ci[6] != 0;
+      const float pu_best = sh.cf[0], pu_new = sh.cf[1], s_keep = sh.cf[2];
+      const double r_best = sh.cr[0], r_new = sh.cr[1];
+      // merge / split terms
+      float k_merge = 0.f;
+      int n_split = 0;
+      if (do_split) {
+        for (int d = tid; d < D; d += kFdThreads) {   // P without x
+          const float m = f.mean[(size_t)cur * D + d], v = f.meanSq[(size_t)cur * D + d] / cP + pv;
+          sh.muP[d] = m;
+          sh.vP[d] = v;
+          sh.lvP[d] = logf(v);
+        }
+        // the split's nodes: cur's children except b1, then b1's children (list order)
+        const int nb1 = f.ccnt[b1];
+        const int64_t b1base = f.coff[b1];
+        n_split = b - 1 + nb1;
+        for (int j = tid; j < b; j += kFdThreads) {
+          if (j == sh.ci[2]) continue;
+          f.jobs[j < sh.ci[2] ? j : j - 1] = f.arena[cbase + j];
+        }
+        for (int j = tid; j < nb1; j += kFdThreads) f.jobs[b - 1 + j] = f.arena[b1base + j];
+      }
+      __syncthreads();
+      if (do_merge && wave == kFdWaves - 1) {   // mean_var_merge(b1, b2) with x vs P + x
+        const float c1 = f.count[b1], c2 = f.count[b2];
+        double sa = 0.0, sb = 0.0;
+        for (int d = lane; d < D; d += 64) {
+          const float ma = f.mean[(size_t)b1 * D + d], mb = f.mean[(size_t)b2 * D + d];
+          const float sa2 = f.meanSq[(size_t)b1 * D + d], sb2 = f.meanSq[(size_t)b2 * D + d];
+          const float delta = mb - ma;
+          const float tot = c1 + c2;
+          float m2 = (sa2 + sb2) + (delta * delta) * ((c1 * c2) / tot);
+          float m = (c1 * ma + c2 * mb) / tot;
+          const float cnt = tot + 1.0f;
+          const float xd = sh.x[d];
+          const float dl = xd - m;
+          m = m + dl / cnt;
+          m2 = m2 + dl * (xd - m);
+          const float v1 = m2 / cnt + pv;
+          const float a = sh.lv2[d] - logf(v1);
+          const float df = m - sh.mu2[d];
+          const float bb = (v1 + df * df) / sh.v2[d];
+          sa += (double)a;
+          sb += (double)bb;
+        }
+        const float K = fd_kl_finish(sa, sb, D);
+        if (lane == 0) sh.cf[3] = K;
+      }
+      if (do_split) {
+        for (int j = wave; j < n_split; j += kFdWaves) {   // KL(c || P) (cand type 0, ref P)
+          const int c = f.jobs[j];
+          const float cc = f.count[c];
+          double sa = 0.0, sb = 0.0;
+          for (int d = lane; d < D; d += 64) {
+            const float mu1 = f.mean[(size_t)c * D + d], v1 = f.meanSq[(size_t)c * D + d] / cc + pv;
+            const float a = sh.lvP[d] - logf(v1);
+            const float df = mu1 - sh.muP[d];
+            const float bb = (v1 + df * df) / sh.vP[d];
+            sa += (double)a;
+            sb += (double)bb;
+          }
+          const float K = fd_kl_finish(sa, sb, D);
+          if (lane == 0) f.kres[2 * b + 1 + j] = K;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        // get_best_operation: max of (pu, random(), name); names "best" < "merge" < "new" < "split"
+        float bp = pu_best;
+        double br = r_best;
+        int bn = 0;   // 0 best, 1 merge, 2 new, 3 split (the names' order)
+        auto offer = [&](float pu, double r, int nm) {
+          if (pu > bp || (pu == bp && (r > br || (r == br && nm > bn)))) {
+            bp = pu;
+            br = r;
+            bn = nm;
+          }
+        };
+        offer(pu_new, r_new, 2);
+        if (do_merge) {
+          k_merge = sh.cf[3];
+          const float pm = ((f.count[b1] + f.count[b2]) + 1.0f) / nP1;
+          const float pu_merge = (s_keep + pm * k_merge) / (float)(b - 1);
+          const double r = mt_random(sh.mt, mt_idx);
+          drawn += 1;
+          offer(pu_merge, r, 1);
+        }
+        if (do_split) {
+          float s = 0.f;
+          bool first = true;
+          for (int j = 0; j < n_split; ++j) {
+            const float t = (f.count[f.jobs[j]] / cP) * f.kres[2 * b + 1 + j];
+            s = first ? t : s + t;
+            first = false;
+          }
+          const float pu_split = s / (float)(b - 1 + f.ccnt[b1]);
+          const double r = mt_random(sh.mt, mt_idx);
+          drawn += 1;
+          offer(pu_split, r, 3);
+        }
+        sh.ci[7] = bn;
+      }
+      __syncthreads();
+      const int op = sh.ci[7];
+      __syncthreads();
+      if (op == 0) {          // best: into b1
+        fd_increment(f, cur, sh.x);
+        cur = b1;
+      } else if (op == 2) {   // new child
+        fd_increment(f, cur, sh.x);
+        const int ch = fd_new_node(f, sh);
+        if (ch < 0) break;
+        if (tid == 0) f.parent[ch] = cur;
+        __syncthreads();
+        fd_increment(f, ch, sh.x);
+        fd_append(f, sh, cur, ch);
+        leaf = ch;
+        break;
+      } else if (op == 1) {   // merge (CobwebTorchNode.py:517-548)
+        fd_increment(f, cur, sh.x);
+        const int nc = fd_new_node(f, sh);
+        if (nc < 0) break;
+        if (tid == 0) f.parent[nc] = cur;
+        __syncthreads();
+        fd_combine(f, nc, b1);
+        fd_combine(f, nc, b2);
+        if (tid == 0) {
+          f.parent[b1] = nc;
+          f.parent[b2] = nc;
+        }
+        __syncthreads();
+        fd_append(f, sh, nc, b1);
+        fd_append(f, sh, nc, b2);
+        fd_remove(f, sh, cur, b1);
+        fd_remove(f, sh, cur, b2);
+        fd_append(f, sh, cur, nc);
+        cur = nc;
+      } else {                // split (CobwebTorchNode.py:593-609): b1's children move up to cur
+        fd_remove(f, sh, cur, b1);
+        const int nb1 = f.ccnt[b1];
+        for (int j = 0; j < nb1; ++j) {
+          const int c = f.arena[f.coff[b1] + j];
+          if (tid == 0) f.parent[c] = cur;
+          __syncthreads();
+          fd_append(f, sh, cur, c);
+        }
+        if (tid == 0) {
+          f.ccnt[b1] = 0;
+          f.parent[b1] = -2;   // freed
+        }
+        __syncthreads();
+      }
+      if (f.ctrl[3] == FD_FULL) break;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (f.ctrl[3] == FD_FULL) break;
+    if (tid == 0) {
+      leaf_out[row] = leaf;
+      f.ctrl64[1] = row + 1;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int i = tid; i < kMtN; i += kFdThreads) f.mt[i] = sh.mt[i];
+  if (tid == 0) {
+    f.ctrl[4] = mt_idx;
+    f.ctrl64[2] += (int64_t)drawn;
+  }
+}
+
+}  // namespace cwq
+
+using namespace cwq;
+
+struct cwq_fit {
+  int device = 0;
+  FitDev f{};
+  std::vector<void*> allocs;
+  void* zero = nullptr;
+};
+
+static thread_local std::string g_fit_err;
+static int fit_fail(int code, const std::string& m) {
+  g_fit_err = m;
+  return code;
+}
+
+extern "C" const char* cwq_fit_last_error(void) { return g_fit_err.c_str(); }
+
+extern "C" int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t cap_nodes, cwq_fit** out) {
+  if (!out || dim <= 0 || dim > kFdMaxD || cap_nodes <= 0) return fit_fail(CWQ_ERR_ARG, "bad cwq_fit_create arguments");
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "hipSetDevice failed");
+  std::unique_ptr<cwq_fit> h(new cwq_fit());
+  h->device = device;
+  FitDev& f = h->f;
+  f.D = dim;
+  f.pv = prior_var;
+  f.cap = cap_nodes;
+  f.arena_cap = (int64_t)8 * cap_nodes + 4096;
+  auto al = [&](void** p, size_t b) -> bool {
+    if (hipMalloc(p, b < 256 ? 256 : b) != hipSuccess) return false;
+    h->allocs.push_back(*p);
+    return true;
+  };
+  const size_t C = (size_t)cap_nodes;
+  bool ok = al((void**)&f.count, C * 4) && al((void**)&f.mean, C * dim * 4) && al((void**)&f.meanSq, C * dim * 4) &&
+            al((void**)&f.parent, C * 4) && al((void**)&f.ccnt, C * 4) && al((void**)&f.ccap, C * 4) &&
+            al((void**)&f.coff, C * 8) && al((void**)&f.arena, (size_t)f.arena_cap * 4) &&
+            al((void**)&f.ctrl, 64) && al((void**)&f.ctrl64, 64) &&
+            al((void**)&f.mt, kMtN * 4) && al((void**)&f.kres, (3 * C + 8) * 4) && al((void**)&f.gain, C * 4) &&
+            al((void**)&f.tall, C * 4) && al((void**)&f.tins, C * 4) && al((void**)&f.ncv, C * 4) &&
+            al((void**)&f.jobs, (2 * C + 8) * 4);
+  if (!ok) {
+    for (void* p : h->allocs) (void)hipFree(p);
+    return fit_fail(CWQ_ERR_OOM, "cwq_fit_create: device allocation failed");
+  }
+  *out = h.release();
+  return CWQ_OK;
+}
+
+extern "C" int cwq_fit_destroy(cwq_fit* h) {
+  if (!h) return CWQ_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : h->allocs) (void)hipFree(p);
+  delete h;
+  return CWQ_OK;
+}
+
+// Load a tree into slots 0..n_nodes-1 (parent -1 for the root; child lists as CSR in list
+// order; statistics from the host) and the random() state (mt: 624 words + index,
+// Python's random.getstate()[1]).
+extern "C" int cwq_fit_load(cwq_fit* h, int32_t n_nodes, int32_t root, const int32_t* parent,
+                            const int32_t* child_ptr, const int32_t* child_idx, const float* count,
+                            const float* mean, const float* meanSq, const uint32_t* mt_state, void* stream) {
+  if (!h || n_nodes <= 0 || n_nodes > h->f.cap || root < 0 || root >= n_nodes || !parent || !child_ptr || !count ||
+      !mean || !meanSq || !mt_state)
+    return fit_fail(CWQ_ERR_ARG, "bad cwq_fit_load arguments");
+  FitDev& f = h->f;
+  if ((int64_t)child_ptr[n_nodes] > f.arena_cap / 4) return fit_fail(CWQ_ERR_ARG, "child lists exceed the arena");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipSetDevice(h->device) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "hipSetDevice failed");
+  std::vector<int> ccnt(n_nodes), ccap(n_nodes);
+  std::vector<int64_t> coff(n_nodes);
+  std::vector<int> arena;
+  arena.reserve((size_t)child_ptr[n_nodes] * 2 + 16);
+  for (int i = 0; i < n_nodes; ++i) {
+    const int c0 = child_ptr[i], c1 = child_ptr[i + 1];
+    ccnt[i] = c1 - c0;
+    ccap[i] = ccnt[i] < 4 ? 4 : ccnt[i] * 2;
+    coff[i] = (int64_t)arena.size();
+    for (int j = c0; j < c1; ++j) arena.push_back(child_idx[j]);
+    arena.resize(arena.size() + (ccap[i] - ccnt[i]), 0);
+  }
+  if ((int64_t)arena.size() > f.arena_cap / 2) return fit_fail(CWQ_ERR_ARG, "child lists exceed the arena");
+  std::vector<int> ctrl(16, 0);
+  ctrl[0] = n_nodes;
+  ctrl[2] = root;
+  ctrl[3] = FD_OK;
+  ctrl[4] = (int)mt_state[kMtN];
+  std::vector<int64_t> ctrl64(8, 0);
+  ctrl64[0] = (int64_t)arena.size();
+  const size_t D = (size_t)f.D;
+#define FCPY(dst, src, bytes)                                                                        \
+  if ((bytes) && hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) != hipSuccess)            \
+    return fit_fail(CWQ_ERR_HIP, "cwq_fit_load upload failed");
+  FCPY(f.parent, parent, (size_t)n_nodes * 4);
+  FCPY(f.ccnt, ccnt.data(), (size_t)n_nodes * 4);
+  FCPY(f.ccap, ccap.data(), (size_t)n_nodes * 4);
+  FCPY(f.coff, coff.data(), (size_t)n_nodes * 8);
+  FCPY(f.arena, arena.data(), arena.size() * 4);
+  FCPY(f.count, count, (size_t)n_nodes * 4);
+  FCPY(f.mean, mean, (size_t)n_nodes * D * 4);
+  FCPY(f.meanSq, meanSq, (size_t)n_nodes * D * 4);
+  FCPY(f.ctrl, ctrl.data(), ctrl.size() * 4);
+  FCPY(f.ctrl64, ctrl64.data(), ctrl64.size() * 8);
+  FCPY(f.mt, mt_state, (size_t)kMtN * 4);
+#undef FCPY
+  if (hipStreamSynchronize(s) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "cwq_fit_load sync failed");
+  return CWQ_OK;
+}
+
+// Insert rows X[rows_done..n) (device [n][dim]) in order; leaf_out[i] (device) = the slot
+// of the node row i ended in (ifit's return value).  Runs until every row is in or the
+// pool/arena needs room (info[2] = 1: export, reload with a larger capacity, call again).
+// info (host): {rows done, randoms drawn (total), status, slots in use}.
+extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* leaf_out, int64_t* info,
+                              void* stream) {
+  if (!h || (!X && n > 0) || (!leaf_out && n > 0) || !info) return fit_fail(CWQ_ERR_ARG, "bad cwq_fit_insert arguments");
+  if (hipSetDevice(h->device) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "hipSetDevice failed");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = sizeof(FdShared);
+  hipLaunchKernelGGL(fit_insert_kernel, dim3(1), dim3(kFdThreads), lds, s, h->f, X, n, leaf_out);
+  if (hipGetLastError() != hipSuccess) return fit_fail(CWQ_ERR_HIP, "fit_insert_kernel launch failed");
+  int ctrl[16];
+  int64_t c64[8];
+  if (hipMemcpyAsync(ctrl, h->f.ctrl, 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(c64, h->f.ctrl64, 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fit_fail(CWQ_ERR_HIP, "cwq_fit_insert sync failed");
+  info[0] = c64[1];
+  info[1] = c64[2];
+  info[2] = ctrl[3];
+  info[3] = ctrl[0];
+  if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");
+  // the next call resumes: clear the room flag
+  if (ctrl[3] == FD_ROOM) {
+    const int z = 0;
+    if (hipMemcpyAsync(h->f.ctrl + 3, &z, 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fit_fail(CWQ_ERR_HIP, "cwq_fit_insert reset failed");
+  }
+  return CWQ_OK;
+}
+
+// Export the device tree: slots in use (out2[0]), root (out2[1]); parent [cap] (-2: a
+// node removed by a split), child CSR (child_ptr [cap+1], child_idx [cap]), count [cap],
+// mean / meanSq [cap][dim] (host), mt_state [625] (the random() state to hand back).
+extern "C" int cwq_fit_export(cwq_fit* h, int32_t* out2, int32_t* parent, int32_t* child_ptr, int32_t* child_idx,
+                              float* count, float* mean, float* meanSq, uint32_t* mt_state, void* stream) {
+  if (!h || !out2 || !parent || !child_ptr || !child_idx || !count || !mean || !meanSq || !mt_state)
+    return fit_fail(CWQ_ERR_ARG, "bad cwq_fit_export arguments");
+  if (hipSetDevice(h->device) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "hipSetDevice failed");
+  hipStream_t s = (hipStream_t)stream;
+  FitDev& f = h->f;
+  int ctrl[16];
+  int64_t c64[8];
+  if (hipMemcpyAsync(ctrl, f.ctrl, 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(c64, f.ctrl64, 64, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fit_fail(CWQ_ERR_HIP, "cwq_fit_export failed");
+  const int used = ctrl[0];
+  const size_t D = (size_t)f.D;
+  std::vector<int> ccnt(used);
+  std::vector<int64_t> coff(used);
+  std::vector<int> arena((size_t)c64[0]);
+#define FGET(dst, src, bytes)                                                                        \
+  if ((bytes) && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)            \
+    return fit_fail(CWQ_ERR_HIP, "cwq_fit_export download failed");
+  FGET(parent, f.parent, (size_t)used * 4);
+  FGET(ccnt.data(), f.ccnt, (size_t)used * 4);
+  FGET(coff.data(), f.coff, (size_t)used * 8);
+  FGET(arena.data(), f.arena, arena.size() * 4);
+  FGET(count, f.count, (size_t)used * 4);
+  FGET(mean, f.mean, (size_t)used * D * 4);
+  FGET(meanSq, f.meanSq, (size_t)used * D * 4);
+  FGET(mt_state, f.mt, (size_t)kMtN * 4);
+#undef FGET
+  if (hipStreamSynchronize(s) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "cwq_fit_export sync failed");
+  mt_state[kMtN] = (uint32_t)ctrl[4];
+  child_ptr[0] = 0;
+  for (int i = 0; i < used; ++i) {
+    const int nc = parent[i] == -2 ? 0 : ccnt[i];
+    for (int j = 0; j < nc; ++j) child_idx[child_ptr[i] + j] = arena[coff[i] + j];
+    child_ptr[i + 1] = child_ptr[i] + nc;
+  }
+  out2[0] = used;
+  out2[1] = ctrl[2];
+  return CWQ_OK;
+}
+
+// Host run of the device MT19937 code (CPU test of the random() stream; no GPU).
+extern "C" int cwq_mt19937_draw(uint32_t* state625, int64_t n, double* out) {
+  if (!state625 || n < 0 || (n > 0 && !out)) return CWQ_ERR_ARG;
+  int idx = (int)state625[kMtN];
+  for (int64_t i = 0; i < n; ++i) out[i] = mt_random(state625, idx);
+  state625[kMtN] = (uint32_t)idx;
+  return CWQ_OK;
+}

@@ -270,3 +270,144 @@ class TreeFitter:
                 n.count = F32(cnt[n.slot])
                 n.mean = mean[n.slot].copy()
                 n.meanSq = m2[n.slot].copy()
+
+
+# ----------------------------------------------------------------------------
+# Device-resident ifit (cwq_fitdev.hip): the whole insert loop on the GPU
+# ----------------------------------------------------------------------------
+_ROOM = 1
+_MAX_DEVICE_DIM = 1024
+
+
+class DeviceTreeFitter:
+    """CobwebTorchTree.cobweb (CobwebTorchTree.py:143-233) for a batch of rows with the
+    tree resident on the GPU (libcwq cwq_fit_*): one kernel inserts every row in order,
+    making every decision of TreeFitter.ifit above on the device -- the same KL
+    arithmetic, the same float32 scalar order, and random() drawn from Python's own
+    MT19937 stream (the state of `rng` goes to the device and comes back advanced by the
+    draws made, exactly as if the reference had drawn them).  No host round trip per
+    insert or per level; the host tree is rebuilt once after the batch.  Existing Node
+    objects keep their identity (slots are never reused within a batch)."""
+
+    def __init__(self, tree, device=None, rng=None):
+        if tree.dim > _MAX_DEVICE_DIM:
+            raise ValueError(f"DeviceTreeFitter supports dim <= {_MAX_DEVICE_DIM}")
+        self.tree = tree
+        self.D = tree.dim
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rng = rng if rng is not None else _random_mod
+        self.stats = {}
+
+    # ---- host tree <-> slot arrays ----
+    def _flatten(self):
+        """The live host tree as slot arrays (root = slot 0, DFS preorder), children in
+        list order as CSR."""
+        nodes, stack = [], [self.tree.root]
+        while stack:
+            n = stack.pop()
+            nodes.append(n)
+            stack.extend(reversed(n.children))
+        slot = {id(n): i for i, n in enumerate(nodes)}
+        N = len(nodes)
+        parent = np.full(N, -1, np.int32)
+        cptr = np.zeros(N + 1, np.int32)
+        cidx = []
+        for i, n in enumerate(nodes):
+            if n.parent is not None:
+                parent[i] = slot[id(n.parent)]
+            cidx.extend(slot[id(c)] for c in n.children)
+            cptr[i + 1] = len(cidx)
+        count = np.array([n.count for n in nodes], F32)
+        mean = np.ascontiguousarray(np.stack([np.asarray(n.mean, F32) for n in nodes]))
+        m2 = np.ascontiguousarray(np.stack([np.asarray(n.meanSq, F32) for n in nodes]))
+        return nodes, parent, cptr, np.asarray(cidx if cidx else [0], np.int32), count, mean, m2
+
+    def fit_batch(self, X):
+        """Insert the rows of X in order; returns the node each row ended in (ifit's
+        return value, CobwebTorchTree.py:123-141), as host Node objects."""
+        import time
+        L = lib()
+        X = torch.as_tensor(X if torch.is_tensor(X) else np.asarray(X, F32), dtype=torch.float32)
+        X = X.to(self.dev).contiguous()
+        n = int(X.shape[0])
+        if n == 0:
+            return []
+        mt = np.ascontiguousarray(np.asarray(self.rng.getstate()[1], np.uint32))   # 624 words + index
+        leaf = torch.full((n,), -1, dtype=torch.int32, device=self.dev)
+        info = np.zeros(4, np.int64)
+        sp = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        out = [None] * n
+        done, t_kernel, draws, loads = 0, 0.0, 0, 0
+
+        def chk(rc):
+            if rc:
+                raise RuntimeError(f"libcwq device fit: {L.cwq_fit_last_error().decode()}")
+
+        while done < n:
+            nodes, parent, cptr, cidx, count, mean, m2 = self._flatten()
+            cap = int(len(nodes) + 3 * (n - done) + 1024)
+            h = ctypes.c_void_p()
+            with torch.cuda.device(self.dev):
+                chk(L.cwq_fit_create(self.dev.index, self.D, float(self.tree.prior_var), cap, ctypes.byref(h)))
+                try:
+                    chk(L.cwq_fit_load(h, len(nodes), 0, _np_ptr(parent), _np_ptr(cptr), _np_ptr(cidx),
+                                       _np_ptr(count), _np_ptr(mean), _np_ptr(m2), _np_ptr(mt), sp))
+                    loads += 1
+                    t0 = time.perf_counter()
+                    chk(L.cwq_fit_insert(h, ctypes.c_void_p(X[done:].data_ptr()), n - done,
+                                         ctypes.c_void_p(leaf[done:].data_ptr()), _np_ptr(info), sp))
+                    t_kernel += time.perf_counter() - t0
+                    used = int(info[3])
+                    out2 = np.zeros(2, np.int32)
+                    P = np.zeros(used, np.int32)
+                    CP = np.zeros(used + 1, np.int32)
+                    CI = np.zeros(max(used, 1), np.int32)
+                    CNT = np.zeros(used, F32)
+                    MEAN = np.zeros((used, self.D), F32)
+                    M2 = np.zeros((used, self.D), F32)
+                    chk(L.cwq_fit_export(h, _np_ptr(out2), _np_ptr(P), _np_ptr(CP), _np_ptr(CI), _np_ptr(CNT),
+                                         _np_ptr(MEAN), _np_ptr(M2), _np_ptr(mt), sp))
+                finally:
+                    L.cwq_fit_destroy(h)
+            objs = self._rebuild(nodes, out2, P, CP, CI, CNT, MEAN, M2)
+            k = int(info[0])
+            draws += int(info[1])
+            lv = leaf[done:done + k].cpu().numpy()
+            for i in range(k):
+                out[done + i] = objs[int(lv[i])]
+            done += k
+            if int(info[2]) != _ROOM:
+                if done != n:
+                    raise RuntimeError(f"device fit stopped after {done} of {n} rows (status {int(info[2])})")
+                break
+        # hand the advanced random() state back: the reference's draws, in its order
+        old = self.rng.getstate()
+        self.rng.setstate((old[0], tuple(int(v) for v in mt), old[2]))
+        self.stats = {"rows": n, "kernel_s": round(t_kernel, 4), "random_draws": draws, "loads": loads}
+        return out
+
+    def _rebuild(self, nodes, out2, P, CP, CI, CNT, MEAN, M2):
+        """Host Node objects from the exported slots (loaded slots keep their objects);
+        returns the slot -> Node list (None for nodes a split removed)."""
+        used, root = int(out2[0]), int(out2[1])
+        objs = list(nodes) + [Node(self.D) for _ in range(used - len(nodes))]
+        for i in range(used):
+            if P[i] == -2:            # removed by a split
+                objs[i].children = []
+                objs[i].parent = None
+                objs[i] = None
+        for i in range(used):
+            o = objs[i]
+            if o is None:
+                continue
+            o.count = F32(CNT[i])
+            o.mean = MEAN[i]
+            o.meanSq = M2[i]
+            o.parent = objs[P[i]] if P[i] >= 0 else None
+            o.children = [objs[c] for c in CI[CP[i]:CP[i + 1]]]
+        self.tree.root = objs[root]
+        return objs
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)

@@ -20,6 +20,8 @@ Differences (documented in DESIGN.md §6):
 import json
 import math
 
+import os
+
 import numpy as np
 import torch
 
@@ -81,21 +83,30 @@ class CobwebWrapper:
                 print(f"[Warning] Provided vector dim {new_embeddings.shape[1]} != tree dim "
                       f"{self.tree.shape[0]}, re-encoding...")
                 new_embeddings = np.asarray(self.encode_func(new_sentences), dtype=np.float32)
-        from .fit import TreeFitter
+        from .fit import _MAX_DEVICE_DIM, DeviceTreeFitter, TreeFitter
         X = np.asarray(new_embeddings.detach().cpu().numpy() if torch.is_tensor(new_embeddings)
                        else new_embeddings, dtype=np.float32)
         if self.tree is None:
             self.tree = CobwebTree(X.shape[1:])
-        fitter = TreeFitter(self.tree, device=self.device)
         start = len(self.sentences)
+        n = len(new_sentences)
+        # the device-resident insert loop (one kernel for the whole batch) unless disabled
+        # (CWQ_FIT_DEVICE=0) or the dimension is past its LDS budget: then the host-driven
+        # fitter (per level one KL launch) -- both build the same tree
+        use_dev = os.environ.get("CWQ_FIT_DEVICE", "1") != "0" and self.tree.dim <= _MAX_DEVICE_DIM
+        if use_dev:
+            leaves = DeviceTreeFitter(self.tree, device=self.device).fit_batch(X[:n])
+        else:
+            fitter = TreeFitter(self.tree, device=self.device)
+            leaves = [fitter.ifit(X[i]) for i in range(n)]
+            fitter.sync_to_host()
         for i, sent in enumerate(new_sentences):
             self.sentences.append(sent)
-            leaf = fitter.ifit(X[i])
+            leaf = leaves[i]
             if leaf.sentence_id is None:
                 leaf.sentence_id = []
             leaf.sentence_id.append(start + i)
             self.sentence_to_node[start + i] = leaf
-        fitter.sync_to_host()
         self._invalidate_prediction_index()
 
     # --------------------------------------------------------------- index build

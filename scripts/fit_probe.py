@@ -37,7 +37,10 @@ def main():
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--clusters", type=int, default=0, help="0: X ~ N(0,I); else Gaussian clusters (sd 0.3)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--host", action="store_true", help="the host-driven fitter (CWQ_FIT_DEVICE=0)")
     args = ap.parse_args()
+    if args.host:
+        os.environ["CWQ_FIT_DEVICE"] = "0"
     pkg = cobweb_pkg.load()
     rng = np.random.default_rng(args.seed)
     if args.clusters:
@@ -55,7 +58,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n, nint, mx, rootc = depth_stats(w.tree.root)
-    print(f"ifit n={args.n} d={args.dim} clusters={args.clusters}: {dt:.2f} s  {args.n / dt:.0f} inserts/s  "
+    mode = "host-driven" if args.host else "device-resident"
+    print(f"ifit ({mode}) n={args.n} d={args.dim} clusters={args.clusters}: {dt:.2f} s  {args.n / dt:.0f} inserts/s  "
           f"{1e3 * dt / args.n:.2f} ms/insert  tree: {n} nodes ({nint} internal), depth {mx}, root children {rootc}",
           flush=True)
 

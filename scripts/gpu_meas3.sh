@@ -20,6 +20,12 @@ for s in "$@"; do
     alltests) step pytest_all 1200 python -u -m pytest -x -q -p no:cacheprovider --timeout 400 --timeout-method thread \
         tests -m gpu ;;
     cat100k_replay) CWQ_CAT_COUNT=0 step cat_g100k_replay 600 python scripts/basic_probe.py --clusters 100000 --queries 500 --reps 1 ;;
+    fittest) step pytest_fit 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 400 --timeout-method thread \
+        tests/test_gpu_fit.py ;;
+    fitprobe) step fit_dev_2k 600 python scripts/fit_probe.py --n 2000 --dim 768 --clusters 20 &&
+      step fit_host_2k 600 python scripts/fit_probe.py --n 2000 --dim 768 --clusters 20 --host &&
+      step fit_dev_20k 600 python scripts/fit_probe.py --n 20000 --dim 768 --clusters 50 ;;
+    fit100k) step fit_dev_100k 1000 python scripts/fit_probe.py --n 100000 --dim 768 --clusters 100 ;;
     c4) step c4_preset 600 python bench.py --preset c4 --steps 3 --warmup 1 --no-cpu-baseline --no-per-call ;;
     cat100k) step cat_g100k 600 python scripts/basic_probe.py --clusters 100000 --queries 2000 --reps 2 ;;
     cat1024) step cat_g1024 600 python scripts/basic_probe.py --clusters 1024 --queries 10000 --reps 2 ;;

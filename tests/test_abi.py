@@ -104,3 +104,19 @@ def test_compact_var_roundtrip_cpu(pkg):
     assert torch.equal(cv.full().view(torch.int32), torch.from_numpy(var).view(torch.int32))
     np.testing.assert_array_equal(cv[13].numpy(), var[13])
     np.testing.assert_array_equal(cv[7].numpy(), var[7])
+
+
+def test_device_mt19937_is_pythons_random(pkg):
+    """The device fitter's random() (cwq_fitdev.hip, run here on the host) is Python's
+    random.random() stream from the same state, and leaves the same state behind."""
+    import random
+    r = random.Random(2024)
+    for _ in range(5):
+        r.random()
+    st = np.ascontiguousarray(np.asarray(r.getstate()[1], np.uint32))
+    out = np.zeros(2000, np.float64)
+    assert pkg.lib().cwq_mt19937_draw(st.ctypes.data_as(ctypes.c_void_p), 2000,
+                                      out.ctypes.data_as(ctypes.c_void_p)) == 0
+    want = np.array([r.random() for _ in range(2000)])
+    np.testing.assert_array_equal(out, want)
+    assert tuple(int(v) for v in st) == r.getstate()[1]

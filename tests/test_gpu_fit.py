@@ -22,10 +22,14 @@ def bfs(root):
     return out
 
 
+@pytest.mark.parametrize("fitter", ["device", "host"])
 @pytest.mark.parametrize("name", ["g1_hier_d32", "g5_hier_d384"])
-def test_gpu_ifit_reproduces_reference_tree(pkg, name):
+def test_gpu_ifit_reproduces_reference_tree(pkg, name, fitter, monkeypatch):
+    """fitter "device": the whole insert loop in one kernel (cwq_fitdev.hip); "host": the
+    host-driven fitter (fit.py TreeFitter, one KL launch per level)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1" if fitter == "device" else "0")
     g = load_golden(name)
     random.seed(0)   # gen_golden.py seeds the reference the same way
     w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(len(g["X"]))], corpus_embeddings=g["X"])
@@ -71,3 +75,41 @@ def test_wrapper_json_roundtrip_and_add(pkg):
         a = w.cobweb_predict_fast(g["Xq"][qi], 10, return_ids=True)
         b = w2.cobweb_predict_fast(g["Xq"][qi], 10, return_ids=True)
         assert a == b
+
+
+def _tree_arrays(root):
+    nodes = bfs(root)
+    pos = {id(n): i for i, n in enumerate(nodes)}
+    parent = np.array([-1 if n.parent is None else pos[id(n.parent)] for n in nodes])
+    return (parent, np.array([n.count for n in nodes], np.float32), np.stack([n.mean for n in nodes]),
+            np.stack([n.meanSq for n in nodes]), [list(n.sentence_id) for n in nodes])
+
+
+@pytest.mark.parametrize("D,n,clusters", [(48, 1500, 12), (384, 600, 6), (768, 400, 0)])
+def test_device_fit_equals_host_fit(pkg, D, n, clusters, monkeypatch):
+    """Device-resident ifit == host-driven ifit: structure, sentence placement, statistics
+    bit for bit, and the random() stream position afterwards; with a batch split in two
+    add_sentences calls (state carried over)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(D + n)
+    if clusters:
+        C = rng.standard_normal((clusters, D)).astype(np.float32) * 2.0
+        X = (C[rng.integers(0, clusters, n)] + 0.3 * rng.standard_normal((n, D))).astype(np.float32)
+    else:
+        X = rng.standard_normal((n, D)).astype(np.float32)
+    X[n // 3] = X[n // 5]          # an exact match (leaf increment)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CWQ_FIT_DEVICE", mode)
+        random.seed(7)
+        w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(n // 2)], corpus_embeddings=X[:n // 2])
+        w.add_sentences([f"s{i}" for i in range(n // 2, n)], X[n // 2:])
+        res[mode] = (_tree_arrays(w.tree.root), random.random())
+    (pa, ca, ma, sa, ia), ra = res["0"]
+    (pb, cb, mb, sb, ib), rb = res["1"]
+    np.testing.assert_array_equal(pa, pb)
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(sa, sb)
+    assert ia == ib and ra == rb
