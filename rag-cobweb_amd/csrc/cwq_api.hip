@@ -119,9 +119,11 @@ struct cwq_index {
   // their RowF constants, row-major fp32 A/B copies for the exact chain in final_kernel
   bool int_bounds = false;
   int DPB2 = 0;
-  int64_t ld_i2 = 0;
-  uint16_t* int_Mb2 = nullptr;
+  int64_t ld_i2 = 0;                  // operand rows: levels 0-1 together, then each deeper level
+  uint16_t* int_Mb2 = nullptr;        // from a new 256-row tile (a tile never holds a node and its parent)
   RowF* int_rf2 = nullptr;
+  int* int_rowid = nullptr;           // operand row -> internal id (-1: padding)
+  int2* int_tdep = nullptr;           // per operand row tile: the row tiles holding its rows' parents
   float *int_Ar = nullptr, *int_Br = nullptr;
   float root_w = 1.f, root_ld = 0.f;   // the root's level weight and logdet (host copies)
   int* samp_rows = nullptr;
@@ -616,17 +618,59 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   if (ix->NL_iso > 0 && ix->NI >= 2 && ix->max_depth <= kMaxChain) {
     // internal-node bound operands: K = [x'^2, x'] -> DPB2 = fgemm width of 2*DP
     ix->DPB2 = fgemm_dpb(2 * ix->DP);
-    ix->ld_i2 = round_up(ix->NI, kFgTile);
+    // level-aligned operand layout: segments [levels 0 and 1], [level 2], [level 3], ...,
+    // each padded to whole 256-row tiles, so a row tile's parents always sit in earlier
+    // tiles (depth-1 rows take the root's exact prefix from the tile setup)
+    std::vector<std::pair<int, int>> segs;   // internal id ranges
+    for (size_t lv = 0; lv < ix->levels.size(); ++lv) {
+      if (lv == 1) segs.back().second = ix->levels[1].second;
+      else segs.push_back(ix->levels[lv]);
+    }
+    std::vector<int64_t> seg_row(segs.size());
+    int64_t rows = 0;
+    for (size_t g = 0; g < segs.size(); ++g) {
+      seg_row[g] = rows;
+      rows += round_up(segs[g].second - segs[g].first, kFgTile);
+    }
+    ix->ld_i2 = rows;
+    std::vector<int> rowid(rows, -1), row_of_int(ix->NI, 0);
+    for (size_t g = 0; g < segs.size(); ++g)
+      for (int i = segs[g].first; i < segs[g].second; ++i) {
+        rowid[seg_row[g] + (i - segs[g].first)] = i;
+        row_of_int[i] = (int)(seg_row[g] + (i - segs[g].first));
+      }
+    const int n_rt2 = (int)(rows / kFgTile);
+    std::vector<int2> tdep(n_rt2, make_int2(-1, -1));
+    for (int t = 0; t < n_rt2; ++t) {
+      int plo = INT32_MAX, phi = -1;
+      for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
+        const int i = rowid[r];
+        if (i < 0) continue;
+        const int p = par_int[i];
+        if (p <= 0) continue;   // root and depth 1: no wait
+        plo = std::min(plo, p);
+        phi = std::max(phi, p);
+      }
+      if (phi >= 0) tdep[t] = make_int2(row_of_int[plo] / kFgTile, row_of_int[phi] / kFgTile);
+    }
     if ((rc = ix->alloc(&ix->int_Mb2, (size_t)ix->DPB2 * ix->ld_i2))) return rc;
     if ((rc = ix->alloc(&ix->int_rf2, (size_t)ix->ld_i2))) return rc;
     if ((rc = ix->alloc(&ix->int_Ar, (size_t)ix->NI * DP))) return rc;
     if ((rc = ix->alloc(&ix->int_Br, (size_t)ix->NI * DP))) return rc;
+    if ((rc = ix->upload(&ix->int_rowid, rowid, s))) return rc;
+    if ((rc = ix->upload(&ix->int_tdep, tdep, s))) return rc;
     const float gamma2 = (float)((ix->DPB2 + 64) * std::ldexp(1.0, -23));
     ix->root_w = w_int[0];
     HIPCHK(hipMemcpyAsync(&ix->root_ld, ix->logdet_int, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes, ix->NI, ix->iso_c, ix->logdet_int, ix->par_int, ix->w_int, DP,
-                           ix->DPB2, ix->ld_i2, ix->int_Mb2, ix->int_rf2, ix->int_Ar, ix->int_Br, gamma2, s));
+    for (size_t g = 0; g < segs.size(); ++g) {
+      const int i0 = segs[g].first, n = segs[g].second - segs[g].first;
+      HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes + i0, n, ix->iso_c, ix->logdet_int + i0, ix->par_int + i0,
+                             ix->w_int + i0, DP, ix->DPB2, round_up(n, kFgTile),
+                             ix->int_Mb2 + (size_t)seg_row[g] * ix->DPB2, ix->int_rf2 + seg_row[g],
+                             ix->int_Ar + (size_t)i0 * DP, ix->int_Br + (size_t)i0 * DP, gamma2, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));   // tdep / rowid host vectors are freed on return
     ix->int_bounds = true;
   }
   if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
@@ -723,6 +767,7 @@ namespace {
 constexpr int kQPad = 128;   // queries are padded to a multiple of the largest query block
 
 struct Chunk {
+  int* tfail = nullptr;   // fused internal bounds: a dependency wait gave up (device flag)
   int nq = 0;           // valid queries
   int64_t nq_pad = 0;
   float* X = nullptr;   // [nq_pad][DP]
@@ -821,7 +866,9 @@ bool use_int_bounds(const cwq_index* ix) {
 }
 
 size_t int_bounds_bytes(const cwq_index* ix, int64_t nqf) {
-  return ix->int_bounds ? (size_t)nqf * ix->DPB2 * 2 + (size_t)nqf * 16 + (size_t)nqf * 4 + 3 * 256 : 0;
+  return ix->int_bounds ? (size_t)nqf * ix->DPB2 * 2 + (size_t)nqf * 16 + (size_t)nqf * 4 + 5 * 256 +
+                              (size_t)(nqf / kFgTile) * (ix->ld_i2 / kFgTile) * 4
+                        : 0;
 }
 
 // Internal nodes by bounds: c.P <- lower, c.S_int <- upper bounds of the path prefix of
@@ -857,32 +904,32 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   g.Sroot = Sroot;
   g.root_w = ix->root_w;
   g.root_ld = ix->root_ld;
-  // One launch per tree level (the root and depth 1 together): each row's prefix bounds
-  // are finished in the epilogue from its parent's, which the previous launch wrote
-  // (prefix_step on intervals), so the bounds are written once and never re-read by a
-  // separate prefix pass.  A row tile straddling two levels is computed by both launches
-  // with identical results.  Measured on balanced trees (1M x 768, 10k queries): branching
-  // 10 / depth 5 internal pass 10.7 -> 10.3 ms, branching 4 / depth 9 36.3 -> 38.7 ms (the
-  // small levels' launches and the parent gathers cost what the prefix passes did), so it
-  // is off by default: CWQ_INT_LEVELS=1 enables it.
-  const char* el = getenv("CWQ_INT_LEVELS");
-  const bool per_level = el && *el && atoi(el) == 1 && ix->levels.size() > 2;
-  if (!per_level) {
+  g.row_id = ix->int_rowid;
+  g.nrows = (int)ix->ld_i2;
+  // One launch: with >= 8 query tiles (each XCD keeps its own query tiles, so a row tile's
+  // parent tiles are claimed before it by the same XCD) the prefix bounds are finished in
+  // the epilogue from the parents' final bounds (prefix_step on intervals), each tile
+  // waiting for its parents' tiles -- written once, no separate prefix pass over the
+  // [nq][NI] matrices; CWQ_INT_FUSED=0 keeps the separate per-level prefix passes.
+  const char* ef = getenv("CWQ_INT_FUSED");
+  const bool fused = g.n_qt >= 8 && ix->levels.size() > 2 && !(ef && *ef && atoi(ef) == 0);
+  if (fused) {
+    g.qgroups = 8;
+    g.rgroups = 1;
+    g.fuse_prefix = 1;
+    g.tdep = ix->int_tdep;
+    g.tflag = b.take<int>((size_t)g.n_qt * g.n_rt);
+    g.tfail = b.take<int>(64);
+    HIPCHK(hipMemsetAsync(g.tflag, 0, (size_t)g.n_qt * g.n_rt * 4, s));
+    HIPCHK(hipMemsetAsync(g.tfail, 0, 4, s));
+    c.tfail = g.tfail;
     HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
-    for (size_t lv = 2; lv < ix->levels.size(); ++lv)
-      HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first,
-                                  ix->levels[lv].second, ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
     return CWQ_OK;
   }
-  g.fuse_prefix = 1;
-  g.order = 0;   // static tile order: no claim counters to reset between the launches
-  for (size_t lv = 1; lv < ix->levels.size(); ++lv) {
-    const int i0 = lv == 1 ? 0 : ix->levels[lv].first, i1 = ix->levels[lv].second;
-    if (i1 <= i0) continue;
-    g.rt_off = i0 / kFgTile;
-    g.n_rt = (i1 - 1) / kFgTile - g.rt_off + 1;
-    HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
-  }
+  HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+  for (size_t lv = 2; lv < ix->levels.size(); ++lv)
+    HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first, ix->levels[lv].second,
+                                ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
   return CWQ_OK;
 }
 
@@ -1582,8 +1629,12 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         const int* cnth = ix->hflags;
         const int* okh = cnth + nqf;
         const int* nexh = cnth + 2 * nqf;
+        int tf = 0;
+        if (c.tfail) {
+          HIPCHK(hipMemcpy(&tf, c.tfail, 4, hipMemcpyDeviceToHost));
+        }
         for (int i = 0; i < nqc; ++i) {
-          if (!okh[i]) redo.push_back(q0 + i);
+          if (!okh[i] || tf) redo.push_back(q0 + i);
           cand_sum += cnth[i];
           exact_sum += nexh[i];
         }

@@ -231,7 +231,12 @@ struct FgArgs {
   int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)
   int dbg;                                // ablation (perf experiments only): 1 no operand loads, 2 no epilogue
   int cat;                                // categorize key: bounds min'ed with P[q][par] (P = BF)
-  int fuse_prefix;                        // mode 2, one launch per tree level: prefix bounds from the parent's
+  int fuse_prefix;                        // mode 2: prefix bounds from the parent's final bounds in the epilogue
+                                          // (rows in level-aligned tiles; a tile waits for its parents' tiles)
+  const int* row_id;                      // mode 2: operand row -> internal node id (-1: padding)
+  const int2* tdep;                       // mode 2 fused: row tiles holding the parents of row tile rt ([x, y]; x < 0: none)
+  int* tflag;                             // mode 2 fused: [n_qt][n_rt] tile-done flags (zeroed before the launch)
+  int* tfail;                             // mode 2 fused: set when a wait gave up (the host re-runs exactly)
   const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
   const float* T;                         // thresholds, T[q * ldT]
   int64_t ldT;

@@ -780,6 +780,28 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       // through LDS so that each store covers 64 consecutive rows of one query (256 B)
       const int rl = r0 + wr * 64 + lane;   // this lane's row in the store phase
       const RowF f = rl < a.nrows ? a.rf[rl] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+      const int rid = a.row_id ? (rl < a.nrows ? a.row_id[rl] : -1) : rl;   // internal node id
+      if (a.fuse_prefix) {
+        // the parents' final prefix bounds come from earlier row tiles of this query tile
+        // (a level's rows start a new tile, so parents are never in the same tile): wait
+        // for their done flags (agent-scope acquire), bounded
+        const int2 dp = a.tdep[rt];
+        if (tid == 0 && dp.x >= 0) {
+          for (int t = dp.x; t <= dp.y; ++t) {
+            int* fl = a.tflag + (size_t)qt * a.n_rt + t;
+            int spins = 0;
+            while (__hip_atomic_load(fl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+              __builtin_amdgcn_s_sleep(2);
+              if (++spins > (1 << 24)) {   // never expected: give up, flag the call for the exact path
+                __hip_atomic_store(a.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __syncthreads();
+      }
       // ib unrolled: a dynamically indexed acc[ib] would be copied to scratch memory
 #pragma unroll
       for (int ib = 0; ib < 8; ++ib) {
@@ -803,14 +825,20 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             } else {
               int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
               if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
-              else if (a.fuse_prefix)   // deeper: the parent's bounds, final since the previous level's launch
+              else if (a.fuse_prefix)   // deeper: the parent's final bounds (its tile is done)
                 prefix_step(a.lb[(size_t)q * a.ldlb + f.par], a.lb_hi[(size_t)q * a.ldlb + f.par], f.invL, lo, hi);
             }
-            a.lb[(size_t)q * a.ldlb + rl] = lo;
-            a.lb_hi[(size_t)q * a.ldlb + rl] = hi;
+            a.lb[(size_t)q * a.ldlb + rid] = lo;
+            a.lb_hi[(size_t)q * a.ldlb + rid] = hi;
           }
         }
         __builtin_amdgcn_wave_barrier();   // reads of this block done before the next dump
+      }
+      if (a.fuse_prefix) {
+        // this tile's bounds are final: every storing thread's release, then the flag
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(a.tflag + (size_t)qt * a.n_rt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       goto flush;
     }
