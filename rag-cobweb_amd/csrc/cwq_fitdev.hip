@@ -678,7 +678,9 @@ extern "C" int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t 
   f.D = dim;
   f.pv = prior_var;
   f.cap = cap_nodes;
-  f.arena_cap = (int64_t)8 * cap_nodes + 4096;
+  // child-list arena: a load uses <= 6 entries per node (lists at twice their length, >= 4),
+  // inserts stop for room at half of it, which keeps room for the largest list to double
+  f.arena_cap = (int64_t)16 * cap_nodes + 4096;
   auto al = [&](void** p, size_t b) -> bool {
     if (hipMalloc(p, b < 256 ? 256 : b) != hipSuccess) return false;
     h->allocs.push_back(*p);

@@ -376,6 +376,8 @@ class DeviceTreeFitter:
             for i in range(k):
                 out[done + i] = objs[int(lv[i])]
             done += k
+            if int(info[2]) == _ROOM and k == 0:
+                raise RuntimeError("device fit made no progress after a reload")
             if int(info[2]) != _ROOM:
                 if done != n:
                     raise RuntimeError(f"device fit stopped after {done} of {n} rows (status {int(info[2])})")
