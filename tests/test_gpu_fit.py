@@ -113,3 +113,33 @@ def test_device_fit_equals_host_fit(pkg, D, n, clusters, monkeypatch):
     np.testing.assert_array_equal(ma, mb)
     np.testing.assert_array_equal(sa, sb)
     assert ia == ib and ra == rb
+
+
+def test_device_fit_matches_oracle_2k_clustered_768(pkg, monkeypatch):
+    """The device-resident ifit on a 2,000-insert prefix of clustered 768-d data builds the
+    oracle's tree (oracle/cobweb_oracle.py OTree.ifit -- the restatement pinned to the
+    reference's own ifit trees G1/G5): same BFS structure, counts, sentence placement, and
+    statistics bit for bit (CobwebTorchTree.py:143-233)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import cobweb_oracle as O
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1")
+    rng = np.random.default_rng(2024)
+    n, D, k = 2000, 768, 20
+    C = rng.standard_normal((k, D)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, k, n)] + 0.3 * rng.standard_normal((n, D))).astype(np.float32)
+    ot = O.OTree(D, rng=random.Random(5))
+    for i in range(n):
+        ot.ifit(X[i]).sentence_id.append(i)
+    random.seed(5)
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(n)], corpus_embeddings=X)
+    onodes = O.bfs_nodes(ot.root)
+    opos = {id(x): i for i, x in enumerate(onodes)}
+    oparent = np.array([-1 if x.parent is None else opos[id(x.parent)] for x in onodes])
+    p, cnt, mean, m2, sids = _tree_arrays(w.tree.root)
+    np.testing.assert_array_equal(p, oparent)
+    np.testing.assert_array_equal(cnt, np.array([x.count for x in onodes], np.float32))
+    assert sids == [list(x.sentence_id) for x in onodes]
+    np.testing.assert_array_equal(mean, np.stack([x.mean for x in onodes]))
+    np.testing.assert_array_equal(m2, np.stack([x.meanSq for x in onodes]))
+    assert len(onodes) > 2 * k and max(len(x.children) for x in onodes) > 1
