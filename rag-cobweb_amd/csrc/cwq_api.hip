@@ -1955,6 +1955,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                               s)))
         return rc;
       SimArgs sd = sa;
+      sd.pre_status = 0;   // every hard query replays (status2 is fresh scratch)
       sd.nq = ns;
       sd.R = 0;
       sd.LPF = c2.LPF ? c2.LPF : ix->dummy;

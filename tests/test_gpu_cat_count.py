@@ -36,8 +36,13 @@ def _both(ix, Q, k, max_nodes):
     got = ix.categorize(Q, k, max_nodes)
     torch.cuda.synchronize()
     st = ix.last_categorize_stats()
-    for a, b in zip(ref, got):
-        assert torch.equal(a, b)
+    for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
+        if not torch.equal(a, b):
+            bad = (a != b).reshape(a.shape[0], -1).any(1).nonzero().flatten()[:4].tolist()
+            raise AssertionError(f"{name} differs (k={k}, max_nodes={max_nodes}, stats {st}) at queries {bad}: "
+                                 f"replay {[a[i].tolist() for i in bad]} count {[b[i].tolist() for i in bad]}; "
+                                 f"found {[int(ref[1][i]) for i in bad]}, calls {[int(ref[2][i]) for i in bad]} vs "
+                                 f"{[int(got[2][i]) for i in bad]}")
     return st
 
 
@@ -64,7 +69,10 @@ def test_count_equals_replay(gpu):
         n_int = ix.info["internal_nodes"]
         for k, mx in [(10, 100000), (1, 100000), (64, 100000), (10, n_int // 2), (10, n_int + 5), (5, 7),
                       (10, 2), (64, n_int + 40)]:
-            st = _both(ix, Q, k, mx)
+            try:
+                st = _both(ix, Q, k, mx)
+            except AssertionError as e:
+                raise AssertionError(f"{name}: {e}") from None
             totals["by_count"] += st["by_count"]
             totals["by_replay"] += st["by_replay"]
         ix.close()
