@@ -1389,16 +1389,17 @@ __global__ __launch_bounds__(kCcThreads) void cat_count_kernel(const SimArgs a) 
     have = C < M;   // else max_nodes cuts earlier: select below
   }
   if (!have) {
-    // the M-th largest b among the internal nodes and the list (above the k-th retrieval's
-    // group when there is one): radix select, 11 + 11 + 10 bits
+    // the M-th largest b among the internal nodes and the list (those above the k-th
+    // retrieval's group when there is one -- the M-th pop comes before that group):
+    // radix select, 11 + 11 + 10 bits
     const bool lim = kidx >= 0 && s_lk[kidx] > tau;
     const float up = lim ? s_lk[kidx] : CWQ_INF;
     long long total = 0;
     {
       long long c = 0;
-      for (int i = tid; i < NI; i += kCcThreads) c += (BF[i] < up || !lim) ? 1 : 0;
+      for (int i = tid; i < NI; i += kCcThreads) c += (BF[i] > up || !lim) ? 1 : 0;
       total = block_sum_l(c);
-      for (int j = 0; j < nvalid; ++j) total += (s_lk[j] < up || !lim) ? 1 : 0;
+      for (int j = 0; j < nvalid; ++j) total += (s_lk[j] > up || !lim) ? 1 : 0;
     }
     if (total < M) {
       // fewer nodes than max_nodes: the search would exhaust the heap -- only exact when
@@ -1426,7 +1427,7 @@ __global__ __launch_bounds__(kCcThreads) void cat_count_kernel(const SimArgs a) 
         __syncthreads();
         for (int i = tid; i < NI + nvalid; i += kCcThreads) {
           const float v = i < NI ? BF[i] : s_lk[i - NI];
-          if (lim && !(v < up)) continue;
+          if (lim && !(v > up)) continue;
           const uint32_t u = ord_u32(v);
           if ((u & pmask) != prefix) continue;
           atomicAdd(&s_hist[(u >> sh) & (nb - 1)], 1);
@@ -1551,8 +1552,10 @@ __global__ __launch_bounds__(kCcThreads) void cat_count_kernel(const SimArgs a) 
             const uint64_t bm = __ballot(c);
             return bm ? __builtin_ctzll(bm) : -1;
           }();
-          if (w < 0) {   // the group ran out before the search ended: not certified
-            ok = false;
+          if (w < 0) {
+            // the group is exhausted: fine when the next pop is the max_nodes-th (never
+            // processed); otherwise the search would go on below G: not certified
+            if (pos + 1 < a.max_nodes) ok = false;
             break;
           }
           const int m = __shfl(best, w, 64);
