@@ -998,6 +998,11 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
   for (int i = 0; i < 2; ++i) {
     if (segs[i].n == 0) continue;
     ScanArgs a = base_args(ix, c);
+    // categorize keys min(BF[parent], lp) read the path BOTTLENECK (the Fast keys read the
+    // path prefix P); with P here the key was min(prefix, lp), equal to the bottleneck
+    // key only while the leaf's lp stays below its ancestors' (a near-duplicate query
+    // broke the top-R list's order)
+    if (cat) a.P = c.BF ? c.BF : ix->dummy;
     a.ld = segs[i].ld;
     a.nrows = segs[i].n;
     a.nrows_pad = (int)round_up(segs[i].n, kWave);
