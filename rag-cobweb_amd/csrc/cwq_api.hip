@@ -1929,14 +1929,16 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
     const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
     const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ix->NL * 4 +
-                         (size_t)cap_dense * 16 + 64;
+                         (size_t)cap_dense * 16 + 64 + (size_t)k * 8 + (size_t)ix->D * 4;
     const int64_t sub = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q));
     std::vector<float> hx;
     for (size_t r0 = 0; r0 < redo.size(); r0 += sub) {
       const int ns = (int)std::min<int64_t>(sub, (int64_t)redo.size() - (int64_t)r0);
       const int64_t ns_pad = round_up(ns, kQPad);
-      if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) + (size_t)ns_pad * ((size_t)ix->NL * 4 + cap_dense * 16 + 64) +
-                            16 * 256 + (size_t)ns_pad * ix->D * 4)))
+      // per hard query: dense keys, heap, then status / nodes[k] / found / calls
+      if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) +
+                            (size_t)ns_pad * ((size_t)ix->NL * 4 + cap_dense * 16 + 64 + (size_t)k * 8) + 16 * 256 +
+                            (size_t)ns_pad * ix->D * 4)))
         return rc;
       Bump b2(ix->ws, ix->ws_size);
       Chunk c2;
