@@ -1382,6 +1382,14 @@ __global__ __launch_bounds__(kCcThreads) void cat_count_kernel(const SimArgs a) 
   float G = 0.f;
   long long C = 0, S = 0;
   bool have = false;
+  if (M <= 0) {   // max_nodes <= 1: the first pop (the root) already breaks
+    if (tid == 0) {
+      a.n_found[q] = 0;
+      if (a.n_calls) a.n_calls[q] = 1;
+      a.status[q] = 0;
+    }
+    return;
+  }
   if (kidx >= 0 && s_lk[kidx] > tau) {
     G = s_lk[kidx];
     count_pass(G, C, S);

@@ -46,6 +46,8 @@ def _count_search(nodes, x, k, max_nodes, order):
     internal = [n for n in nodes if n.children]
     leaves = sorted((n for n in nodes if not n.children), key=lambda n: (-b[id(n)], order[id(n)]))
     M = max_nodes - 1
+    if M <= 0:
+        return [], 1                                  # the first pop already breaks
     kth = [n for n in leaves if n.sentence_id]
     G = None
     if len(kth) >= k:
@@ -112,7 +114,7 @@ def test_count_formulation_equals_heap_search(seed):
     checked = skipped = 0
     for x in queries:
         for k in (1, 3, 10, 40):
-            for mx in (100000, 2, 5, n_int // 2, n_int + 3, len(nodes) + 5):
+            for mx in (100000, 1, 2, 3, 5, n_int // 2, n_int + 3, len(nodes) + 5):
                 want = _heap_search(t.root, x, k, mx, order)
                 got = _count_search(nodes, x, k, mx, order)
                 if got is None:

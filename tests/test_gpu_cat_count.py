@@ -88,7 +88,7 @@ def test_count_flat_tree_and_small(gpu):
     for k, mx in [(10, 100000), (64, 100000), (10, 5), (10, 1), (1, 2)]:
         st = _both(ix, Q, k, mx)
         if k < 64:   # k = 64 = the list length: its last entry sits at the list's cut-off (DENSE)
-            assert st["by_count"] >= 0.9 * Q.shape[0], st
+            assert st["by_count"] >= 0.9 * Q.shape[0], (k, mx, st)
     ix.close()
     # a tree smaller than the list (every leaf in it): the search exhausts the heap
     t = gpu.synth.two_level_synth(X[:40].contiguous(), torch.arange(40, device="cuda:0") % 3)
