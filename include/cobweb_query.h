@@ -137,6 +137,18 @@ int cwq_rank_scores(cwq_index* idx, const float* q, int64_t nq, float* out, void
 int cwq_node_logprob(cwq_index* idx, const float* q, int64_t nq, int32_t full, float* out, void* stream);
 
 /*
+ * Diagnostic (parity tests): the Fast path's internal path prefixes P (the level-
+ * weighted sum of lp' along the path: the reference's sparse path matrix,
+ * CobwebWrapper.py:145-180, restricted to ancestors) of every internal node by the
+ * exact fp32 pass -> exact, and the rigorous bf16-MFMA bounds lo <= exact <= hi the
+ * filter uses on hierarchical trees (NaN for nodes the filter does not read: with the
+ * default path-sum bounds, internal nodes without isotropic leaf children).  All
+ * device [nq][n_internal] fp32, internal nodes in BFS order; 1 <= nq <= 4096.
+ * CWQ_ERR_ARG when the index keeps no bounds (flat tree, no isotropic leaf rows).
+ */
+int cwq_prefix_bounds(cwq_index* idx, const float* q, int64_t nq, float* lo, float* hi, float* exact, void* stream);
+
+/*
  * "Cobweb Basic" best-first categorize (A4).  Replaces CobwebTorchTree.categorize
  * / _cobweb_categorize with retrieve_k=k (CobwebTorchTree.py:235-310) as called by
  * CobwebWrapper.cobweb_predict (CobwebWrapper.py:435-461).

@@ -34,6 +34,7 @@ SIGNATURES = {
     "cwq_score_topk": (_c.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
     "cwq_rank_scores": (_c.c_int, [_P, _P, _I64, _P, _P]),
     "cwq_node_logprob": (_c.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "cwq_prefix_bounds": (_c.c_int, [_P, _P, _I64, _P, _P, _P, _P]),
     "cwq_categorize": (_c.c_int, [_P, _P, _I64, _I32, _I64, _P, _P, _P, _P]),
     "cwq_set_timing": (_c.c_int, [_P, _c.c_int]),
     "cwq_last_timing": (_c.c_int, [_P, _P]),

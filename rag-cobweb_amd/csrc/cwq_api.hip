@@ -115,15 +115,20 @@ struct cwq_index {
   std::vector<int> cat_uni_prefix;
   float cat_dconst = 0.f;
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
-  // internal-node bounds (hierarchical trees, cwq_mfma.hip int_bounds): bf16 b' rows,
-  // their RowF constants, row-major fp32 A/B copies for the exact chain in final_kernel
+  // internal-node bounds (hierarchical trees): bf16 operand rows, their RowF constants,
+  // row-major fp32 A/B copies for the exact chain in final_kernel.  int_path (default):
+  // the Fast filter reads the path prefix P of leaf parents only, so there is one row per
+  // leaf parent (and the root), its b' vectors summed along the path (cwq_mfma.hip
+  // int_path_prep) -- one GEMM, no prefix passes.  Otherwise (CWQ_INT_PATH=0 at index
+  // creation) one row per internal node, levels 0-1 together and each deeper level from
+  // a new 256-row tile, then prefix_bounds_kernel level by level.
   bool int_bounds = false;
+  bool int_path = true;
   int DPB2 = 0;
-  int64_t ld_i2 = 0;                  // operand rows: levels 0-1 together, then each deeper level
-  uint16_t* int_Mb2 = nullptr;        // from a new 256-row tile (a tile never holds a node and its parent)
+  int64_t ld_i2 = 0;                  // operand rows (padded to 256)
+  uint16_t* int_Mb2 = nullptr;
   RowF* int_rf2 = nullptr;
   int* int_rowid = nullptr;           // operand row -> internal id (-1: padding)
-  int2* int_tdep = nullptr;           // per operand row tile: the row tiles holding its rows' parents
   float *int_Ar = nullptr, *int_Br = nullptr;
   float root_w = 1.f, root_ld = 0.f;   // the root's level weight and logdet (host copies)
   int* samp_rows = nullptr;
@@ -618,59 +623,60 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   if (ix->NL_iso > 0 && ix->NI >= 2 && ix->max_depth <= kMaxChain) {
     // internal-node bound operands: K = [x'^2, x'] -> DPB2 = fgemm width of 2*DP
     ix->DPB2 = fgemm_dpb(2 * ix->DP);
-    // level-aligned operand layout: segments [levels 0 and 1], [level 2], [level 3], ...,
-    // each padded to whole 256-row tiles, so a row tile's parents always sit in earlier
-    // tiles (depth-1 rows take the root's exact prefix from the tile setup)
-    std::vector<std::pair<int, int>> segs;   // internal id ranges
-    for (size_t lv = 0; lv < ix->levels.size(); ++lv) {
-      if (lv == 1) segs.back().second = ix->levels[1].second;
-      else segs.push_back(ix->levels[lv]);
-    }
-    std::vector<int64_t> seg_row(segs.size());
-    int64_t rows = 0;
-    for (size_t g = 0; g < segs.size(); ++g) {
-      seg_row[g] = rows;
-      rows += round_up(segs[g].second - segs[g].first, kFgTile);
-    }
-    ix->ld_i2 = rows;
-    std::vector<int> rowid(rows, -1), row_of_int(ix->NI, 0);
-    for (size_t g = 0; g < segs.size(); ++g)
-      for (int i = segs[g].first; i < segs[g].second; ++i) {
-        rowid[seg_row[g] + (i - segs[g].first)] = i;
-        row_of_int[i] = (int)(seg_row[g] + (i - segs[g].first));
-      }
-    const int n_rt2 = (int)(rows / kFgTile);
-    std::vector<int2> tdep(n_rt2, make_int2(-1, -1));
-    for (int t = 0; t < n_rt2; ++t) {
-      int plo = INT32_MAX, phi = -1;
-      for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
-        const int i = rowid[r];
-        if (i < 0) continue;
-        const int p = par_int[i];
-        if (p <= 0) continue;   // root and depth 1: no wait
-        plo = std::min(plo, p);
-        phi = std::max(phi, p);
-      }
-      if (phi >= 0) tdep[t] = make_int2(row_of_int[plo] / kFgTile, row_of_int[phi] / kFgTile);
-    }
-    if ((rc = ix->alloc(&ix->int_Mb2, (size_t)ix->DPB2 * ix->ld_i2))) return rc;
-    if ((rc = ix->alloc(&ix->int_rf2, (size_t)ix->ld_i2))) return rc;
-    if ((rc = ix->alloc(&ix->int_Ar, (size_t)ix->NI * DP))) return rc;
-    if ((rc = ix->alloc(&ix->int_Br, (size_t)ix->NI * DP))) return rc;
-    if ((rc = ix->upload(&ix->int_rowid, rowid, s))) return rc;
-    if ((rc = ix->upload(&ix->int_tdep, tdep, s))) return rc;
+    const char* ep = getenv("CWQ_INT_PATH");
+    ix->int_path = !(ep && *ep && atoi(ep) == 0);
     const float gamma2 = (float)((ix->DPB2 + 64) * std::ldexp(1.0, -23));
     ix->root_w = w_int[0];
     HIPCHK(hipMemcpyAsync(&ix->root_ld, ix->logdet_int, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    for (size_t g = 0; g < segs.size(); ++g) {
-      const int i0 = segs[g].first, n = segs[g].second - segs[g].first;
-      HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes + i0, n, ix->iso_c, ix->logdet_int + i0, ix->par_int + i0,
-                             ix->w_int + i0, DP, ix->DPB2, round_up(n, kFgTile),
-                             ix->int_Mb2 + (size_t)seg_row[g] * ix->DPB2, ix->int_rf2 + seg_row[g],
-                             ix->int_Ar + (size_t)i0 * DP, ix->int_Br + (size_t)i0 * DP, gamma2, s));
+    if ((rc = ix->alloc(&ix->int_Ar, (size_t)ix->NI * DP))) return rc;
+    if ((rc = ix->alloc(&ix->int_Br, (size_t)ix->NI * DP))) return rc;
+    std::vector<int> rowid;
+    if (ix->int_path) {
+      // rows: the root (its exact prefix: final_kernel's chain starts from P[q][0]) and
+      // every internal node with isotropic leaf rows below it, in id order
+      for (int i = 0; i < ix->NI; ++i)
+        if (i == 0 || la1[i] > la0[i]) rowid.push_back(i);
+      ix->ld_i2 = round_up((int64_t)rowid.size(), kFgTile);
+      const int64_t n = (int64_t)rowid.size();
+      rowid.resize(ix->ld_i2, -1);
+      if ((rc = ix->alloc(&ix->int_Mb2, (size_t)ix->DPB2 * ix->ld_i2))) return rc;
+      if ((rc = ix->alloc(&ix->int_rf2, (size_t)ix->ld_i2))) return rc;
+      if ((rc = ix->upload(&ix->int_rowid, rowid, s))) return rc;
+      HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes, ix->NI, ix->iso_c, ix->logdet_int, ix->par_int, ix->w_int, DP,
+                             ix->DPB2, ix->NI, nullptr, nullptr, ix->int_Ar, ix->int_Br, gamma2, s));
+      HIPCHK(launch_int_path_prep(mean, var, dim, d_int_nodes, ix->int_rowid, n, ix->iso_c, ix->logdet_int,
+                                  ix->par_int, ix->w_int, DP, ix->DPB2, ix->ld_i2, ix->int_Mb2, ix->int_rf2, gamma2, s));
+    } else {
+      // level-aligned operand layout: segments [levels 0 and 1], [level 2], [level 3], ...,
+      // each padded to whole 256-row tiles
+      std::vector<std::pair<int, int>> segs;   // internal id ranges
+      for (size_t lv = 0; lv < ix->levels.size(); ++lv) {
+        if (lv == 1) segs.back().second = ix->levels[1].second;
+        else segs.push_back(ix->levels[lv]);
+      }
+      std::vector<int64_t> seg_row(segs.size());
+      int64_t rows = 0;
+      for (size_t g = 0; g < segs.size(); ++g) {
+        seg_row[g] = rows;
+        rows += round_up(segs[g].second - segs[g].first, kFgTile);
+      }
+      ix->ld_i2 = rows;
+      rowid.assign(rows, -1);
+      for (size_t g = 0; g < segs.size(); ++g)
+        for (int i = segs[g].first; i < segs[g].second; ++i) rowid[seg_row[g] + (i - segs[g].first)] = i;
+      if ((rc = ix->alloc(&ix->int_Mb2, (size_t)ix->DPB2 * ix->ld_i2))) return rc;
+      if ((rc = ix->alloc(&ix->int_rf2, (size_t)ix->ld_i2))) return rc;
+      if ((rc = ix->upload(&ix->int_rowid, rowid, s))) return rc;
+      for (size_t g = 0; g < segs.size(); ++g) {
+        const int i0 = segs[g].first, n = segs[g].second - segs[g].first;
+        HIPCHK(launch_int_prep(mean, var, dim, d_int_nodes + i0, n, ix->iso_c, ix->logdet_int + i0, ix->par_int + i0,
+                               ix->w_int + i0, DP, ix->DPB2, round_up(n, kFgTile),
+                               ix->int_Mb2 + (size_t)seg_row[g] * ix->DPB2, ix->int_rf2 + seg_row[g],
+                               ix->int_Ar + (size_t)i0 * DP, ix->int_Br + (size_t)i0 * DP, gamma2, s));
+      }
     }
-    HIPCHK(hipStreamSynchronize(s));   // tdep / rowid host vectors are freed on return
+    HIPCHK(hipStreamSynchronize(s));   // the rowid host vector is freed on return
     ix->int_bounds = true;
   }
   if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
@@ -767,11 +773,14 @@ namespace {
 constexpr int kQPad = 128;   // queries are padded to a multiple of the largest query block
 
 struct Chunk {
-  int* tfail = nullptr;   // fused internal bounds: a dependency wait gave up (device flag)
   int nq = 0;           // valid queries
   int64_t nq_pad = 0;
   float* X = nullptr;   // [nq_pad][DP]
   float *S_int = nullptr, *P = nullptr, *BF = nullptr, *LPF = nullptr;   // [nq_pad][NI]
+  // P / S_int layout (pidx): query-major [q][ldP] (the exact pass); node-major [node][nq_pad]
+  // after the path-sum bounds (run_internal_bounds)
+  int64_t ldP = 1;
+  int pT = 0;
 };
 
 // Query blocks of a launch; a multiple of 8 under the XCD-aware mapping (the
@@ -813,7 +822,7 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
   a.meta = ix->row_meta;
   a.par = ix->row_par;
   a.flags = ix->row_flags;
-  a.P = c.P ? c.P : ix->dummy;
+  a.P = c.P ? c.P : ix->dummy;   // query-major: the scans run with the exact pass's P (never after pT bounds)
   a.ldP = std::max(ix->NI, 1);
   a.xcd_map = scan_xcd_map();
   return a;
@@ -866,13 +875,12 @@ bool use_int_bounds(const cwq_index* ix) {
 }
 
 size_t int_bounds_bytes(const cwq_index* ix, int64_t nqf) {
-  return ix->int_bounds ? (size_t)nqf * ix->DPB2 * 2 + (size_t)nqf * 16 + (size_t)nqf * 4 + 5 * 256 +
-                              (size_t)(nqf / kFgTile) * (ix->ld_i2 / kFgTile) * 4
-                        : 0;
+  return ix->int_bounds ? (size_t)nqf * ix->DPB2 * 2 + (size_t)nqf * 16 + (size_t)nqf * 4 + 5 * 256 : 0;
 }
 
 // Internal nodes by bounds: c.P <- lower, c.S_int <- upper bounds of the path prefix of
-// every internal node (the root exact in both).  q: the caller's [nq][D] queries.
+// the internal nodes the Fast filter reads (int_path: the leaf parents and the root;
+// otherwise every internal node), the root exact in both.  q: the caller's [nq][D] queries.
 int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bump& b, hipStream_t s) {
   uint16_t* Xb2 = b.take<uint16_t>((size_t)nqf * ix->DPB2);
   float4* qinfo2 = b.take<float4>(nqf);
@@ -896,40 +904,27 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   g.ldP = 1;
   g.ldq = nqf;
   g.mode = 2;
+  g.path_sum = ix->int_path ? 1 : 0;
   g.n_rt = (int)(ix->ld_i2 / kFgTile);
-  g.nrows = ix->NI;
   g.lb = c.P;
   g.lb_hi = c.S_int;
   g.ldlb = std::max(ix->NI, 1);
+  if (ix->int_path) {   // node-major lines of nq_pad queries (the chunk's [nq_pad][NI] space)
+    g.pT = 1;
+    g.ldlb = c.nq_pad;
+    c.pT = 1;
+    c.ldP = c.nq_pad;
+  }
   g.Sroot = Sroot;
   g.root_w = ix->root_w;
   g.root_ld = ix->root_ld;
   g.row_id = ix->int_rowid;
   g.nrows = (int)ix->ld_i2;
-  // One launch: with >= 8 query tiles (each XCD keeps its own query tiles, so a row tile's
-  // parent tiles are claimed before it by the same XCD) the prefix bounds are finished in
-  // the epilogue from the parents' final bounds (prefix_step on intervals), each tile
-  // waiting for its parents' tiles -- written once, no separate prefix pass over the
-  // [nq][NI] matrices; CWQ_INT_FUSED=0 keeps the separate per-level prefix passes.
-  const char* ef = getenv("CWQ_INT_FUSED");
-  const bool fused = g.n_qt >= 8 && ix->levels.size() > 2 && !(ef && *ef && atoi(ef) == 0);
-  if (fused) {
-    g.qgroups = 8;
-    g.rgroups = 1;
-    g.fuse_prefix = 1;
-    g.tdep = ix->int_tdep;
-    g.tflag = b.take<int>((size_t)g.n_qt * g.n_rt);
-    g.tfail = b.take<int>(64);
-    HIPCHK(hipMemsetAsync(g.tflag, 0, (size_t)g.n_qt * g.n_rt * 4, s));
-    HIPCHK(hipMemsetAsync(g.tfail, 0, 4, s));
-    c.tfail = g.tfail;
-    HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
-    return CWQ_OK;
-  }
   HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
-  for (size_t lv = 2; lv < ix->levels.size(); ++lv)
-    HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first, ix->levels[lv].second,
-                                ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
+  if (!ix->int_path)
+    for (size_t lv = 2; lv < ix->levels.size(); ++lv)
+      HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first,
+                                  ix->levels[lv].second, ix->par_int, ix->w_int, ix->logdet_int, Sroot, s));
   return CWQ_OK;
 }
 
@@ -961,6 +956,8 @@ bool use_small_scan(const cwq_index* ix, int64_t nq, int K) {
 int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, float dconst, float* out, int64_t ldo,
                   float* pkey, float* paux, int* prow, int K, int* nslab_total_out, hipStream_t s,
                   int seg_mask = 3, int slab_off0 = 0, int max_lists = INT_MAX) {
+  if (c.pT && ((seg_mask & 1) ? ix->NL : ix->NL_an) > 0)   // the scans read query-major exact prefixes
+    return fail(CWQ_ERR_ARG, "leaf scan after node-major prefix bounds (internal error)");
   const int tq = scan_tq(kl);
   const int nqb = n_qblocks_for(c.nq, kl);
   const bool small = epi == EPI_TOPK && !cat && (seg_mask & 1) && use_small_scan(ix, c.nq, K);
@@ -1044,6 +1041,8 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
   c.nq = nq;
   c.nq_pad = round_up(nq, kQPad);
   c.X = b.take<float>((size_t)c.nq_pad * ix->DP);
+  c.ldP = std::max(ix->NI, 1);
+  c.pT = 0;
   if (ix->NI > 0) {
     const size_t n = (size_t)c.nq_pad * ix->NI;
     c.S_int = b.take<float>(n);
@@ -1298,7 +1297,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.rf = ix->iso_rf;
   a.P = c.P ? c.P : ix->dummy;
   a.Phi = ib ? c.S_int : nullptr;
-  a.ldP = std::max(ix->NI, 1);
+  a.ldP = c.ldP;
+  a.pT = c.pT;
   a.eps_n = (float)fc.eps_n;
   a.slack = (float)fc.slack;
   a.Tb = Tb;
@@ -1345,7 +1345,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   const bool ftail = nst == 1 && final_wide_lds(ix->DP, capq) <= 65536 && !getenv("CWQ_FW_UNFUSED");
   const FwExpand fx{ix->sent_ptr, ix->sent_ids, ids, scores, k, ix->hflags};
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
-                      ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, (int64_t)nst * K, okf,
+                      ix->row_par, c.P ? c.P : ix->dummy, c.pT ? 1 : c.ldP, 0, pkey, paux, prow, (int64_t)nst * K, okf,
                       nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s, ftail ? &fx : nullptr));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[2], s));
@@ -1435,8 +1435,7 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   float2* pmm = (!cat && ix->n_multi_tiles) ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
   HIPCHK(launch_query_prep(qsrc, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
   if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
-    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, std::max(ix->NI, 1), nqc, ix->iso_tf, n_rt, pmm, nqf,
-                              s));
+    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s));
   FgArgs g;
   memset(&g, 0, sizeof(g));
   g.DPB = ix->DPB;
@@ -1454,7 +1453,8 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.ldq = nqf;
   g.P = cat ? (c.BF ? c.BF : ix->dummy) : (c.P ? c.P : ix->dummy);
   g.Phi = (!cat && ib) ? c.S_int : nullptr;
-  g.ldP = std::max(ix->NI, 1);
+  g.ldP = cat ? std::max(ix->NI, 1) : c.ldP;
+  g.pT = cat ? 0 : c.pT;
   g.gamma = (float)fc.gamma;
   g.eps_n = (float)fc.eps_n;
   g.slack = (float)fc.slack;
@@ -1615,8 +1615,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
           return rc;
         const IntChain chain = int_chain(ix);
         HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, kFgCapQ, qcnt, qover, crow, cu, cl, tl + (K - 1), 64,
-                            ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow,
-                            (int64_t)nst * K, okf, nex, tlk, tr, tdone, ib ? &chain : nullptr, 0, 0.f, s));
+                            ix->row_meta, ix->row_par, c.P ? c.P : ix->dummy, c.pT ? 1 : c.ldP, 0, pkey, paux,
+                            prow, (int64_t)nst * K, okf, nex, tlk, tr, tdone, ib ? &chain : nullptr, 0, 0.f, s));
         qcnt_d = qcnt;
         nex_d = nex;
         if (ix->timing) HIPCHK(hipEventRecord(ix->ev[7], s));
@@ -1634,12 +1634,8 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         const int* cnth = ix->hflags;
         const int* okh = cnth + nqf;
         const int* nexh = cnth + 2 * nqf;
-        int tf = 0;
-        if (c.tfail) {
-          HIPCHK(hipMemcpy(&tf, c.tfail, 4, hipMemcpyDeviceToHost));
-        }
         for (int i = 0; i < nqc; ++i) {
-          if (!okh[i] || tf) redo.push_back(q0 + i);
+          if (!okh[i]) redo.push_back(q0 + i);
           cand_sum += cnth[i];
           exact_sum += nexh[i];
         }
@@ -1791,6 +1787,42 @@ extern "C" int cwq_node_logprob(cwq_index* ix, const float* q, int64_t nq, int32
       return rc;
     HIPCHK(launch_node_lp(c.S_int ? c.S_int : ix->dummy, std::max(ix->NI, 1), sleaf, std::max(ix->NL, 1), nqc,
                           ix->node_src, ix->logdet_int, ix->logdet_row, dconst, ix->n_nodes, out + q0 * ix->n_nodes, s));
+  }
+  return CWQ_OK;
+}
+
+extern "C" int cwq_prefix_bounds(cwq_index* ix, const float* q, int64_t nq, float* lo, float* hi, float* exact,
+                                 void* stream) {
+  if (!ix || !q || !lo || !hi || !exact) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (nq <= 0 || nq > 4096) return fail(CWQ_ERR_ARG, "nq must be in [1, 4096]");
+  if (!ix->int_bounds)
+    return fail(CWQ_ERR_ARG, "no internal-node bounds on this index (flat tree, no isotropic leaf rows or too deep)");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
+  if (wu.rc) return wu.rc;
+  const int64_t nq_pad = round_up(nq, kQPad), nqf = round_up(nq, kFgTile);
+  int rc;
+  if ((rc = ix->reserve(chunk_bytes(ix, nq_pad, false) + int_bounds_bytes(ix, nqf) + 64 * 256))) return rc;
+  Bump b(ix->ws, ix->ws_size);
+  Chunk c;
+  carve_chunk(ix, b, c, (int)nq, false);
+  const size_t n = (size_t)nq * ix->NI * 4;
+  HIPCHK(launch_pad_queries(q, nq, ix->D, c.X, c.nq_pad, ix->DP, s));
+  if ((rc = run_internal(ix, c, s, false))) return rc;
+  HIPCHK(hipMemcpyAsync(exact, c.P, n, hipMemcpyDeviceToDevice, s));
+  const size_t nall = (size_t)c.nq_pad * ix->NI * 4;
+  HIPCHK(hipMemsetAsync(c.P, 0xff, nall, s));   // NaN where the bound pass writes nothing
+  HIPCHK(hipMemsetAsync(c.S_int, 0xff, nall, s));
+  if ((rc = run_internal_bounds(ix, c, q, nqf, b, s))) return rc;
+  if (c.pT) {   // node-major [NI][nq_pad] -> [nq][NI]
+    HIPCHK(launch_transpose(c.P, ix->NI, nq, c.ldP, lo, ix->NI, s));
+    HIPCHK(launch_transpose(c.S_int, ix->NI, nq, c.ldP, hi, ix->NI, s));
+  } else {
+    HIPCHK(hipMemcpyAsync(lo, c.P, n, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(hi, c.S_int, n, hipMemcpyDeviceToDevice, s));
   }
   return CWQ_OK;
 }

@@ -104,6 +104,9 @@ struct VarSrc {
 
 // ---- launchers (cwq_kernels.hip) ----
 hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s);
+// out[c][r] = in[r][c] (r < rows, c < cols), leading dimensions ld_in / ld_out
+hipError_t launch_transpose(const float* in, int64_t rows, int64_t cols, int64_t ld_in, float* out, int64_t ld_out,
+                            hipStream_t s);
 // rows of `words` 4-byte words: dst[di ? di[i] : i] = src[si ? si[i] : i] (strides in words)
 hipError_t launch_copy_rows(const void* src, int64_t src_stride_w, const int64_t* src_idx, void* dst,
                             int64_t dst_stride_w, const int64_t* dst_idx, int64_t n, int64_t words, hipStream_t s);
@@ -221,6 +224,13 @@ __device__ __forceinline__ void fg_bounds(float dot, float eextra, float4 qi, co
   fg_bounds2(dot, eextra, qi, rf, pi, pi, eps_n, slack, u, l);
 }
 
+// Element (query q, internal node p) of a prefix matrix: query-major [q][ld] (the exact
+// pass) or node-major [p][ld] (pT: the path-sum bounds -- the filter's reads of one
+// parent over a tile's queries and the tile ranges' reads are then coalesced).
+__host__ __device__ __forceinline__ size_t pidx(int64_t ld, int pT, int64_t q, int64_t p) {
+  return pT ? (size_t)(p * ld + q) : (size_t)(q * ld + p);
+}
+
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds),
                                           // 2: internal-node lp' bounds (dense lo/hi)
@@ -231,12 +241,9 @@ struct FgArgs {
   int* tctr;                              // order 2: per-XCD tile counters [8] (zeroed before the launch)
   int dbg;                                // ablation (perf experiments only): 1 no operand loads, 2 no epilogue
   int cat;                                // categorize key: bounds min'ed with P[q][par] (P = BF)
-  int fuse_prefix;                        // mode 2: prefix bounds from the parent's final bounds in the epilogue
-                                          // (rows in level-aligned tiles; a tile waits for its parents' tiles)
+  int path_sum;                           // mode 2: rows are path sums (int_path_prep): bounds of the path
+                                          // prefix P itself (path_bounds); 0: per-node lp' bounds
   const int* row_id;                      // mode 2: operand row -> internal node id (-1: padding)
-  const int2* tdep;                       // mode 2 fused: row tiles holding the parents of row tile rt ([x, y]; x < 0: none)
-  int* tflag;                             // mode 2 fused: [n_qt][n_rt] tile-done flags (zeroed before the launch)
-  int* tfail;                             // mode 2 fused: set when a wait gave up (the host re-runs exactly)
   const float4* qinfo;                    // [nq_pad] {|x'|^2, |x_hi|, |x_lo|, -}
   const float* T;                         // thresholds, T[q * ldT]
   int64_t ldT;
@@ -248,6 +255,7 @@ struct FgArgs {
   const float* P;                         // [nq][ldP] path prefixes of internal nodes (lower bounds when Phi)
   const float* Phi;                       // [nq][ldP] upper bounds of the prefixes (NULL: P is exact)
   int64_t ldP;
+  int pT;                                 // P / Phi (and mode-2 lb / lb_hi) node-major: [node][ldP] (pidx)
   float gamma, eps_n, slack;              // error-bound constants (cwq_mfma.hip header)
   float* lb;                              // sample: [nq_pad][ldlb]; internal bounds (mode 2): lp' lower bounds
   float* lb_hi;                           // internal bounds (mode 2): lp' upper bounds [nq][ldlb]
@@ -311,6 +319,7 @@ struct StreamArgs {
   const float* P;              // [nq][ldP] internal-node path prefixes (lower bounds when Phi)
   const float* Phi;            // [nq][ldP] upper bounds (NULL: P exact)
   int64_t ldP;
+  int pT;                      // node-major P / Phi (pidx)
   float eps_n, slack;
   int* Tb;                     // [K][nq] ordered-int block maxima of candidate lower bounds (filter)
   int* Tlive;                  // [nq] ordered-int live threshold (= Tb + K * nq)
@@ -343,6 +352,14 @@ hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp,
 hipError_t launch_int_prep(const float* mean, const VarSrc& var, int D, const int64_t* nodes, int64_t n,
                            const float* c, const float* logdet, const int* par_int, const float* w_int, int DP, int DPB2,
                            int64_t ld, void* Mb2, RowF* rf, float* Ar, float* Br, float gamma, hipStream_t s);
+// Path-sum operands (the Fast filter's leaf parents): for internal node i = rows[r] (the
+// root: an exact row, par -1), Bsum = sum over the path's non-root nodes a of w_a b'_a as
+// bf16 hi [ld][DPB2] and RowF {R0 = Zc, beta, delta, rn2 = K0, hs = Zq, hl = cr, invL 0,
+// par} for path_bounds (cwq_mfma.hip); padding rows par -2.  nodes: node id per internal id.
+hipError_t launch_int_path_prep(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const int* rows,
+                                int64_t n, const float* c, const float* logdet, const int* par_int,
+                                const float* w_int, int DP, int DPB2, int64_t ld, void* Mb2, RowF* rf, float gamma,
+                                hipStream_t s);
 // Queries for the internal bounds: a = [x'^2, x'] bf16 hi [nq_pad][DPB2], qinfo =
 // {sum x^2 + sum x'^2, |a_hi|, |a_lo|, 0}.
 hipError_t launch_query_prep2(const float* q, int64_t nq, int D, const float* c, int DP, int DPB2, int64_t nq_pad,
@@ -361,8 +378,8 @@ struct IntChain {
   const float* w_int;
   const float* logdet_int;
 };
-hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int nq, const TileF* tf, int n_rt,
-                              float2* pmm, int64_t ldq, hipStream_t s);
+hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int pT, int nq, const TileF* tf,
+                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
 // lkb/lrb [nq][64] and done [nq] carry each query's top-K candidate lower bounds between

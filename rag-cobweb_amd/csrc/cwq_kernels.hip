@@ -1637,6 +1637,28 @@ __global__ void pad_queries_kernel(const float* __restrict__ q, int64_t nq, int 
   }
 }
 
+// 32 x 32 tiles through LDS (diagnostic copies)
+__global__ void transpose_kernel(const float* __restrict__ in, int64_t rows, int64_t cols, int64_t ld_in, float* out,
+                                 int64_t ld_out) {
+  __shared__ float t[32][33];
+  const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 8 rows per pass
+  for (int i = ty; i < 32; i += 8)
+    if (r0 + i < rows && c0 + tx < cols) t[i][tx] = in[(r0 + i) * ld_in + c0 + tx];
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8)
+    if (c0 + i < cols && r0 + tx < rows) out[(c0 + i) * ld_out + r0 + tx] = t[tx][i];
+}
+
+hipError_t launch_transpose(const float* in, int64_t rows, int64_t cols, int64_t ld_in, float* out, int64_t ld_out,
+                            hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if ((rows + 31) / 32 > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32)), dim3(256), 0,
+                     s, in, rows, cols, ld_in, out, ld_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_pad_queries(const float* q, int64_t nq, int D, float* X, int64_t nq_pad, int DP, hipStream_t s) {
   const int64_t total = nq_pad * DP;
   hipLaunchKernelGGL(pad_queries_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)), dim3(256), 0, s, q, nq,

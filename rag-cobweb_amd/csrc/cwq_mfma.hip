@@ -298,7 +298,7 @@ __global__ void int_prep_kernel(const float* __restrict__ mean, const VarSrc var
     const __bf16 h = (__bf16)v;
     const float hf = (float)h;
     const float lo = v - hf;
-    Mb2[r * DPB2 + k] = h;
+    if (Mb2) Mb2[r * DPB2 + k] = h;
     shi += (double)hf * (double)hf;
     slo += (double)lo * (double)lo;
   }
@@ -324,7 +324,7 @@ __global__ void int_prep_kernel(const float* __restrict__ mean, const VarSrc var
     } else {
       f = RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
     }
-    rf[r] = f;
+    if (rf) rf[r] = f;
   }
 }
 
@@ -334,6 +334,113 @@ hipError_t launch_int_prep(const float* mean, const VarSrc& var, int D, const in
   if (ld <= 0) return hipSuccess;
   hipLaunchKernelGGL(int_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, var, D, nodes, n, c,
                      logdet, par_int, w_int, DP, DPB2, ld, (__bf16*)Mb2, rf, Ar, Br, gamma);
+  return hipGetLastError();
+}
+
+// Path-sum operands (launch_int_path_prep, cwq_internal.h).  The Fast filter needs the path
+// prefix P(n) = P(root) + sum_a w_a lp'(a) of leaf parents n only (a: the path's non-root
+// nodes), and with int_prep's split lp'(a) = -0.5 (logdet_a + c_a) + a.b'_a that sum is one
+// linear form in the query vector a = [x'^2, x']:
+//   P(n) - P(root) = K0 + a.Bsum,  K0 = -0.5 sum w_a (logdet_a + c_a),  Bsum = sum w_a b'_a,
+// so one GEMM row per leaf parent replaces a row per internal node and the level-by-level
+// prefix passes.  Bsum is accumulated in fp64 from int_prep's fp32 b' values and rounded
+// once.  The bound must hold for the exact pass's fp32 chain P_i = fmaf(w_i, lp'_fp32(i),
+// P_{i-1}); its distance to the real sum is bounded per node a, as int_bounds does, by
+// 2^-12 (wmax_a qx + M_a + |logdet_a| + c_a) (the fp32 S evaluation, lp' roundings; |S_a|
+// <= 2 wmax_a |x'|^2 + 2 c_a), plus one rounding of <= 2^-24 |P_i| per chain step with
+// |P_i| <= |P(root)| + sum_a (|logdet_a| + c_a + M_a + 1.01 wmax_a qx) |w_a|.  Hence, with
+// Z3 = sum |w_a| wmax_a, Z0 = sum |w_a| (M_a + |logdet_a| + c_a), depth = path length:
+//   Zq = cz Z3, Zc = cz Z0 + 2^-23 |K0|, cz = 1.02 (2^-12 + depth 2^-24), cr = depth 2^-24 + 2^-22
+// (the 1.02 also covers Bsum's fp32 rounding, <= 2^-24 sum |w_a| (wmax_a qx + c_a)).
+// One wave per row.
+__global__ void int_path_prep_kernel(const float* __restrict__ mean, const VarSrc var, int D,
+                                     const int64_t* __restrict__ nodes, const int* __restrict__ rows, int64_t n,
+                                     const float* __restrict__ c, const float* __restrict__ logdet,
+                                     const int* __restrict__ par_int, const float* __restrict__ w_int, int DP, int DPB2,
+                                     int64_t ld, __bf16* Mb2, RowF* rf, float gamma) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= ld) return;
+  const int i = r < n ? rows[r] : -1;
+  // per-node scalar terms, node by node up the path (the root excluded)
+  double K0 = 0.0, Z0 = 0.0, Z3 = 0.0;
+  int depth = 0;
+  for (int a = i; a >= 0 && par_int[a] >= 0; a = par_int[a]) {
+    ++depth;
+    const int64_t nd = nodes[a];
+    double cn = 0.0, mn = 0.0;
+    float wmax = 0.f;
+    for (int d = lane; d < D; d += kWave) {
+      const float A = 1.0f / sqrtf(var.at(nd, d, D));   // as int_prep
+      const float w = A * A;
+      const float mu = mean[nd * (int64_t)D + d];
+      const float mc = mu - c[d];
+      const double am = fabs((double)mu) + fabs((double)c[d]);
+      cn += (double)mc * (double)mc * (double)w;
+      mn += (double)w * am * am;
+      wmax = fmaxf(wmax, w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      cn += __shfl_xor(cn, off, 64);
+      mn += __shfl_xor(mn, off, 64);
+      wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
+    }
+    const double wa = (double)w_int[a], ld_a = (double)logdet[a];
+    K0 += -0.5 * wa * (ld_a + cn);
+    Z0 += fabs(wa) * (mn + fabs(ld_a) + cn);
+    Z3 += fabs(wa) * (double)wmax;
+  }
+  // Bsum, bf16 hi parts and the split norms
+  double shi = 0.0, slo = 0.0;
+  for (int k = lane; k < DPB2; k += kWave) {
+    const int d = k < DP ? k : k - DP;
+    double acc = 0.0;
+    if (k < 2 * DP && d < D)
+      for (int a = i; a >= 0 && par_int[a] >= 0; a = par_int[a]) {
+        const int64_t nd = nodes[a];
+        const float A = 1.0f / sqrtf(var.at(nd, d, D));
+        const float w = A * A;
+        const float v = k < DP ? -0.5f * w : (mean[nd * (int64_t)D + d] - c[d]) * w;   // int_prep's b'
+        acc += (double)w_int[a] * (double)v;
+      }
+    const float v = (float)acc;
+    const __bf16 h = (__bf16)v;
+    const float hf = (float)h;
+    const float lo = v - hf;
+    Mb2[r * DPB2 + k] = h;
+    shi += (double)hf * (double)hf;
+    slo += (double)lo * (double)lo;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    shi += __shfl_xor(shi, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+  }
+  if (lane == 0) {
+    RowF f = RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+    if (i >= 0) {
+      f.par = par_int[i];   // -1: the root (exact row)
+      if (f.par >= 0) {
+        const double bh = sqrt(shi) * (1.0 + 0x1p-20), bl = sqrt(slo) * (1.0 + 0x1p-20);
+        const double cz = 1.02 * (0x1p-12 + depth * 0x1p-24);
+        f.beta = up(bl + (double)gamma * bh);
+        f.delta = up(bh + bl);
+        f.rn2 = (float)K0;
+        f.hs = up(cz * Z3);
+        f.R0 = up(cz * Z0 + 0x1p-23 * fabs(K0));
+        f.hl = up(depth * 0x1p-24 + 0x1p-22);
+      }
+    }
+    rf[r] = f;
+  }
+}
+
+hipError_t launch_int_path_prep(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const int* rows,
+                                int64_t n, const float* c, const float* logdet, const int* par_int,
+                                const float* w_int, int DP, int DPB2, int64_t ld, void* Mb2, RowF* rf, float gamma,
+                                hipStream_t s) {
+  if (ld <= 0) return hipSuccess;
+  hipLaunchKernelGGL(int_path_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, var, D, nodes, rows,
+                     n, c, logdet, par_int, w_int, DP, DPB2, ld, (__bf16*)Mb2, rf, gamma);
   return hipGetLastError();
 }
 
@@ -453,6 +560,21 @@ __device__ __forceinline__ void int_bounds(float dot, float4 qi, const RowF& f, 
   const float m = 0x1p-20f * (fabsf(f.hl) + Shi);
   hi = -0.5f * (f.hl + Slo) + m;
   lo = -0.5f * (f.hl + Shi) - m;
+}
+
+// Path-sum row (int_path_prep_kernel): bounds lo <= P_fp32(n) <= hi of the exact pass's
+// path prefix from the MFMA dot a_hi.Bsum_hi and the exact root prefix proot.  RowF fields:
+// rn2 = K0, beta/delta = Bsum's split norms, hs = Zq, R0 = Zc, hl = cr; qinfo {qx, |a_hi|,
+// |a_lo|}.  2^-21 (|dot| + |K0| + |proot|) covers the dot's last rounding and the two fp32
+// additions; (1 + 2^-20) the evaluation of E and the final subtractions.
+__device__ __forceinline__ void path_bounds(float dot, float4 qi, const RowF& f, float proot, float& lo, float& hi) {
+  const float s = proot + (f.rn2 + dot);
+  const float ap = fabsf(proot);
+  const float E = (fmaf(qi.y, f.beta, qi.z * f.delta) + fmaf(f.hs, qi.x, f.R0) + f.hl * ap +
+                   0x1p-21f * (fabsf(dot) + fabsf(f.rn2) + ap)) *
+                  (1.f + 0x1p-20f);
+  lo = s - E;
+  hi = s + E;
 }
 
 // XCD-local tile i -> (query tile, row tile).  order 0/2: query tiles fastest (the
@@ -633,8 +755,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       qi = a.qinfo[qs];
       if (qs < a.nq && MODE == 0) Tq = a.T[(size_t)qs * a.ldT];
       if (uni && tf.par >= 0 && qs < a.nq) {
-        Pq = Pu[(size_t)qs * a.ldP + tf.par];
-        Pql = a.P[(size_t)qs * a.ldP + tf.par];
+        Pq = Pu[pidx(a.ldP, a.pT, qs, tf.par)];
+        Pql = a.P[pidx(a.ldP, a.pT, qs, tf.par)];
       }
     }
     float R0[4];
@@ -775,33 +897,53 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     // blocks: jb (16 rows) x half (query blocks 0-3 / 4-7): 16 values per lane
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
+    if (MODE == 2 && a.pT) {
+      // path-sum bounds, node-major [node][ldlb]: lane (r16, c16) of MFMA block (ib, jb)
+      // holds queries 4 c16 .. 4 c16 + 3 of one row -- 16 contiguous bytes of that node's
+      // line -- so the bounds go straight from the accumulators to float4 stores (a store
+      // instruction covers 16 rows x 64 B), no LDS transpose
+      RowF f[4];
+      int rid[4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int r = r0 + wr * 64 + jb * 16 + r16;
+        f[jb] = r < a.nrows ? a.rf[r] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+        rid[jb] = r < a.nrows ? a.row_id[r] : -1;
+      }
+#pragma unroll
+      for (int ib = 0; ib < 8; ++ib) {
+        const int ql = wq * 128 + ib * 16 + 4 * c16;
+        const int q = q0 + ql;
+        if (q >= a.ldlb) continue;   // query padding beyond the lines (ldlb: a multiple of 4)
+        float4 qi[4];
+        float pr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          qi[j] = s_qi[ql + j];
+          pr[j] = s_pl[ql + j];
+        }
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          if (f[jb].par < -1 || rid[jb] < 0) continue;
+          float lo[4], hi[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (f[jb].par < 0) lo[j] = hi[j] = pr[j];   // the root: its exact prefix
+            else path_bounds(acc[ib][jb][j], qi[j], f[jb], pr[j], lo[j], hi[j]);
+          }
+          const size_t o = (size_t)rid[jb] * a.ldlb + q;
+          *reinterpret_cast<float4*>(a.lb + o) = make_float4(lo[0], lo[1], lo[2], lo[3]);
+          *reinterpret_cast<float4*>(a.lb_hi + o) = make_float4(hi[0], hi[1], hi[2], hi[3]);
+        }
+      }
+      goto flush;
+    }
     if (MODE == 2) {
       // internal-node bounds, dense: per 16-query block ib, the wave's 16 x 64 block goes
       // through LDS so that each store covers 64 consecutive rows of one query (256 B)
       const int rl = r0 + wr * 64 + lane;   // this lane's row in the store phase
       const RowF f = rl < a.nrows ? a.rf[rl] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
       const int rid = a.row_id ? (rl < a.nrows ? a.row_id[rl] : -1) : rl;   // internal node id
-      if (a.fuse_prefix) {
-        // the parents' final prefix bounds come from earlier row tiles of this query tile
-        // (a level's rows start a new tile, so parents are never in the same tile): wait
-        // for their done flags (agent-scope acquire), bounded
-        const int2 dp = a.tdep[rt];
-        if (tid == 0 && dp.x >= 0) {
-          for (int t = dp.x; t <= dp.y; ++t) {
-            int* fl = a.tflag + (size_t)qt * a.n_rt + t;
-            int spins = 0;
-            while (__hip_atomic_load(fl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-              __builtin_amdgcn_s_sleep(2);
-              if (++spins > (1 << 24)) {   // never expected: give up, flag the call for the exact path
-                __hip_atomic_store(a.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __syncthreads();
-      }
       // ib unrolled: a dynamically indexed acc[ib] would be copied to scratch memory
 #pragma unroll
       for (int ib = 0; ib < 8; ++ib) {
@@ -822,23 +964,17 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             float lo, hi;
             if (f.par < 0) {   // the root: its exact prefix
               lo = hi = s_pl[ql];
+            } else if (a.path_sum) {   // the path prefix itself
+              path_bounds(d0, s_qi[ql], f, s_pl[ql], lo, hi);
             } else {
               int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
               if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
-              else if (a.fuse_prefix)   // deeper: the parent's final bounds (its tile is done)
-                prefix_step(a.lb[(size_t)q * a.ldlb + f.par], a.lb_hi[(size_t)q * a.ldlb + f.par], f.invL, lo, hi);
             }
             a.lb[(size_t)q * a.ldlb + rid] = lo;
             a.lb_hi[(size_t)q * a.ldlb + rid] = hi;
           }
         }
         __builtin_amdgcn_wave_barrier();   // reads of this block done before the next dump
-      }
-      if (a.fuse_prefix) {
-        // this tile's bounds are final: every storing thread's release, then the flag
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(a.tflag + (size_t)qt * a.n_rt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       goto flush;
     }
@@ -887,10 +1023,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 d0 = acc[ib][jb][j];
               }
             const float4 qi = s_qi[ql];
-            const float pi = (fb.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + fb.par] * fb.invL : 0.f;
+            const float pi = (fb.par >= 0 && q < a.nq) ? a.P[pidx(a.ldP, a.pT, q, fb.par)] * fb.invL : 0.f;
             float u;
             fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, fb, pi, a.eps_n, a.slack, u, m);
-            if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, a.P[(size_t)q * a.ldP + fb.par]);
+            if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, a.P[pidx(a.ldP, a.pT, q, fb.par)]);
           }
           a.lb[(size_t)q * a.ldlb + g] = m;
         }
@@ -942,8 +1078,6 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 } else {
                   int_bounds(d0, s_qi[ql], f, a.gamma, lo, hi);
                   if (f.par == 0) prefix_step(s_pl[ql], s_pl[ql], f.invL, lo, hi);   // depth 1: fused
-                  else if (a.fuse_prefix)
-                    prefix_step(a.lb[(size_t)q * a.ldlb + f.par], a.lb_hi[(size_t)q * a.ldlb + f.par], f.invL, lo, hi);
                 }
                 a.lb[(size_t)q * a.ldlb + r] = lo;
                 a.lb_hi[(size_t)q * a.ldlb + r] = hi;
@@ -952,10 +1086,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               float lo = -CWQ_INF;
               if (usable) {
                 const float4 qi = s_qi[ql];
-                const float pi = (f.par >= 0 && q < a.nq) ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+                const float pi = (f.par >= 0 && q < a.nq) ? a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
                 float u;
                 fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f, pi, a.eps_n, a.slack, u, lo);
-                if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, a.P[(size_t)q * a.ldP + f.par]);
+                if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, a.P[pidx(a.ldP, a.pT, q, f.par)]);
               }
               a.lb[(size_t)q * a.ldlb + r] = lo;
             } else if (usable && q < a.nq && (!uni || d0 >= 0.f)) {
@@ -966,8 +1100,8 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 d = d0 - init;
                 ex = a.gamma * fabsf(init) + 0x1p-23f * (fabsf(d0) + fabsf(init));
                 if (!ALLUNI && multi) {
-                  pi = Pu[(size_t)q * a.ldP + f.par] * f.invL;
-                  pl = a.P[(size_t)q * a.ldP + f.par] * f.invL;
+                  pi = Pu[pidx(a.ldP, a.pT, q, f.par)] * f.invL;
+                  pl = a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL;
                 } else {
                   pi = s_pi[ql];
                   pl = s_pl[ql];
@@ -975,13 +1109,13 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               } else {
                 d = d0;
                 ex = 0x1p-23f * fabsf(d0);
-                pi = f.par >= 0 ? Pu[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
-                pl = f.par >= 0 ? a.P[(size_t)q * a.ldP + f.par] * f.invL : 0.f;
+                pi = f.par >= 0 ? Pu[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
+                pl = f.par >= 0 ? a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
               }
               float u, lo;
               fg_bounds2(d, ex, qi, f, pi, pl, a.eps_n, a.slack, u, lo);
               if (a.cat && f.par >= 0) {   // categorize key min(BF[parent], lp)
-                const float bp = a.P[(size_t)q * a.ldP + f.par];
+                const float bp = a.P[pidx(a.ldP, a.pT, q, f.par)];
                 u = fminf(u, bp);
                 lo = fminf(lo, bp);
               }
@@ -1267,9 +1401,46 @@ __global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restric
   if (act) pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
 }
 
-hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int nq, const TileF* tf, int n_rt,
-                              float2* pmm, int64_t ldq, hipStream_t s) {
+// Node-major prefixes (pidx pT): thread = query, one tile per blockIdx.y; the tile's parents
+// are read one line at a time, each read coalesced over the block's 256 queries.
+__global__ __launch_bounds__(256) void tile_prange_t_kernel(const float* __restrict__ P, const float* __restrict__ Phi,
+                                                            int64_t ldP, int nq, const TileF* __restrict__ tf,
+                                                            int t0, float2* __restrict__ pmm, int64_t ldq) {
+  const int t = t0 + blockIdx.y;
+  const TileF T = tf[t];
+  if (T.uniform != 2) return;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  float mn0 = CWQ_INF, mx0 = -CWQ_INF, mn1 = CWQ_INF, mx1 = -CWQ_INF;
+  int p = T.par;
+  for (; p + 1 <= T.par_hi; p += 2) {   // two lines in flight per step
+    const float a0 = P[(size_t)p * ldP + q], b0 = Phi[(size_t)p * ldP + q];
+    const float a1 = P[(size_t)(p + 1) * ldP + q], b1 = Phi[(size_t)(p + 1) * ldP + q];
+    mn0 = fminf(mn0, fminf(a0 * T.invL, b0 * T.invL));
+    mx0 = fmaxf(mx0, fmaxf(a0 * T.invL, b0 * T.invL));
+    mn1 = fminf(mn1, fminf(a1 * T.invL, b1 * T.invL));
+    mx1 = fmaxf(mx1, fmaxf(a1 * T.invL, b1 * T.invL));
+  }
+  if (p <= T.par_hi) {
+    const float a0 = P[(size_t)p * ldP + q], b0 = Phi[(size_t)p * ldP + q];
+    mn0 = fminf(mn0, fminf(a0 * T.invL, b0 * T.invL));
+    mx0 = fmaxf(mx0, fmaxf(a0 * T.invL, b0 * T.invL));
+  }
+  pmm[(size_t)t * ldq + q] = make_float2(fminf(mn0, mn1), fmaxf(mx0, mx1));
+}
+
+hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int pT, int nq, const TileF* tf,
+                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s) {
   static_assert(kPrQ * kPrTiles <= 256, "one thread per (query, tile)");
+  if (pT) {
+    if (nq <= 0 || n_rt <= 0) return hipSuccess;
+    for (int t0 = 0; t0 < n_rt; t0 += 65535) {   // grid y limit
+      hipLaunchKernelGGL(tile_prange_t_kernel, dim3((unsigned)((nq + 255) / 256), (unsigned)std::min(65535, n_rt - t0)),
+                         dim3(256), 0, s, P, Phi ? Phi : P, ldP, nq, tf, t0, pmm, ldq);
+      if (hipError_t e = hipGetLastError()) return e;
+    }
+    return hipSuccess;
+  }
   const int64_t blocks = (int64_t)((nq + kPrQ - 1) / kPrQ) * ((n_rt + kPrTiles - 1) / kPrTiles);
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(tile_prange_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P, Phi ? Phi : P, ldP, nq, tf, n_rt,
@@ -1478,8 +1649,10 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         const int rr = crow[base + jj];
         const RowMeta md = meta[rr];
         const int p = par[rr];
-        float pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);   // exact (cat: BF)
-        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
+        // exact (cat: BF); with the chain only the root's P[q][0] is read (ldP 1: node-major)
+        float pp = p < 0 ? (cat ? CWQ_INF : 0.f)
+                         : (use_chain && p > 0 ? exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP])
+                                               : P[(size_t)q * ldP + p]);
         key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp, cat, dconst);
         rid = seg_base + rr;
         ++nx;
@@ -1631,8 +1804,9 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       }
       float pp = 0.f;
       if (wave == 0 && lane < cnt) {
-        pp = p >= 0 ? P[(size_t)q * ldP + p] : (cat ? CWQ_INF : 0.f);
-        if (use_chain && p > 0) pp = exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]);
+        pp = p < 0 ? (cat ? CWQ_INF : 0.f)
+                   : (use_chain && p > 0 ? exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP])
+                                         : P[(size_t)q * ldP + p]);
       }
       __syncthreads();
       if (wave == 0) {

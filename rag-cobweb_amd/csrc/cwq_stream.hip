@@ -202,7 +202,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         cpar = rf[j].par;
 #pragma unroll
         for (int qb = 0; qb < MQB; ++qb) {
-          const size_t o = (size_t)(qb * 16 + r16) * a.ldP + cpar;
+          const size_t o = pidx(a.ldP, a.pT, qb * 16 + r16, cpar);
           cP[qb] = (qok[qb] && cpar >= 0) ? a.P[o] : 0.f;
           cPh[qb] = (qok[qb] && cpar >= 0) ? Pu[o] : 0.f;
         }

@@ -214,6 +214,18 @@ class CobwebIndex:
                                          _stream(self.device)))
         return out
 
+    def prefix_bounds(self, q):
+        """Diagnostic: (lo, hi, exact) [nq, n_internal] -- the Fast path prefixes of the
+        internal nodes (BFS order) by the exact pass, and the bf16-MFMA bounds the filter
+        uses on hierarchical trees (NaN where the filter reads none)."""
+        q = self._queries(q)
+        shape = (q.shape[0], int(self.info["internal_nodes"]))
+        lo, hi, ex = (torch.empty(shape, dtype=torch.float32, device=self.device) for _ in range(3))
+        with torch.cuda.device(self.device):
+            check(self._L.cwq_prefix_bounds(self._h, _ptr(q), q.shape[0], _ptr(lo), _ptr(hi), _ptr(ex),
+                                          _stream(self.device)))
+        return lo, hi, ex
+
     def categorize(self, q, k, max_nodes=100000):
         """Best-first categorize ("Cobweb Basic", A4): retrieved BFS node ids in pop
         order [nq, k], number found [nq], log_prob call count [nq]."""

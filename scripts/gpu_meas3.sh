@@ -26,6 +26,14 @@ for s in "$@"; do
       step fit_host_2k 600 python scripts/fit_probe.py --n 2000 --dim 768 --clusters 20 --host &&
       step fit_dev_20k 600 python scripts/fit_probe.py --n 20000 --dim 768 --clusters 50 ;;
     fit100k) step fit_dev_100k 1000 python scripts/fit_probe.py --n 100000 --dim 768 --clusters 100 ;;
+    pathtest) step pytest_path 900 python -u -m pytest -x -v -s -p no:cacheprovider --timeout 400 --timeout-method thread \
+        tests/test_gpu_filter.py -k "prefix_bounds or deep_balanced or internal_bounds or hierarchical or two_level" ;;
+    pathab) step fast_b4_path 600 python scripts/filter_probe.py --balanced 4,9 --modes 1 &&
+      step fast_b4_nodes 600 env CWQ_INT_PATH=0 python scripts/filter_probe.py --balanced 4,9 --modes 1 &&
+      step fast_b10_path 600 python scripts/filter_probe.py --balanced 10,5 --modes 1 &&
+      step fast_g100k_path 600 python scripts/filter_probe.py --clusters 100000 --modes 1 ;;
+    proffastb4) step prof_fast_b4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fb4 -o fb4 --output-format csv -- \
+        python3 scripts/filter_probe.py --balanced 4,9 --modes 1 --reps 2 ;;
     c4) step c4_preset 600 python bench.py --preset c4 --steps 3 --warmup 1 --no-cpu-baseline --no-per-call ;;
     cat100k) step cat_g100k 600 python scripts/basic_probe.py --clusters 100000 --queries 2000 --reps 2 ;;
     cat1024) step cat_g1024 600 python scripts/basic_probe.py --clusters 1024 --queries 10000 --reps 2 ;;

@@ -355,13 +355,13 @@ def test_categorize_filter_equals_exact(gpu, N, D, G, k):
 
 
 @pytest.mark.parametrize("branching,depth", [(4, 6), (3, 8), (10, 3)])
-@pytest.mark.parametrize("levels", ["1", "0"])
-def test_deep_balanced_tree(gpu, branching, depth, levels, monkeypatch):
+@pytest.mark.parametrize("path", ["1", "0"])
+def test_deep_balanced_tree(gpu, branching, depth, path, monkeypatch):
     """Deep trees shaped like Cobweb hierarchies (synth.balanced_synth): internal-node
-    bounds one launch per level with fused prefix steps (CWQ_INT_LEVELS=1, default) or one
-    launch + per-level prefix passes (0); multi-parent leaf tiles with up to ~90 parents;
-    ids and scores identical to the exact scan, batch and per-call paths."""
-    monkeypatch.setenv("CWQ_INT_LEVELS", levels)
+    bounds as path sums over the leaf parents (CWQ_INT_PATH=1, default) or per node plus
+    per-level prefix passes (0); multi-parent leaf tiles with up to ~90 parents; ids and
+    scores identical to the exact scan, batch and per-call paths."""
+    monkeypatch.setenv("CWQ_INT_PATH", path)
     X = gpu.synth.synthetic_corpus(30000, 64, seed=61)
     t = gpu.synth.balanced_synth(X, branching, depth, seed=62)
     ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
@@ -370,4 +370,59 @@ def test_deep_balanced_tree(gpu, branching, depth, levels, monkeypatch):
         ids0, s0, ids1, s1, st = both(ix, q, 10)
         assert st["filter_used"], st
         assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    ix.close()
+
+
+def _bounds_tree(pkg, name):
+    if name.startswith("three_level"):
+        X = pkg.synth.synthetic_corpus(40000, 96, seed=71)
+        mean, var, parent, nos = three_level(pkg, X, 200, 4)
+        w = (1.0, -0.5, 2.0, 1.0) if name.endswith("negw") else (0.3, 1.0, 1.0, 1.5)
+        return X, mean, var, np.asarray(parent), nos, w
+    if name.startswith("balanced"):
+        b, d = (int(v) for v in name.split("_")[1:])
+        X = pkg.synth.synthetic_corpus(30000, 64, seed=72)
+        t = pkg.synth.balanced_synth(X, b, d, seed=73)
+    else:
+        X = pkg.synth.synthetic_corpus(50000, 256, seed=74)
+        lab = torch.randint(0, 3000, (X.shape[0],), device="cuda:0",
+                            generator=torch.Generator(device="cuda:0").manual_seed(75))
+        t = pkg.synth.two_level_synth(X, lab)
+    return X, t["mean"], t["var"], np.asarray(t["parent"]), t["node_of_sentence"], None
+
+
+@pytest.mark.parametrize("tree", ["three_level", "three_level_negw", "balanced_4_6", "balanced_3_8", "two_level"])
+@pytest.mark.parametrize("path", ["1", "0"])
+def test_prefix_bounds_enclose_exact(gpu, tree, path, monkeypatch):
+    """The bf16-MFMA internal bounds the Fast filter reads enclose the exact pass's fp32
+    path prefixes (cwq_prefix_bounds): path sums over the leaf parents (CWQ_INT_PATH=1)
+    and per-node bounds + prefix passes (0), level weights incl. a negative one, queries
+    near the data and far from it.  Every leaf parent has finite bounds; the widths stay
+    far below the prefixes' magnitude (the pretest keeps its pruning power)."""
+    monkeypatch.setenv("CWQ_INT_PATH", path)
+    X, mean, var, parent, nos, w = _bounds_tree(gpu, tree)
+    ix = gpu.index.CobwebIndex(mean, var, parent, nos, w, device="cuda:0")
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=76)
+    g = torch.Generator(device="cuda:0").manual_seed(77)
+    Q = torch.cat([Q, 3.0 * torch.randn(40, X.shape[1], device="cuda:0", generator=g)])
+    lo, hi, ex = ix.prefix_bounds(Q)
+    n = parent.shape[0]
+    nch = np.bincount(parent[1:], minlength=n)
+    internal = np.nonzero(nch > 0)[0]
+    leafpar = np.zeros(n, dtype=bool)
+    kids = np.arange(1, n)
+    leafpar[parent[1:][nch[kids] == 0]] = True
+    need = torch.from_numpy(leafpar[internal]).to("cuda:0")
+    fin = torch.isfinite(lo) & torch.isfinite(hi)
+    assert bool(fin[:, need].all()), "a leaf parent without bounds"
+    if path == "0":
+        assert bool(fin.all())
+    assert bool(torch.isfinite(ex).all())
+    ok = (lo <= ex) & (ex <= hi)
+    bad = (~ok & fin).nonzero()
+    assert bad.shape[0] == 0, [(int(q), int(i), float(lo[q, i]), float(ex[q, i]), float(hi[q, i]))
+                               for q, i in bad[:5].tolist()]
+    rel = ((hi - lo) / ex.abs().clamp_min(1.0))[fin]
+    print(f"{tree} path={path}: rel width median {float(rel.median()):.2e} max {float(rel.max()):.2e}")
+    assert float(rel.median()) < 5e-2
     ix.close()
