@@ -65,12 +65,15 @@ class CwqError(RuntimeError):
         self.rc = rc
 
 
-def load_library(path):
-    """A configured CDLL for a libcwq build at ``path``."""
+def load_library(path, strict=True):
+    """A configured CDLL for a libcwq build at ``path``.  strict=False (A/B scripts
+    loading older builds only) skips entry points the build does not export."""
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: build it with __graft_entry__.build()")
     L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

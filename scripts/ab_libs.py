@@ -74,7 +74,7 @@ def main():
             arms.append(arms[0])
             continue
         with env(knobs[p]):
-            L._lib = L.load_library(os.path.abspath(p.split("@")[0]))
+            L._lib = L.load_library(os.path.abspath(p.split("@")[0]), strict=False)
             ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)
             ix.set_filter(1)
             ix.score_topk(Q, args.k)
