@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -129,6 +130,7 @@ struct cwq_index {
   uint16_t* int_Mb2 = nullptr;
   RowF* int_rf2 = nullptr;
   int* int_rowid = nullptr;           // operand row -> internal id (-1: padding)
+  RowF* int_nrf = nullptr;            // int_path: int_rf2 by internal id (par -2: no operand row), PathB
   float *int_Ar = nullptr, *int_Br = nullptr;
   float root_w = 1.f, root_ld = 0.f;   // the root's level weight and logdet (host copies)
   int* samp_rows = nullptr;
@@ -150,6 +152,7 @@ struct cwq_index {
   size_t ws_budget = 0;   // query-chunk workspace budget, from the free memory at the first call
   hipEvent_t ws_ev = nullptr;
   bool ws_ev_live = false;
+  hipStream_t ws_ev_stream = nullptr;   // the stream ws_ev was last recorded on
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
   size_t hflags_n = 0;
   // fallback re-runs (cwq_score_topk / cwq_categorize): gathered queries, their results
@@ -202,7 +205,10 @@ struct cwq_index {
   int ws_begin(hipStream_t s) {
     if (!ws_ev && hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming) != hipSuccess)
       return fail(CWQ_ERR_HIP, "hipEventCreate failed");
-    if (ws_ev_live && hipStreamWaitEvent(s, ws_ev, 0) != hipSuccess) return fail(CWQ_ERR_HIP, "hipStreamWaitEvent failed");
+    // a call on the stream of the previous one is ordered after it already (no barrier
+    // packet on the per-call path)
+    if (ws_ev_live && s != ws_ev_stream && hipStreamWaitEvent(s, ws_ev, 0) != hipSuccess)
+      return fail(CWQ_ERR_HIP, "hipStreamWaitEvent failed");
     return CWQ_OK;
   }
   // end of a query call: the workspace is busy until the work queued on s so far is done
@@ -215,6 +221,7 @@ struct cwq_index {
       return fail(CWQ_ERR_HIP, "hipEventRecord failed");
     }
     ws_ev_live = true;
+    ws_ev_stream = s;
     return CWQ_OK;
   }
   ~cwq_index() {
@@ -647,6 +654,12 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
                              ix->DPB2, ix->NI, nullptr, nullptr, ix->int_Ar, ix->int_Br, gamma2, s));
       HIPCHK(launch_int_path_prep(mean, var, dim, d_int_nodes, ix->int_rowid, n, ix->iso_c, ix->logdet_int,
                                   ix->par_int, ix->w_int, DP, ix->DPB2, ix->ld_i2, ix->int_Mb2, ix->int_rf2, gamma2, s));
+      // the same RowF by internal id, for the readers of the path-sum dots (PathB)
+      std::vector<RowF> rf2h((size_t)n), nrf((size_t)ix->NI, RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2});
+      HIPCHK(hipMemcpyAsync(rf2h.data(), ix->int_rf2, (size_t)n * sizeof(RowF), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (int64_t r = 0; r < n; ++r) nrf[rowid[r]] = rf2h[r];
+      if ((rc = ix->upload(&ix->int_nrf, nrf, s))) return rc;
     } else {
       // level-aligned operand layout: segments [levels 0 and 1], [level 2], [level 3], ...,
       // each padded to whole 256-row tiles
@@ -781,7 +794,14 @@ struct Chunk {
   // after the path-sum bounds (run_internal_bounds)
   int64_t ldP = 1;
   int pT = 0;
+  const float4* qi2 = nullptr;   // path-sum bounds: the queries' [x'^2, x'] norms (PathB)
 };
+
+// The path-sum dots of a chunk after run_internal_bounds (int_path), or none.
+PathB path_b(const cwq_index* ix, const Chunk& c) {
+  if (c.pT && ix->int_path && c.qi2 && ix->int_nrf) return PathB{c.P, c.ldP, c.qi2, ix->int_nrf};
+  return PathB{nullptr, 0, nullptr, nullptr};
+}
 
 // Query blocks of a launch; a multiple of 8 under the XCD-aware mapping (the
 // extra blocks exit at once).
@@ -909,11 +929,13 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   g.lb = c.P;
   g.lb_hi = c.S_int;
   g.ldlb = std::max(ix->NI, 1);
-  if (ix->int_path) {   // node-major lines of nq_pad queries (the chunk's [nq_pad][NI] space)
+  if (ix->int_path) {   // node-major lines of nq_pad queries (the chunk's [nq_pad][NI] space): dots
     g.pT = 1;
+    g.lb_hi = nullptr;
     g.ldlb = c.nq_pad;
     c.pT = 1;
     c.ldP = c.nq_pad;
+    c.qi2 = qinfo2;
   }
   g.Sroot = Sroot;
   g.root_w = ix->root_w;
@@ -1157,6 +1179,19 @@ void fg_groups(int n_qt, int& qg, int& rg) {
 int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                     hipStream_t s, bool allow_filter);
 
+// Wait for a one-query call's kernels by polling the stream: a blocking
+// hipStreamSynchronize issued ~0.3 ms before the work ends falls back to an interrupt
+// wait, whose wake-up is a large share of the per-call path's fixed cost.  Polls for at
+// most ~20 ms, then blocks.
+hipError_t sync_spin(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipStreamSynchronize(s);
+  }
+}
+
 // Queries whose certificate failed: exact scan, results scattered back in place.
 int rerun_exact(cwq_index* ix, const float* q, const std::vector<int64_t>& qi, int32_t k, int64_t* ids, float* scores,
                 hipStream_t s) {
@@ -1296,7 +1331,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.Mb = ix->iso_Mb;
   a.rf = ix->iso_rf;
   a.P = c.P ? c.P : ix->dummy;
-  a.Phi = ib ? c.S_int : nullptr;
+  a.pb = ib ? path_b(ix, c) : PathB{nullptr, 0, nullptr, nullptr};
+  a.Phi = ib && !a.pb.dot ? c.S_int : nullptr;
   a.ldP = c.ldP;
   a.pT = c.pT;
   a.eps_n = (float)fc.eps_n;
@@ -1354,7 +1390,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     HIPCHK(hipMemcpyAsync(ix->hflags, qcnt, (size_t)3 * nqc * 4, hipMemcpyDeviceToHost, s));
   }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[3], s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(sync_spin(s));
   std::vector<int64_t> redo;
   int64_t cand_sum = 0, exact_sum = 0;
   for (int i = 0; i < nqc; ++i) {
@@ -1434,8 +1470,9 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   int4* rec_dir = b.take<int4>((size_t)dir_cap);
   float2* pmm = (!cat && ix->n_multi_tiles) ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
   HIPCHK(launch_query_prep(qsrc, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
+  const PathB pb = (!cat && ib) ? path_b(ix, c) : PathB{nullptr, 0, nullptr, nullptr};
   if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
-    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s));
+    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s, &pb));
   FgArgs g;
   memset(&g, 0, sizeof(g));
   g.DPB = ix->DPB;
@@ -1452,7 +1489,8 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.pmm = pmm;
   g.ldq = nqf;
   g.P = cat ? (c.BF ? c.BF : ix->dummy) : (c.P ? c.P : ix->dummy);
-  g.Phi = (!cat && ib) ? c.S_int : nullptr;
+  g.pb = pb;
+  g.Phi = (!cat && ib && !pb.dot) ? c.S_int : nullptr;
   g.ldP = cat ? std::max(ix->NI, 1) : c.ldP;
   g.pT = cat ? 0 : c.pT;
   g.gamma = (float)fc.gamma;
@@ -1468,7 +1506,7 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   // large samples: lower bounds reduced to maxima over groups of 4 rows in the
   // kernel (fgemm_kernel<1>); small ones keep one value per row so that K groups exist
   g.lb = lb;
-  g.lbg = ix->n_samp >= 64 * K ? 4 : 1;
+  g.lbg = ix->n_samp >= 64 * K && !pb.dot ? 4 : 1;   // path-sum bounds: per-row values (fgemm_kernel<1>)
   g.ldlb = ix->ld_s / g.lbg;
   HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
   HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
@@ -1817,7 +1855,10 @@ extern "C" int cwq_prefix_bounds(cwq_index* ix, const float* q, int64_t nq, floa
   HIPCHK(hipMemsetAsync(c.P, 0xff, nall, s));   // NaN where the bound pass writes nothing
   HIPCHK(hipMemsetAsync(c.S_int, 0xff, nall, s));
   if ((rc = run_internal_bounds(ix, c, q, nqf, b, s))) return rc;
-  if (c.pT) {   // node-major [NI][nq_pad] -> [nq][NI]
+  const PathB pb = path_b(ix, c);
+  if (pb.dot) {   // path-sum dots, node-major [NI][nq_pad] -> bounds [nq][NI]
+    HIPCHK(launch_pathb_expand(pb, (int)nq, ix->NI, lo, hi, s));
+  } else if (c.pT) {   // node-major [NI][nq_pad] -> [nq][NI]
     HIPCHK(launch_transpose(c.P, ix->NI, nq, c.ldP, lo, ix->NI, s));
     HIPCHK(launch_transpose(c.S_int, ix->NI, nq, c.ldP, hi, ix->NI, s));
   } else {

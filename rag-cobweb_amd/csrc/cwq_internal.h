@@ -231,6 +231,52 @@ __host__ __device__ __forceinline__ size_t pidx(int64_t ld, int pT, int64_t q, i
   return pT ? (size_t)(p * ld + q) : (size_t)(q * ld + p);
 }
 
+// Path-sum row (int_path_prep_kernel): bounds lo <= P_fp32(n) <= hi of the exact pass's
+// path prefix from the MFMA dot a_hi.Bsum_hi and the exact root prefix proot.  RowF fields:
+// rn2 = K0, beta/delta = Bsum's split norms, hs = Zq, R0 = Zc, hl = cr; qinfo {qx, |a_hi|,
+// |a_lo|}.  2^-21 (|dot| + |K0| + |proot|) covers the dot's last rounding and the two fp32
+// additions; (1 + 2^-20) the evaluation of E and the final subtractions.
+__device__ __forceinline__ void path_bounds(float dot, float4 qi, const RowF& f, float proot, float& lo, float& hi) {
+  const float s = proot + (f.rn2 + dot);
+  const float ap = fabsf(proot);
+  const float E = (fmaf(qi.y, f.beta, qi.z * f.delta) + fmaf(f.hs, qi.x, f.R0) + f.hl * ap +
+                   0x1p-21f * (fabsf(dot) + fabsf(f.rn2) + ap)) *
+                  (1.f + 0x1p-20f);
+  lo = s - E;
+  hi = s + E;
+}
+
+// Bounded path prefixes of the leaf parents (int_path, run_internal_bounds): the internal
+// GEMM stores only its dot per (node, query), node-major [node][ld] -- node 0's line holds
+// the root's exact prefix -- and every reader turns a dot into [lo, hi] with path_bounds
+// (the per-query [x'^2, x'] norms qi2, the node's RowF nrf, indexed by internal id; par -2:
+// a node with no operand row, i.e. no isotropic leaf row below it).  Half the bytes of
+// storing lo and hi, bit-identical bounds.
+struct PathB {
+  const float* dot;     // [node][ld]; nullptr: not in use (the readers take P / Phi)
+  int64_t ld;
+  const float4* qi2;    // [nq]
+  const RowF* nrf;      // [NI]
+};
+// f: node p's RowF (b.nrf[p]), loaded by the caller (hoisted out of per-query loops)
+__device__ __forceinline__ void pathb_bounds_f(const PathB& b, int64_t q, int p, const RowF& f, float& lo,
+                                               float& hi) {
+  const float d = b.dot[(size_t)p * b.ld + q];
+  if (p == 0) {   // the root: its exact prefix
+    lo = hi = d;
+    return;
+  }
+  if (f.par < -1) {   // no operand row: unbounded (never read for a parent of a filter row)
+    lo = -__builtin_inff();
+    hi = __builtin_inff();
+    return;
+  }
+  path_bounds(d, b.qi2[q], f, b.dot[q], lo, hi);
+}
+__device__ __forceinline__ void pathb_bounds(const PathB& b, int64_t q, int p, float& lo, float& hi) {
+  pathb_bounds_f(b, q, p, p > 0 ? b.nrf[p] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -1}, lo, hi);
+}
+
 struct FgArgs {
   int DPB, nq, n_qt, n_rt, nrows, mode;   // mode 0: filter (records), 1: sample (dense lower bounds),
                                           // 2: internal-node lp' bounds (dense lo/hi)
@@ -254,6 +300,7 @@ struct FgArgs {
   const int* rowmap;                      // sample pass: operand row -> filter row (-1 pad)
   const float* P;                         // [nq][ldP] path prefixes of internal nodes (lower bounds when Phi)
   const float* Phi;                       // [nq][ldP] upper bounds of the prefixes (NULL: P is exact)
+  PathB pb;                               // path-sum bounds (pb.dot set: read instead of P / Phi)
   int64_t ldP;
   int pT;                                 // P / Phi (and mode-2 lb / lb_hi) node-major: [node][ldP] (pidx)
   float gamma, eps_n, slack;              // error-bound constants (cwq_mfma.hip header)
@@ -272,6 +319,77 @@ struct FgArgs {
   int* qover;                             // queries whose records were lost (re-run exactly)
   unsigned long long* stamp;              // FG_STAMP diagnostic builds only: s_memtime stamps
 };
+// ---------------------------------------------------------------------------
+// 64-lane lists (order: key desc, row asc), shared by the filter kernels
+// ---------------------------------------------------------------------------
+// whole-wave shift by one lane (lane i <- lane i-1; lane 0 keeps v): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ float rl_f2(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, float ck, int cr, int K) {
+  const bool prec = lk > ck || (lk == ck && lr < cr);
+  const int pos = __popcll(__ballot(prec));
+  if (pos < K) {
+    const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
+    const int sr = wave_shr1(lr);
+    if (lane == pos) {
+      lk = ck;
+      lr = cr;
+    } else if (lane > pos) {
+      lk = sk;
+      lr = sr;
+    }
+  }
+}
+
+__device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float key, int row, int K) {
+  const float tk = rl_f2(lk, K - 1);
+  const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+  const bool c = key != -__builtin_inff() && (key > tk || (key == tk && row < tr));
+  uint64_t mask = __ballot(c);
+  while (mask) {
+    const int j = __builtin_ctzll(mask);
+    mask &= mask - 1;
+    list64_insert(lk, lr, lane, rl_f2(key, j), __builtin_amdgcn_readlane(row, j), K);
+  }
+}
+
+// One wave: the top-Kp list (lk, lr: lane i holds the i-th) of the per-lane maxima of up to
+// 16 values of uq[0, nrows) -- the K-th largest of maxima over distinct rows is still a
+// lower bound of the K-th largest value.  Reads whole 1024-value steps (the buffer carries
+// >= 1024 floats of tail slack, masked here); g values per maximum, up to 16 while at
+// least 8*Kp maxima remain.  select_kernel (cwq_mfma.hip) and the per-call stream filter's
+// fused select (cwq_stream.hip) both run this, so their thresholds are identical.
+__device__ __forceinline__ void select_wave(const float* __restrict__ uq, int nrows, int Kp, int lane, float& lk,
+                                            int& lr) {
+  lk = -__builtin_inff();
+  lr = 0x7fffffff;
+  constexpr int STEP = 1024;
+  int g = 16;
+  while (g > 1 && nrows / g < 8 * Kp) g >>= 1;
+  for (int r0 = 0; r0 < nrows; r0 += STEP) {
+    float4 v4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v4[t] = *reinterpret_cast<const float4*>(uq + r0 + t * 256 + lane * 4);
+    float m = -__builtin_inff();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float vv[4] = {v4[t].x, v4[t].y, v4[t].z, v4[t].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int r = r0 + t * 256 + lane * 4 + c;
+        m = fmaxf(m, r < nrows ? vv[c] : -__builtin_inff());
+        if (((t * 4 + c + 1) & (g - 1)) == 0) {
+          list64_offer(lk, lr, lane, m, r, Kp);
+          m = -__builtin_inff();
+        }
+      }
+    }
+  }
+}
+
 // Small-batch stream filter (cwq_stream.hip): nq <= kStreamMaxQ queries per launch
 constexpr int kStreamMaxQ = 64;
 // small-batch prep (launch_sb_prep): pad + query prep + exact internal pass + counter clear
@@ -318,6 +436,7 @@ struct StreamArgs {
   const RowF* rf;              // [ld_f]
   const float* P;              // [nq][ldP] internal-node path prefixes (lower bounds when Phi)
   const float* Phi;            // [nq][ldP] upper bounds (NULL: P exact)
+  PathB pb;                    // path-sum bounds (pb.dot set: read instead of P / Phi)
   int64_t ldP;
   int pT;                      // node-major P / Phi (pidx)
   float eps_n, slack;
@@ -378,8 +497,9 @@ struct IntChain {
   const float* w_int;
   const float* logdet_int;
 };
+hipError_t launch_pathb_expand(const PathB& pb, int nq, int NI, float* lo, float* hi, hipStream_t s);
 hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int pT, int nq, const TileF* tf,
-                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s);
+                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s, const PathB* pb = nullptr);
 hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill, int64_t rec_cap, const int4* rec_dir,
                          int dir_cap, int capq, int* qcnt, int* qover, int* crow, float* cu, float* cl, hipStream_t s);
 // lkb/lrb [nq][64] and done [nq] carry each query's top-K candidate lower bounds between

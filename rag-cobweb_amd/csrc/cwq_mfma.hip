@@ -52,12 +52,6 @@ typedef __attribute__((address_space(1))) void glb_void;
 
 #define CWQ_INF __builtin_inff()
 
-// whole-wave shift by one lane (lane i <- lane i-1; lane 0 keeps v): DPP wave_shr:1
-__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
-__device__ __forceinline__ float rl_f2(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-
 // |v| rounded up a little (norms are used as bounds)
 __device__ __forceinline__ float up(double v) { return (float)(v * (1.0 + 0x1p-20)); }
 
@@ -562,21 +556,6 @@ __device__ __forceinline__ void int_bounds(float dot, float4 qi, const RowF& f, 
   lo = -0.5f * (f.hl + Shi) - m;
 }
 
-// Path-sum row (int_path_prep_kernel): bounds lo <= P_fp32(n) <= hi of the exact pass's
-// path prefix from the MFMA dot a_hi.Bsum_hi and the exact root prefix proot.  RowF fields:
-// rn2 = K0, beta/delta = Bsum's split norms, hs = Zq, R0 = Zc, hl = cr; qinfo {qx, |a_hi|,
-// |a_lo|}.  2^-21 (|dot| + |K0| + |proot|) covers the dot's last rounding and the two fp32
-// additions; (1 + 2^-20) the evaluation of E and the final subtractions.
-__device__ __forceinline__ void path_bounds(float dot, float4 qi, const RowF& f, float proot, float& lo, float& hi) {
-  const float s = proot + (f.rn2 + dot);
-  const float ap = fabsf(proot);
-  const float E = (fmaf(qi.y, f.beta, qi.z * f.delta) + fmaf(f.hs, qi.x, f.R0) + f.hl * ap +
-                   0x1p-21f * (fabsf(dot) + fabsf(f.rn2) + ap)) *
-                  (1.f + 0x1p-20f);
-  lo = s - E;
-  hi = s + E;
-}
-
 // XCD-local tile i -> (query tile, row tile).  order 0/2: query tiles fastest (the
 // XCD's query panels stay in L2 while row panels stream past, each read by every
 // query tile of the group at about the same time); order 1: row tiles fastest.
@@ -677,6 +656,16 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
   float* s_pi = reinterpret_cast<float*>(smem + OFF_PI);
   float* s_pl = reinterpret_cast<float*>(smem + OFF_PL);
   const float* Pu = a.Phi ? a.Phi : a.P;   // upper bounds of the parent prefixes
+  // bounds [lo, hi] of internal node p's prefix for query q: the path-sum dots (a.pb) or
+  // the P / Phi matrices (equal when exact)
+  auto pboth = [&](int64_t q, int p, float& lo, float& hi) {
+    if (a.pb.dot) {
+      pathb_bounds(a.pb, q, p, lo, hi);
+    } else {
+      lo = a.P[pidx(a.ldP, a.pT, q, p)];
+      hi = Pu[pidx(a.ldP, a.pT, q, p)];
+    }
+  };
   int4* s_rec = reinterpret_cast<int4*>(smem + OFF_REC);
   int* s_cnt = reinterpret_cast<int*>(smem + OFF_CNT);
   // per-lane source offsets of the two 16-row pieces a wave stages per operand
@@ -755,8 +744,12 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       qi = a.qinfo[qs];
       if (qs < a.nq && MODE == 0) Tq = a.T[(size_t)qs * a.ldT];
       if (uni && tf.par >= 0 && qs < a.nq) {
-        Pq = Pu[pidx(a.ldP, a.pT, qs, tf.par)];
-        Pql = a.P[pidx(a.ldP, a.pT, qs, tf.par)];
+        if (a.pb.dot) {
+          pathb_bounds(a.pb, qs, tf.par, Pql, Pq);
+        } else {
+          Pq = Pu[pidx(a.ldP, a.pT, qs, tf.par)];
+          Pql = a.P[pidx(a.ldP, a.pT, qs, tf.par)];
+        }
       }
     }
     float R0[4];
@@ -898,16 +891,16 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     bool anyb[4][2];
     if (a.dbg & 2) goto flush;
     if (MODE == 2 && a.pT) {
-      // path-sum bounds, node-major [node][ldlb]: lane (r16, c16) of MFMA block (ib, jb)
-      // holds queries 4 c16 .. 4 c16 + 3 of one row -- 16 contiguous bytes of that node's
-      // line -- so the bounds go straight from the accumulators to float4 stores (a store
-      // instruction covers 16 rows x 64 B), no LDS transpose
-      RowF f[4];
-      int rid[4];
+      // path sums, node-major [node][ldlb]: the dot of each (node, query) -- readers turn
+      // it into bounds with path_bounds (PathB) -- and the root's exact prefix in its line.
+      // Lane (r16, c16) of MFMA block (ib, jb) holds queries 4 c16 .. 4 c16 + 3 of one row
+      // -- 16 contiguous bytes of that node's line -- so the values go straight from the
+      // accumulators to float4 stores (a store instruction covers 16 rows x 64 B)
+      int par[4], rid[4];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         const int r = r0 + wr * 64 + jb * 16 + r16;
-        f[jb] = r < a.nrows ? a.rf[r] : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+        par[jb] = r < a.nrows ? a.rf[r].par : -2;
         rid[jb] = r < a.nrows ? a.row_id[r] : -1;
       }
 #pragma unroll
@@ -915,25 +908,13 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
         const int ql = wq * 128 + ib * 16 + 4 * c16;
         const int q = q0 + ql;
         if (q >= a.ldlb) continue;   // query padding beyond the lines (ldlb: a multiple of 4)
-        float4 qi[4];
-        float pr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          qi[j] = s_qi[ql + j];
-          pr[j] = s_pl[ql + j];
-        }
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
-          if (f[jb].par < -1 || rid[jb] < 0) continue;
-          float lo[4], hi[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (f[jb].par < 0) lo[j] = hi[j] = pr[j];   // the root: its exact prefix
-            else path_bounds(acc[ib][jb][j], qi[j], f[jb], pr[j], lo[j], hi[j]);
-          }
+          if (par[jb] < -1 || rid[jb] < 0) continue;
           const size_t o = (size_t)rid[jb] * a.ldlb + q;
-          *reinterpret_cast<float4*>(a.lb + o) = make_float4(lo[0], lo[1], lo[2], lo[3]);
-          *reinterpret_cast<float4*>(a.lb_hi + o) = make_float4(hi[0], hi[1], hi[2], hi[3]);
+          const float4 v = par[jb] < 0 ? *reinterpret_cast<const float4*>(s_pl + ql)   // the root: its exact prefix
+                                       : make_float4(acc[ib][jb][0], acc[ib][jb][1], acc[ib][jb][2], acc[ib][jb][3]);
+          *reinterpret_cast<float4*>(a.lb + o) = v;
         }
       }
       goto flush;
@@ -978,20 +959,24 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       }
       goto flush;
     }
-    if (MODE == 1 && a.lbg == 4) {
+    if (MODE == 1 && a.lbg == 4 && !a.pb.dot) {   // (path-sum bounds: one value per row, below)
       // sample pass: lower bounds reduced to row groups of 4 -- rows r16 + 16 jb of this
       // wave's 64-row block, all in one lane -- before the store.  The K-th largest group
       // maximum is still <= the K-th largest row lower bound (distinct groups are
-      // distinct rows), and the bounds array and its select shrink 4x.
-      RowF f[4];
+      // distinct rows), and the bounds array and its select shrink 4x.  Per row only the
+      // approximate-key terms stay in registers; the chosen row's RowF is re-read (an L1
+      // hit).  The path-sum bounds' reads (PathB) take the per-row form below: inlined 32
+      // times here they spilled registers.
+      int rrow[4];
       float pa[4], pb[4];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         const int r = r0 + wr * 64 + jb * 16 + r16;
         const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
-        f[jb] = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
-        pa[jb] = fmaf(f[jb].hs, f[jb].rn2, f[jb].hl);   // approximate key = pa + pb * dot (no pi, no error)
-        pb[jb] = -2.f * f[jb].hs;
+        const RowF f = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
+        rrow[jb] = f.par >= -1 ? rr : -1;
+        pa[jb] = fmaf(f.hs, f.rn2, f.hl);   // approximate key = pa + pb * dot (no pi, no error)
+        pb[jb] = -2.f * f.hs;
       }
       const int g = (r0 + wr * 64) / 4 + r16;
 #pragma unroll
@@ -1007,23 +992,25 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
 #pragma unroll
           for (int jb = 0; jb < 4; ++jb) {
             const float pk = fmaf(pb[jb], acc[ib][jb][j], pa[jb]);
-            if (f[jb].par >= -1 && (best < 0 || pk > bk)) {
+            if (rrow[jb] >= 0 && (best < 0 || pk > bk)) {
               bk = pk;
               best = jb;
             }
           }
           float m = -CWQ_INF;
           if (best >= 0) {
-            RowF fb = f[0];
+            int rb = rrow[0];
             float d0 = acc[ib][0][j];
 #pragma unroll
             for (int jb = 1; jb < 4; ++jb)
               if (best == jb) {
-                fb = f[jb];
+                rb = rrow[jb];
                 d0 = acc[ib][jb][j];
               }
+            const RowF fb = a.rf[rb];
             const float4 qi = s_qi[ql];
-            const float pi = (fb.par >= 0 && q < a.nq) ? a.P[pidx(a.ldP, a.pT, q, fb.par)] * fb.invL : 0.f;
+            float pi = 0.f;
+            if (fb.par >= 0 && q < a.nq) pi = a.P[pidx(a.ldP, a.pT, q, fb.par)] * fb.invL;   // exact or lower bounds
             float u;
             fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, fb, pi, a.eps_n, a.slack, u, m);
             if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, a.P[pidx(a.ldP, a.pT, q, fb.par)]);
@@ -1058,6 +1045,13 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       const int rr = a.rowmap ? a.rowmap[r] : (r < a.nrows ? r : -1);
       const RowF f = rr >= 0 ? a.rf[rr] : RowF{-CWQ_INF, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -2};
       const bool usable = f.par >= -1;
+      // the row's parent's path-sum RowF, once per row (not per survivor)
+      const RowF fpar = (MODE == 0 && a.pb.dot && f.par > 0) ? a.pb.nrf[f.par]
+                                                           : RowF{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, -1};
+      auto pboth_row = [&](int64_t q, float& lo, float& hi) {
+        if (a.pb.dot) pathb_bounds_f(a.pb, q, f.par, fpar, lo, hi);
+        else pboth(q, f.par, lo, hi);
+      };
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         if (!anyb[jb][hf]) continue;
@@ -1086,7 +1080,12 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               float lo = -CWQ_INF;
               if (usable) {
                 const float4 qi = s_qi[ql];
-                const float pi = (f.par >= 0 && q < a.nq) ? a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
+                float pi = 0.f;
+                if (f.par >= 0 && q < a.nq) {
+                  float plo_, phi_;
+                  pboth(q, f.par, plo_, phi_);
+                  pi = plo_ * f.invL;
+                }
                 float u;
                 fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f, pi, a.eps_n, a.slack, u, lo);
                 if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, a.P[pidx(a.ldP, a.pT, q, f.par)]);
@@ -1100,8 +1099,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 d = d0 - init;
                 ex = a.gamma * fabsf(init) + 0x1p-23f * (fabsf(d0) + fabsf(init));
                 if (!ALLUNI && multi) {
-                  pi = Pu[pidx(a.ldP, a.pT, q, f.par)] * f.invL;
-                  pl = a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL;
+                  float plo_, phi_;
+                  pboth_row(q, plo_, phi_);
+                  pi = phi_ * f.invL;
+                  pl = plo_ * f.invL;
                 } else {
                   pi = s_pi[ql];
                   pl = s_pl[ql];
@@ -1109,8 +1110,10 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               } else {
                 d = d0;
                 ex = 0x1p-23f * fabsf(d0);
-                pi = f.par >= 0 ? Pu[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
-                pl = f.par >= 0 ? a.P[pidx(a.ldP, a.pT, q, f.par)] * f.invL : 0.f;
+                float plo_ = 0.f, phi_ = 0.f;
+                if (f.par >= 0) pboth_row(q, plo_, phi_);
+                pi = phi_ * f.invL;
+                pl = plo_ * f.invL;
               }
               float u, lo;
               fg_bounds2(d, ex, qi, f, pi, pl, a.eps_n, a.slack, u, lo);
@@ -1263,37 +1266,6 @@ hipError_t launch_bucket(const int4* rec, const int* gctr, const int* chunk_fill
 }
 
 // ---------------------------------------------------------------------------
-// list helpers (64-lane lists, order: key desc, row asc)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, float ck, int cr, int K) {
-  const bool prec = lk > ck || (lk == ck && lr < cr);
-  const int pos = __popcll(__ballot(prec));
-  if (pos < K) {
-    const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
-    const int sr = wave_shr1(lr);
-    if (lane == pos) {
-      lk = ck;
-      lr = cr;
-    } else if (lane > pos) {
-      lk = sk;
-      lr = sr;
-    }
-  }
-}
-
-__device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float key, int row, int K) {
-  const float tk = rl_f2(lk, K - 1);
-  const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-  const bool c = key != -CWQ_INF && (key > tk || (key == tk && row < tr));
-  uint64_t mask = __ballot(c);
-  while (mask) {
-    const int j = __builtin_ctzll(mask);
-    mask &= mask - 1;
-    list64_insert(lk, lr, lane, rl_f2(key, j), __builtin_amdgcn_readlane(row, j), K);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // select: top-Kp values per query of a dense [nq][ld] array (the sample bounds; the
 // values are first reduced to maxima of up to 16 per lane)
 // ---------------------------------------------------------------------------
@@ -1302,35 +1274,9 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ u
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (q >= nq) return;
-  const float* uq = u + (size_t)q * ldu;
-  float lk = -CWQ_INF;
-  int lr = 0x7fffffff;
-  // one wave per query over whole 1024-row steps (16 values per lane per step; the buffer
-  // carries >= 1024 floats of tail slack, masked here).  The K-th largest of maxima over
-  // g values of a lane (distinct rows, so still a lower bound of the K-th key): g up to
-  // 16 while at least 8*Kp maxima remain
-  constexpr int STEP = 1024;
-  int g = 16;
-  while (g > 1 && nrows / g < 8 * Kp) g >>= 1;
-  for (int r0 = 0; r0 < nrows; r0 += STEP) {
-    float4 v4[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v4[t] = *reinterpret_cast<const float4*>(uq + r0 + t * 256 + lane * 4);
-    float m = -CWQ_INF;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float vv[4] = {v4[t].x, v4[t].y, v4[t].z, v4[t].w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int r = r0 + t * 256 + lane * 4 + c;
-        m = fmaxf(m, r < nrows ? vv[c] : -CWQ_INF);
-        if (((t * 4 + c + 1) & (g - 1)) == 0) {
-          list64_offer(lk, lr, lane, m, r, Kp);
-          m = -CWQ_INF;
-        }
-      }
-    }
-  }
+  float lk;
+  int lr;
+  select_wave(u + (size_t)q * ldu, nrows, Kp, lane, lk, lr);
   cu[(size_t)q * 64 + lane] = lk;
   crow[(size_t)q * 64 + lane] = lr;
 }
@@ -1429,9 +1375,73 @@ __global__ __launch_bounds__(256) void tile_prange_t_kernel(const float* __restr
   pmm[(size_t)t * ldq + q] = make_float2(fminf(mn0, mn1), fmaxf(mx0, mx1));
 }
 
+// Path-sum dots (PathB): thread = query, one tile per blockIdx.y; each parent's dot line
+// read coalesced over the block's queries, turned into [lo, hi] by path_bounds with the
+// parent's RowF (uniform over the block: scalar loads); parents without an operand row
+// (no isotropic leaf row below them) are not parents of the tile's rows and are skipped.
+__global__ __launch_bounds__(256) void tile_prange_pb_kernel(const PathB pb, int nq, const TileF* __restrict__ tf,
+                                                             int t0, float2* __restrict__ pmm, int64_t ldq) {
+  const int t = t0 + blockIdx.y;
+  const TileF T = tf[t];
+  if (T.uniform != 2) return;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const float4 qi = pb.qi2[q];
+  const float proot = pb.dot[q];
+  float mn = CWQ_INF, mx = -CWQ_INF;
+  auto one = [&](int p) {
+    const RowF f = pb.nrf[p];
+    const float d = pb.dot[(size_t)p * pb.ld + q];
+    float lo, hi;
+    if (p == 0) lo = hi = d;
+    else path_bounds(d, qi, f, proot, lo, hi);
+    if (f.par >= -1 || p == 0) {
+      mn = fminf(mn, fminf(lo * T.invL, hi * T.invL));
+      mx = fmaxf(mx, fmaxf(lo * T.invL, hi * T.invL));
+    }
+  };
+  // four lines in flight per step (the loads of a step are independent)
+  int p = T.par;
+  for (; p + 3 <= T.par_hi; p += 4) {
+    one(p);
+    one(p + 1);
+    one(p + 2);
+    one(p + 3);
+  }
+  for (; p <= T.par_hi; ++p) one(p);
+  pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
+}
+
+// Diagnostic (cwq_prefix_bounds): the path-sum dots as [lo, hi] matrices [nq][NI].
+__global__ void pathb_expand_kernel(const PathB pb, int nq, int NI, float* lo, float* hi) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nq * NI) return;
+  const int q = (int)(i / NI), p = (int)(i % NI);
+  float l, h;
+  pathb_bounds(pb, q, p, l, h);
+  lo[i] = l;
+  hi[i] = h;
+}
+
+hipError_t launch_pathb_expand(const PathB& pb, int nq, int NI, float* lo, float* hi, hipStream_t s) {
+  const int64_t n = (int64_t)nq * NI;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pathb_expand_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pb, nq, NI, lo, hi);
+  return hipGetLastError();
+}
+
 hipError_t launch_tile_prange(const float* P, const float* Phi, int64_t ldP, int pT, int nq, const TileF* tf,
-                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s) {
+                              int n_rt, float2* pmm, int64_t ldq, hipStream_t s, const PathB* pb) {
   static_assert(kPrQ * kPrTiles <= 256, "one thread per (query, tile)");
+  if (pb && pb->dot) {
+    if (nq <= 0 || n_rt <= 0) return hipSuccess;
+    for (int t0 = 0; t0 < n_rt; t0 += 65535) {   // grid y limit
+      hipLaunchKernelGGL(tile_prange_pb_kernel, dim3((unsigned)((nq + 255) / 256), (unsigned)std::min(65535, n_rt - t0)),
+                         dim3(256), 0, s, *pb, nq, tf, t0, pmm, ldq);
+      if (hipError_t e = hipGetLastError()) return e;
+    }
+    return hipSuccess;
+  }
   if (pT) {
     if (nq <= 0 || n_rt <= 0) return hipSuccess;
     for (int t0 = 0; t0 < n_rt; t0 += 65535) {   // grid y limit
@@ -1590,6 +1600,57 @@ __device__ __forceinline__ float exact_prefix(const float* __restrict__ X, const
   return P;
 }
 
+// Exact path prefixes of the candidates' parents for one query (one wave; every lane
+// calls it, `need` marks the lanes with a parent p > 0), with exact_prefix's arithmetic
+// node for node but each ancestor computed ONCE per query: the chains are walked top-down
+// one depth per step, and at each step the lanes that need the same node (the top
+// levels are shared by every candidate of a query) find it in a per-wave LDS table --
+// the first lane to claim a node computes its exact S and P = fmaf(w, lp', P(parent)),
+// the others read P after the wave barrier (a node's parent prefix is the same for
+// every lane that reaches it).  A node that finds no free slot is computed by its lane.
+constexpr int kChainSlots = 256;
+__device__ __forceinline__ float chain_prefix_cached(const float* __restrict__ X, const IntChain& ch, int DP, int q,
+                                                     bool need, int p, float proot, int* ck, float* cv) {
+  int n = 0;
+  if (need)
+    for (int j = p; j > 0 && n < kMaxChain; j = ch.par_int[j]) ++n;
+  int nmax = n;
+  for (int off = 32; off > 0; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
+  float P = proot;
+  for (int t = 0; t < nmax; ++t) {   // depth t + 1 for every lane
+    const bool on = need && t < n;
+    int a = -1, slot = -1;
+    bool owner = false;
+    if (on) {
+      a = p;
+      for (int u = 0; u < n - 1 - t; ++u) a = ch.par_int[a];
+      int h = a & (kChainSlots - 1);
+      for (int probe = 0; probe < 8; ++probe) {
+        const int old = atomicCAS(ck + h, -1, a);
+        if (old == -1 || old == a) {
+          slot = h;
+          owner = old == -1;
+          break;
+        }
+        h = (h + 1) & (kChainSlots - 1);
+      }
+    }
+    float Pa = 0.f;
+    if (on && (owner || slot < 0)) {
+      const float S = exact_aniso_S(X, ch.Ar, ch.Br, DP, q, a);
+      const float lp = -0.5f * (ch.logdet_int[a] + S);
+      Pa = fmaf(ch.w_int[a], lp, P);
+      if (owner) cv[slot] = Pa;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (on && !owner && slot >= 0) Pa = cv[slot];
+    if (on) P = Pa;
+  }
+  return P;
+}
+
 __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X, const float* __restrict__ Mf, int DP,
                                                     int nq, int K, int capq, const int* __restrict__ qcnt,
                                                     const int* __restrict__ qover, const int* __restrict__ crow,
@@ -1603,9 +1664,17 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
                                                     const IntChain chain, int use_chain, int cat,
                                                     float dconst) {
   __shared__ int s_pend[kWavesPerWG][128];
+  __shared__ int s_ck[kWavesPerWG][kChainSlots];     // exact-prefix table (chain_prefix_cached)
+  __shared__ float s_cv[kWavesPerWG][kChainSlots];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (q >= nq) return;
+  if (use_chain) {
+    for (int i = lane; i < kChainSlots; i += 64) s_ck[threadIdx.x >> 6][i] = -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   const int n = qcnt[q];
   const float Tq = T[(size_t)q * ldT];
   bool ok = qover[q] == 0 && n >= K && n <= capq && Tq > -CWQ_INF;
@@ -1645,14 +1714,17 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
       const int rest = npend > 64 ? pend[64 + lane] : 0;   // lane < npend - 64 <= 63
       float key = -CWQ_INF, lp = 0.f;
       int rid = 0x7fffffff;
+      const int rr = act ? crow[base + jj] : 0;
+      const int p = act ? par[rr] : -1;
+      // with the chain only the root's P[q][0] is read (ldP 1: node-major); every lane of
+      // the wave takes part in the cached chain walk
+      const float pc = use_chain ? chain_prefix_cached(X, chain, DP, q, act && p > 0, p, P[(size_t)q * ldP],
+                                                       s_ck[threadIdx.x >> 6], s_cv[threadIdx.x >> 6])
+                                 : 0.f;
       if (act) {
-        const int rr = crow[base + jj];
         const RowMeta md = meta[rr];
-        const int p = par[rr];
-        // exact (cat: BF); with the chain only the root's P[q][0] is read (ldP 1: node-major)
-        float pp = p < 0 ? (cat ? CWQ_INF : 0.f)
-                         : (use_chain && p > 0 ? exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP])
-                                               : P[(size_t)q * ldP + p]);
+        // exact (cat: BF)
+        float pp = p < 0 ? (cat ? CWQ_INF : 0.f) : (use_chain && p > 0 ? pc : P[(size_t)q * ldP + p]);
         key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp, cat, dconst);
         rid = seg_base + rr;
         ++nx;

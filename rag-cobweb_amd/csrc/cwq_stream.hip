@@ -202,9 +202,15 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         cpar = rf[j].par;
 #pragma unroll
         for (int qb = 0; qb < MQB; ++qb) {
-          const size_t o = pidx(a.ldP, a.pT, qb * 16 + r16, cpar);
-          cP[qb] = (qok[qb] && cpar >= 0) ? a.P[o] : 0.f;
-          cPh[qb] = (qok[qb] && cpar >= 0) ? Pu[o] : 0.f;
+          cP[qb] = cPh[qb] = 0.f;
+          if (!qok[qb] || cpar < 0) continue;
+          if (a.pb.dot) {
+            pathb_bounds(a.pb, qb * 16 + r16, cpar, cP[qb], cPh[qb]);
+          } else {
+            const size_t o = pidx(a.ldP, a.pT, qb * 16 + r16, cpar);
+            cP[qb] = a.P[o];
+            cPh[qb] = Pu[o];
+          }
         }
       }
 #pragma unroll

@@ -31,6 +31,17 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _stream_raw(index):
+    """torch's current HIP stream on device `index` as an int (the per-call path: no
+    Stream object, no device switch -- libcwq sets its device itself)."""
+    if _raw_stream is not None:
+        return _raw_stream(index)
+    return torch.cuda.current_stream(index).cuda_stream
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
@@ -187,14 +198,19 @@ class CobwebIndex:
         return q.to(self.device).contiguous()
 
     def score_topk(self, q, k):
-        """Top-k sentence ids/scores per query ("Cobweb Fast", A6)."""
-        q = self._queries(q)
+        """Top-k sentence ids/scores per query ("Cobweb Fast", A6).  One call per query is
+        the reference harness's mode (benchmark_utils.py:801-805), so a float32 [nq, dim]
+        tensor already on the index device goes straight through: no conversion, no device
+        switch (the library selects its device itself), the raw current stream."""
+        if not (type(q) is torch.Tensor and q.dtype == torch.float32 and q.device == self.device and q.dim() == 2
+                and q.shape[1] == self.dim and q.is_contiguous()):
+            q = self._queries(q)
         nq = q.shape[0]
+        k = int(k)
         ids = torch.empty((nq, k), dtype=torch.int64, device=self.device)
         scores = torch.empty((nq, k), dtype=torch.float32, device=self.device)
-        with torch.cuda.device(self.device):
-            check(self._L.cwq_score_topk(self._h, _ptr(q), nq, int(k), _ptr(ids), _ptr(scores),
-                                       _stream(self.device)))
+        check(self._L.cwq_score_topk(self._h, q.data_ptr(), nq, k, ids.data_ptr(), scores.data_ptr(),
+                                     _stream_raw(self.device.index)))
         return ids, scores
 
     def rank_scores(self, q):
