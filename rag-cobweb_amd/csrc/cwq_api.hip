@@ -153,6 +153,7 @@ struct cwq_index {
   hipEvent_t ws_ev = nullptr;
   bool ws_ev_live = false;
   hipStream_t ws_ev_stream = nullptr;   // the stream ws_ev was last recorded on
+  bool ws_idle = false;   // set by a call that ends with its stream synchronized: no event needed
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
   size_t hflags_n = 0;
   // fallback re-runs (cwq_score_topk / cwq_categorize): gathered queries, their results
@@ -214,6 +215,11 @@ struct cwq_index {
   // end of a query call: the workspace is busy until the work queued on s so far is done
   int ws_end(hipStream_t s) {
     if (!ws_ev) return fail(CWQ_ERR_HIP, "workspace event missing");
+    if (ws_idle) {   // every kernel of the call has finished: the workspace is free now
+      ws_idle = false;
+      ws_ev_live = false;
+      return CWQ_OK;
+    }
     if (hipEventRecord(ws_ev, s) != hipSuccess) {
       // the event no longer marks this call's work: wait for it here instead
       ws_ev_live = false;
@@ -1411,6 +1417,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     ix->t_ms[4] += 1;   // one filter launch
   }
   if (!redo.empty() && (rc = rerun_exact(ix, q, redo, k, ids, scores, s))) return rc;
+  ix->ws_idle = true;   // synchronized above (rerun_exact synchronizes too): no end event
   ix->stats[0] = nq;
   ix->stats[1] = (int64_t)redo.size();
   ix->stats[2] = 2;   // the stream filter
