@@ -214,7 +214,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-call", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r02_fgemm.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03_fgemm.json"))
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="rehearsal only: gloo lets several ranks share one GPU (RCCL refuses that)")
     args = ap.parse_args()
