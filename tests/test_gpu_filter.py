@@ -426,3 +426,96 @@ def test_prefix_bounds_enclose_exact(gpu, tree, path, monkeypatch):
     print(f"{tree} path={path}: rel width median {float(rel.median()):.2e} max {float(rel.max()):.2e}")
     assert float(rel.median()) < 5e-2
     ix.close()
+
+
+def ragged_tree(pkg, X, G1, S, seed=0):
+    """root -> G1 clusters; even clusters hold their leaves directly (depth 2), odd ones
+    through S sub-clusters (depth 3).  In BFS order the depth-2 leaf parents (the even
+    clusters) alternate with internal nodes that have no leaf directly below them, so a
+    leaf tile's parent range [par, par_hi] spans internal ids with no path-sum operand row.
+    Node statistics by the GPU Welford builder."""
+    N, D = X.shape
+    g = torch.Generator(device=X.device)
+    g.manual_seed(seed)
+    l1 = torch.randint(0, G1, (N,), generator=g, device=X.device).cpu().numpy()
+    sub = torch.randint(0, S, (N,), generator=g, device=X.device).cpu().numpy()
+    u1 = np.unique(l1)
+    rows_of = {c: np.nonzero(l1 == c)[0] for c in u1}
+    depth2, depth3, l2groups = [], [], []   # depth-2 entries: ("leaf", row) | ("int", group rows)
+    for c in u1:
+        if c % 2 == 0:
+            depth2 += [("leaf", int(r)) for r in rows_of[c]]
+        else:
+            for sg in np.unique(sub[rows_of[c]]):
+                gr = rows_of[c][sub[rows_of[c]] == sg]
+                depth2.append(("int", len(l2groups)))
+                l2groups.append(gr)
+    for gr in l2groups:
+        depth3 += [int(r) for r in gr]
+
+    def stats(groups):
+        order = torch.from_numpy(np.concatenate(groups)).to(X.device)
+        ptr = torch.from_numpy(np.cumsum([0] + [len(x) for x in groups])).to(X.device)
+        n, m, q = pkg.index.welford_groups(X, order, ptr)
+        return m, q / n[:, None] + float(pkg.PRIOR_VAR)
+
+    m0, v0 = stats([np.arange(N)])
+    m1, v1 = stats([rows_of[c] for c in u1])
+    m2, v2 = stats(l2groups)
+    G1n = len(u1)
+    parent, nos = [-1] + [0] * G1n, np.empty(N, dtype=np.int64)
+    mean_parts, var_parts = [m0, m1], [v0, v1]
+    int_node = {}
+    pos = 1 + G1n
+    leaf_rows = []
+    ci = {c: 1 + i for i, c in enumerate(u1)}
+    for kind, v in depth2:
+        if kind == "leaf":
+            parent.append(ci[l1[v]])
+            nos[v] = pos
+            leaf_rows.append(v)
+        else:
+            parent.append(ci[l1[l2groups[v][0]]])
+            int_node[v] = pos
+        pos += 1
+    d2_leaf = torch.from_numpy(np.asarray(leaf_rows, dtype=np.int64)).to(X.device)
+    for gi, gr in enumerate(l2groups):
+        for r in gr:
+            parent.append(int_node[gi])
+            nos[r] = pos
+            pos += 1
+    # depth-2 node means/vars in BFS order: leaves (X rows, prior var) and level-2 groups
+    d2m, d2v = [], []
+    for kind, v in depth2:
+        if kind == "leaf":
+            d2m.append(X[v:v + 1])
+            d2v.append(torch.full((1, D), float(pkg.PRIOR_VAR), device=X.device))
+        else:
+            d2m.append(m2[v:v + 1])
+            d2v.append(v2[v:v + 1])
+    d3 = torch.from_numpy(np.asarray(depth3, dtype=np.int64)).to(X.device)
+    mean = torch.cat(mean_parts + d2m + [X[d3]])
+    var = torch.cat(var_parts + d2v + [torch.full((len(depth3), D), float(pkg.PRIOR_VAR), device=X.device)])
+    assert mean.shape[0] == len(parent) and int(d2_leaf.numel()) + len(depth3) == N
+    return mean, var, np.asarray(parent, dtype=np.int64), nos
+
+
+def test_ragged_tree_parent_gaps(gpu):
+    """Leaves at depths 2 and 3 (ragged_tree): multi-parent leaf tiles whose parent ranges
+    include internal nodes with no leaf below them (no path-sum operand row, PathB
+    par -2).  The filter's ids and scores equal the exact scan's, batch and per-call; the
+    path-sum bounds enclose the exact prefixes of every leaf parent."""
+    X = gpu.synth.synthetic_corpus(40000, 96, seed=81)
+    mean, var, parent, nos = ragged_tree(gpu, X, 120, 3)
+    ix = gpu.index.CobwebIndex(mean, var, parent, nos, device="cuda:0")
+    assert ix.info["max_depth"] == 3
+    Q, _ = gpu.synth.synthetic_queries(X, 300, seed=82)
+    for q in (Q, Q[:5]):
+        for k in (1, 10):
+            ids0, s0, ids1, s1, st = both(ix, q, k)
+            assert st["filter_used"], st
+            assert torch.equal(ids0, ids1) and torch.equal(s0, s1), (q.shape[0], k, st)
+    lo, hi, ex = ix.prefix_bounds(Q[:100])
+    fin = torch.isfinite(lo) & torch.isfinite(hi)
+    assert bool(((lo <= ex) | ~fin).all()) and bool(((ex <= hi) | ~fin).all())
+    ix.close()
