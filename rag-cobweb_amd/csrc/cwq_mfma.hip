@@ -1786,6 +1786,129 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
 // count is known; entries past it are never used), and the survivors' row terms fly with
 // their partials' row loads.  fx (optional): the fused expansion + host flags (FwExpand).
 constexpr int kFwThreads = 512;
+// Exact path prefixes of a round's survivor parents with the whole workgroup
+// (final_wide_kernel, hierarchical trees): the distinct ancestors of every parent go into an
+// LDS table (wave 0; a lane stops at the first node another lane has entered, whose
+// ancestors that lane enters), then every (node, 16-dim slice) partial is computed in
+// parallel, one thread per node adds them in slice order (exact_aniso_S's arithmetic), and
+// the prefixes P = fmaf(w, lp', P(parent)) are stepped level by level from the root's exact
+// prefix -- exact_prefix's values, without a depth x D serial chain per lane (226 of a
+// 905 us one-query call on a depth-9 tree).  Returns false when the table overflows (the
+// caller then takes the per-lane chain).
+constexpr int kFwChainNodes = 1024, kFwChainHash = 2048, kFwChainPart = 8192;
+struct FwChainLds {
+  int hk[kFwChainHash];      // node id (-1: empty)
+  int hv[kFwChainHash];      // its entry
+  int node[kFwChainNodes];
+  int depth[kFwChainNodes];
+  float val[kFwChainNodes];  // lp', then P
+  float part[kFwChainPart];  // [entries of a chunk][NV16] slice partials
+  float pp[64];              // the result per wave-0 lane
+  int m, maxd, over;
+};
+__device__ __forceinline__ int fw_hash(int a) { return (int)(((unsigned)a * 2654435761u) >> 21) & (kFwChainHash - 1); }
+__device__ __forceinline__ int fw_find(const FwChainLds& L, int a) {
+  int h = fw_hash(a);
+  for (int t = 0; t < kFwChainHash; ++t) {
+    const int k = L.hk[h];
+    if (k == a) return L.hv[h];
+    if (k == -1) return -1;
+    h = (h + 1) & (kFwChainHash - 1);
+  }
+  return -1;
+}
+// every thread of the workgroup calls it; wave 0 lanes with `need` have parent p > 0
+__device__ bool fw_chain_prefixes(FwChainLds& L, const f32x16* __restrict__ xg, const IntChain& ch, int DP, bool need,
+                                  int p, float proot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < kFwChainHash; i += kFwThreads) L.hk[i] = -1;
+  if (tid == 0) {
+    L.m = 0;
+    L.maxd = 0;
+    L.over = 0;
+  }
+  __syncthreads();
+  if (wave == 0 && need) {
+    int d = 0;
+    for (int j = p; j > 0 && d < kMaxChain; j = ch.par_int[j]) ++d;
+    atomicMax(&L.maxd, d);
+    for (int a = p; a > 0 && d > 0; a = ch.par_int[a], --d) {
+      int h = fw_hash(a), t = 0;
+      bool stop = false;
+      for (; t < kFwChainHash; ++t) {
+        const int old = atomicCAS(&L.hk[h], -1, a);
+        if (old == -1) {   // entered here: its entry, then on to its parent
+          const int e = atomicAdd(&L.m, 1);
+          if (e < kFwChainNodes) {
+            L.node[e] = a;
+            L.depth[e] = d;
+          } else {
+            L.over = 1;
+          }
+          L.hv[h] = e;
+          break;
+        }
+        if (old == a) {   // entered by another lane, which enters its ancestors
+          stop = true;
+          break;
+        }
+        h = (h + 1) & (kFwChainHash - 1);
+      }
+      if (t == kFwChainHash) L.over = 1;
+      if (stop) break;
+    }
+  }
+  __syncthreads();
+  if (L.over) return false;
+  const int m = L.m, NV16 = DP / 16;
+  const int chunk = kFwChainPart / NV16;
+  for (int c0 = 0; c0 < m; c0 += chunk) {
+    const int nc = min(chunk, m - c0);
+    for (int it = tid; it < nc * NV16; it += kFwThreads) {
+      const int e = it / NV16, v = it - e * NV16;
+      const int a = L.node[c0 + e];
+      const float* __restrict__ ar = ch.Ar + (size_t)a * DP + v * 16;
+      const float* __restrict__ br = ch.Br + (size_t)a * DP + v * 16;
+      float4 a4[4], b4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
+        b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
+      }
+      const f32x16 xa = xg[(size_t)v * kXQ];
+      float part;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float4 ta = a4[j >> 2], tb = b4[j >> 2];
+        const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
+        const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
+        const float t = fmaf(xa[j], aj, -bj);
+        part = (j == 0) ? t * t : fmaf(t, t, part);
+      }
+      L.part[it] = part;
+    }
+    __syncthreads();
+    for (int e = tid; e < nc; e += kFwThreads) {
+      float acc = 0.f;
+      for (int v = 0; v < NV16; ++v) acc += L.part[e * NV16 + v];
+      L.val[c0 + e] = -0.5f * (ch.logdet_int[L.node[c0 + e]] + acc);
+    }
+    __syncthreads();
+  }
+  for (int d = 1; d <= L.maxd; ++d) {   // prefixes, root side first
+    for (int e = tid; e < m; e += kFwThreads) {
+      if (L.depth[e] != d) continue;
+      const int a = L.node[e], pa = ch.par_int[a];
+      const float Pp = pa > 0 ? L.val[fw_find(L, pa)] : proot;
+      L.val[e] = fmaf(ch.w_int[a], L.val[e], Pp);
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && need) L.pp[lane] = L.val[fw_find(L, p)];
+  __syncthreads();
+  return true;
+}
+
 __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const float* __restrict__ X, const float* __restrict__ Mf, int DP, int nq, int K, int capq,
     const int* __restrict__ qcnt, const int* __restrict__ qover, const int* __restrict__ crow,
@@ -1802,6 +1925,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   __shared__ int s_wr[kFwThreads];
   __shared__ int s_rr[64];
   __shared__ int s_ns;
+  __shared__ FwChainLds s_chain;   // exact parent chains (fw_chain_prefixes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
   const size_t base = (size_t)q * capq;
@@ -1875,9 +1999,13 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         s_part[sv * LDP + v] = part;
       }
       float pp = 0.f;
+      // exact parent chains (bounded internal prefixes): the whole workgroup, every distinct
+      // ancestor once (fw_chain_prefixes); the per-lane chain if its table overflows
+      const bool chained = use_chain && fw_chain_prefixes(s_chain, xg, chain, DP, wave == 0 && lane < cnt && p > 0, p,
+                                                          P[(size_t)q * ldP]);
       if (wave == 0 && lane < cnt) {
         pp = p < 0 ? (cat ? CWQ_INF : 0.f)
-                   : (use_chain && p > 0 ? exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP])
+                   : (use_chain && p > 0 ? (chained ? s_chain.pp[lane] : exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]))
                                          : P[(size_t)q * ldP + p]);
       }
       __syncthreads();

@@ -42,6 +42,8 @@ for s in "$@"; do
     prof100k) step prof_cat_g100k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cat -o cat --output-format csv -- \
         python3 scripts/basic_probe.py --clusters 100000 --queries 2000 --reps 1 --rank-queries 1 ;;
     fastb4) step fast_b4 600 python scripts/filter_probe.py --balanced 4,9 ;;
+    pcb4) step pc_b4 600 python scripts/percall_probe.py --balanced 4,9 --nq 1,8,64 --modes -1 ;;
+    pcb10) step pc_b10 600 python scripts/percall_probe.py --balanced 10,5 --nq 1,8,64 --modes -1 ;;
     profcatb4) step prof_cat_b4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_catb4 -o catb4 --output-format csv -- \
         python3 scripts/basic_probe.py --balanced 4,9 --queries 2000 --reps 1 --rank-queries 1 ;;
     ragged) step pytest_ragged 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 400 --timeout-method thread \
