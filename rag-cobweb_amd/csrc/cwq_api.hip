@@ -948,7 +948,33 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   g.root_ld = ix->root_ld;
   g.row_id = ix->int_rowid;
   g.nrows = (int)ix->ld_i2;
-  HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+  const int nqb = (c.nq + 15) / 16;
+  if (ix->int_path && c.nq <= kStreamMaxQ && stream_lds_bytes(nqb, ix->DPB2) <= (size_t)kStreamMaxLds &&
+      !getenv("CWQ_INT_STREAM_OFF")) {
+    // a few queries (the per-call path): the path-sum rows streamed once against <= 64
+    // queries (stream_kernel<2>) instead of 256-query MFMA tiles that are mostly padding;
+    // the same dots and root lines
+    StreamArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.DPB = ix->DPB2;
+    sa.nq = c.nq;
+    sa.nqb = nqb;
+    sa.nrows = ix->ld_i2;
+    sa.K = 1;
+    sa.Xb = Xb2;
+    sa.qinfo = qinfo2;
+    sa.Mb = ix->int_Mb2;
+    sa.rf = ix->int_rf2;
+    sa.row_id = ix->int_rowid;
+    sa.Sroot = Sroot;
+    sa.root_w = ix->root_w;
+    sa.root_ld = ix->root_ld;
+    sa.pout = c.P;
+    sa.ldpout = g.ldlb;
+    HIPCHK(launch_stream(sa, 2, ix->cus, s));
+  } else {
+    HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
+  }
   if (!ix->int_path)
     for (size_t lv = 2; lv < ix->levels.size(); ++lv)
       HIPCHK(launch_prefix_bounds(c.P, c.S_int, std::max(ix->NI, 1), c.nq, ix->levels[lv].first,

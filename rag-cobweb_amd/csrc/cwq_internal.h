@@ -444,6 +444,13 @@ struct StreamArgs {
   int* Tlive;                  // [nq] ordered-int live threshold (= Tb + K * nq)
   int live_every;              // filter: raise T to Tlive every this many groups (0: off)
   float* T;                    // [nq] initial threshold (written by the filter launch, read by final_kernel)
+  // MODE 2 (path-sum dots): operand row -> internal id, the root's exact raw sum and terms,
+  // output lines [internal id][ldpout]
+  const int* row_id;
+  const float* Sroot;
+  float root_w, root_ld;
+  float* pout;
+  int64_t ldpout;
   int* qcnt;                   // [nq] candidates per query
   int* qover;                  // [nq] list overflow
   int capq;                    // candidate slots per query
@@ -451,7 +458,7 @@ struct StreamArgs {
   float* cu;
   float* cl;
 };
-hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s);   // mode 1 probe, 0 filter
+hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s);   // 0 filter, 1 probe, 2 path dots
 hipError_t launch_stream_init(int* Tb, int n, hipStream_t s);
 
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,

@@ -60,6 +60,9 @@ __device__ __forceinline__ int f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 
+// MODE 0: filter (candidates), 1: threshold probe, 2: the path-sum dots of the internal
+// rows for a few queries (run_internal_bounds' small-batch form: rows x <= 64 queries
+// streamed once instead of 256-query fgemm tiles that are mostly padding).
 // MQB: query blocks the instantiation holds (1: nq <= 16, the per-call case, fewer live
 // registers; SK_MAXQB otherwise)
 template <int MODE, int MQB>
@@ -94,6 +97,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
   }
   __syncthreads();
+  float proot[MQB];   // MODE 2: the root's exact prefix per query (fgemm_kernel<2>'s formula)
+#pragma unroll
+  for (int qb = 0; qb < MQB; ++qb)
+    proot[qb] = (MODE == 2 && qok[qb]) ? a.root_w * (-0.5f * (a.root_ld + a.Sroot[qb * 16 + (lane & 15)])) : 0.f;
   const int64_t ngroups = MODE == 1 ? a.n_probe : (int64_t)((a.nrows + 15) >> 4);
   const int64_t gstride = (int64_t)gridDim.x * SK_WAVES;
   const int c16 = lane >> 4, r16 = lane & 15;
@@ -195,8 +202,25 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
       for (int qb = 0; qb < MQB; ++qb) Tq[qb] = fmaxf(Tq[qb], ord2f(tlive[qb]));
     }
+    if (MODE == 2) {
+      // path-sum dots, node-major: row r0 + 4 c16 + j is internal node row_id[r]; the
+      // root's line gets its exact prefix (run_internal_bounds' fgemm_kernel<2> output)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t r = r0 + 4 * c16 + j;
+        const int rid = (rf[j].par >= -1 && r < a.nrows) ? a.row_id[r] : -1;
+        if (rid < 0) continue;
+#pragma unroll
+        for (int qb = 0; qb < MQB; ++qb) {
+          if (qb >= nqb) break;
+          if (!qok[qb]) continue;
+          a.pout[(size_t)rid * a.ldpout + qb * 16 + r16] = rf[j].par < 0 ? proot[qb] : acc[qb][j];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      if (MODE == 2) break;
       const bool rok = rf[j].par >= -1;
       if (rok && rf[j].par != cpar) {
         cpar = rf[j].par;
@@ -276,10 +300,12 @@ hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s)
     return hipErrorInvalidValue;
   static bool attr = false;   // dynamic LDS above the 64 KiB default
   if (!attr) {
-    const void* fns[4] = {reinterpret_cast<const void*>(&stream_kernel<0, 1>),
+    const void* fns[6] = {reinterpret_cast<const void*>(&stream_kernel<0, 1>),
                           reinterpret_cast<const void*>(&stream_kernel<0, SK_MAXQB>),
                           reinterpret_cast<const void*>(&stream_kernel<1, 1>),
-                          reinterpret_cast<const void*>(&stream_kernel<1, SK_MAXQB>)};
+                          reinterpret_cast<const void*>(&stream_kernel<1, SK_MAXQB>),
+                          reinterpret_cast<const void*>(&stream_kernel<2, 1>),
+                          reinterpret_cast<const void*>(&stream_kernel<2, SK_MAXQB>)};
     for (const void* f : fns) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
       if (e != hipSuccess) return e;
@@ -289,9 +315,11 @@ hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s)
   const dim3 grid((unsigned)n_wg), block(64 * SK_WAVES);
   if (a.nqb == 1) {
     if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, 1>), grid, block, lds, s, a);
+    else if (mode == 2) hipLaunchKernelGGL((stream_kernel<2, 1>), grid, block, lds, s, a);
     else hipLaunchKernelGGL((stream_kernel<0, 1>), grid, block, lds, s, a);
   } else {
     if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, SK_MAXQB>), grid, block, lds, s, a);
+    else if (mode == 2) hipLaunchKernelGGL((stream_kernel<2, SK_MAXQB>), grid, block, lds, s, a);
     else hipLaunchKernelGGL((stream_kernel<0, SK_MAXQB>), grid, block, lds, s, a);
   }
   return hipGetLastError();
