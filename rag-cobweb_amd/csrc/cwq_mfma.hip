@@ -1376,39 +1376,42 @@ __global__ __launch_bounds__(256) void tile_prange_t_kernel(const float* __restr
 }
 
 // Path-sum dots (PathB): thread = query, one tile per blockIdx.y; each parent's dot line
-// read coalesced over the block's queries, turned into [lo, hi] by path_bounds with the
-// parent's RowF (uniform over the block: scalar loads); parents without an operand row
-// (no isotropic leaf row below them) are not parents of the tile's rows and are skipped.
+// read coalesced over the block's queries (eight in flight), turned into [lo, hi] by
+// path_bounds with the parent's RowF (staged in LDS once per block); parents without an
+// operand row (no isotropic leaf row below them) are not parents of the tile's rows and are
+// skipped.
 __global__ __launch_bounds__(256) void tile_prange_pb_kernel(const PathB pb, int nq, const TileF* __restrict__ tf,
                                                              int t0, float2* __restrict__ pmm, int64_t ldq) {
+  __shared__ RowF s_f[kFgMaxTileParents];   // the tile's parents' RowF, staged once per block
   const int t = t0 + blockIdx.y;
   const TileF T = tf[t];
-  if (T.uniform != 2) return;
+  if (T.uniform != 2) return;   // uniform over the block
+  const int np = min(T.par_hi - T.par + 1, kFgMaxTileParents);
+  for (int i = threadIdx.x; i < np; i += blockDim.x) s_f[i] = pb.nrf[T.par + i];
+  __syncthreads();
   const int q = blockIdx.x * 256 + threadIdx.x;
   if (q >= nq) return;
   const float4 qi = pb.qi2[q];
   const float proot = pb.dot[q];
   float mn = CWQ_INF, mx = -CWQ_INF;
-  auto one = [&](int p) {
-    const RowF f = pb.nrf[p];
-    const float d = pb.dot[(size_t)p * pb.ld + q];
-    float lo, hi;
-    if (p == 0) lo = hi = d;
-    else path_bounds(d, qi, f, proot, lo, hi);
-    if (f.par >= -1 || p == 0) {
+  // eight dot lines in flight per step (independent loads, then the bounds)
+  for (int i0 = 0; i0 < np; i0 += 8) {
+    float d8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d8[u] = i0 + u < np ? pb.dot[(size_t)(T.par + i0 + u) * pb.ld + q] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u, p = T.par + i;
+      if (i >= np) break;
+      const RowF f = s_f[i];
+      if (f.par < -1 && p != 0) continue;   // no operand row: not a parent of the tile's rows
+      float lo, hi;
+      if (p == 0) lo = hi = d8[u];
+      else path_bounds(d8[u], qi, f, proot, lo, hi);
       mn = fminf(mn, fminf(lo * T.invL, hi * T.invL));
       mx = fmaxf(mx, fmaxf(lo * T.invL, hi * T.invL));
     }
-  };
-  // four lines in flight per step (the loads of a step are independent)
-  int p = T.par;
-  for (; p + 3 <= T.par_hi; p += 4) {
-    one(p);
-    one(p + 1);
-    one(p + 2);
-    one(p + 3);
   }
-  for (; p <= T.par_hi; ++p) one(p);
   pmm[(size_t)t * ldq + q] = make_float2(mn, mx);
 }
 
