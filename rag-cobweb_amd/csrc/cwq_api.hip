@@ -107,6 +107,11 @@ struct cwq_index {
   uint16_t* iso_Mb = nullptr;
   RowF* iso_rf = nullptr;
   TileF* iso_tf = nullptr;
+  // int8 operands of the stream filter pass (launch_rows_i8), built on the first small-batch
+  // call: 0 not yet, 1 built, -1 off (CWQ_STREAM_I8=0, DPB % 64, or too little free memory)
+  int8_t* iso_Mq = nullptr;
+  RowF* iso_rf8 = nullptr;
+  int i8_state = 0;
   std::vector<int> tile_uni_prefix;   // prefix counts of uniform row tiles (all_uniform per launch range)
   int n_multi_tiles = 0;              // tiles with several parents (TileF uniform 2)
   // the same tables for the categorize key min(BF[parent], lp) (cwq_categorize through the
@@ -1258,6 +1263,32 @@ bool use_stream(const cwq_index* ix, int64_t nq, int k) {
   return !(e && *e && atoi(e) == 0);
 }
 
+// The stream filter's int8 row panel (half the bf16 panel's bytes per row; the per-call pass
+// is HBM-bound).  Built once, from the fp32 rerank copy, when the device has room for it.
+// Used when it pays: the pass saves ~half its HBM time, the wider int8 bounds cost the
+// exact rerank ~10x the reranks per query (one workgroup per query).  Measured at D = 768
+// (profiles/r03_i8_*): a win at 1M rows and nq = 1 (-75 us), a loss at 100k rows; so by
+// default for nq <= 16 and an int8 panel of >= kI8MinBytes.  CWQ_STREAM_I8=0 / 1: off /
+// forced on (read per call, for in-process A/Bs).
+constexpr int64_t kI8MinBytes = (int64_t)384 << 20;
+bool ensure_i8(cwq_index* ix, int64_t nq, hipStream_t s) {
+  const char* e = getenv("CWQ_STREAM_I8");
+  if (e && *e && atoi(e) == 0) return false;
+  if (!(e && *e && atoi(e) == 1) && (nq > 16 || (int64_t)ix->NL_iso * ix->DPB < kI8MinBytes)) return false;
+  if (ix->i8_state) return ix->i8_state > 0;
+  ix->i8_state = -1;
+  if (ix->DPB % 64 || !ix->iso_Mf || !ix->iso_rf) return false;
+  const size_t need = (size_t)ix->ld_f * ix->DPB + (size_t)ix->ld_f * sizeof(RowF);
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < need + std::max<size_t>((size_t)4 << 30, tot / 20)) return false;
+  if (ix->alloc(&ix->iso_Mq, (size_t)ix->ld_f * ix->DPB) || ix->alloc(&ix->iso_rf8, (size_t)ix->ld_f)) return false;
+  if (launch_rows_i8(ix->iso_Mf, ix->DP, ix->D, ix->iso_c, ix->DPB, ix->ld_f, ix->iso_rf, ix->iso_Mq, ix->iso_rf8, s) !=
+      hipSuccess)
+    return false;
+  ix->i8_state = 1;
+  return true;
+}
+
 int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                      hipStream_t s) {
   const int K = k, kl = k <= 16 ? 16 : 64;
@@ -1271,7 +1302,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                 (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)64 * nqc * 4 + (size_t)nqc * 4 +
                 (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
                 (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256 +
-                int_bounds_bytes(ix, kFgTile);
+                int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512;
+  const bool i8 = ensure_i8(ix, nq, s);
   int rc;
   if ((rc = ix->reserve(need))) return rc;
   Bump b(ix->ws, ix->ws_size);
@@ -1282,6 +1314,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   int* prow = b.take<int>((size_t)nq_pad * slabs * K);
   uint16_t* Xb = b.take<uint16_t>((size_t)nq16 * ix->DPB);
   float4* qinfo = b.take<float4>(nq16);
+  int8_t* Xq = i8 ? b.take<int8_t>((size_t)nq16 * ix->DPB) : nullptr;
+  float4* qinfo8 = i8 ? b.take<float4>(nq16) : nullptr;
   int* Tb = b.take<int>((size_t)(K + 1) * nqc);   // [K][nq] blocks + [nq] live threshold
   float* T = b.take<float>(nqc);
   int* qcnt = b.take<int>((size_t)5 * nqc);   // [qcnt | ok | n_exact | qover | done]
@@ -1317,6 +1351,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     sp.X = c.X;
     sp.Xb = Xb;
     sp.qinfo = qinfo;
+    sp.Xq = Xq;
+    sp.qinfo8 = qinfo8;
     sp.c = ix->iso_c;
     sp.A = ix->int_A;
     sp.B = ix->int_B;
@@ -1348,6 +1384,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     }
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
     HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
+    if (i8) HIPCHK(launch_query_prep_i8(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xq, qinfo8, s));
     HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
   }
   const FiltConsts fc = filt_consts(ix->DPB);
@@ -1401,7 +1438,17 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
   HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
-  HIPCHK(launch_stream(a, 0, ix->cus, s));
+  if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)
+    StreamArgs a8 = a;
+    a8.i8 = 1;
+    a8.Xb = reinterpret_cast<const uint16_t*>(Xq);
+    a8.qinfo = qinfo8;
+    a8.Mb = reinterpret_cast<const uint16_t*>(ix->iso_Mq);
+    a8.rf = ix->iso_rf8;
+    HIPCHK(launch_stream(a8, 0, ix->cus, s));
+  } else {
+    HIPCHK(launch_stream(a, 0, ix->cus, s));
+  }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
   int nst = 0;
   if ((rc = run_leaf_scan(ix, c, EPI_TOPK, false, kl, 0.f, nullptr, 0, pkey, paux, prow, K, &nst, s, 2, 1, slabs)))
@@ -1410,7 +1457,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   if ((rc = ix->host_flags((size_t)3 * nqc))) return rc;
   // one candidate list per query (no anisotropic rows): final_wide expands the top-K to
   // sentence ids and writes the host flags itself (no merge launch, no flag copy)
-  const bool ftail = nst == 1 && final_wide_lds(ix->DP, capq) <= 65536 && !getenv("CWQ_FW_UNFUSED");
+  const bool ftail = nst == 1 && final_wide_rows(ix->DP, capq) > 0 && !getenv("CWQ_FW_UNFUSED");
   const FwExpand fx{ix->sent_ptr, ix->sent_ids, ids, scores, k, ix->hflags};
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, c.pT ? 1 : c.ldP, 0, pkey, paux, prow, (int64_t)nst * K, okf,

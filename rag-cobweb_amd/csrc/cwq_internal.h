@@ -344,6 +344,27 @@ __device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, floa
   }
 }
 
+// list64_insert with an aux value carried along (final_wide_kernel's (key, lp, row) lists)
+__device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr, int lane, float ck, float ca, int cr,
+                                                  int K) {
+  const bool prec = lk > ck || (lk == ck && lr < cr);
+  const int pos = __popcll(__ballot(prec));
+  if (pos < K) {
+    const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
+    const float sa = __int_as_float(wave_shr1(__float_as_int(la)));
+    const int sr = wave_shr1(lr);
+    if (lane == pos) {
+      lk = ck;
+      la = ca;
+      lr = cr;
+    } else if (lane > pos) {
+      lk = sk;
+      la = sa;
+      lr = sr;
+    }
+  }
+}
+
 __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float key, int row, int K) {
   const float tk = rl_f2(lk, K - 1);
   const int tr = __builtin_amdgcn_readlane(lr, K - 1);
@@ -401,6 +422,8 @@ struct SbPrepArgs {
   float* X;             // scan layout, nq_pad rows
   void* Xb;             // bf16 hi parts [nq16][DPB]
   float4* qinfo;        // [nq16]
+  void* Xq;             // int8 parts [nq16][DPB] of the stream filter's int8 pass (NULL: none)
+  float4* qinfo8;       // [nq16] {|x'|^2, |x_hi8|, |x_lo8|, scale}
   const float* c;       // centre (root mean)
   const float *A, *B;   // internal nodes, dim-major [DP][ld]
   int64_t ld;
@@ -417,9 +440,21 @@ hipError_t launch_sb_prep(const SbPrepArgs& a, hipStream_t s);
 constexpr int kStreamMaxLds = 160 * 1024;
 constexpr int kStreamChunk = 8;   // K fragments (of 32 dims) per stream-kernel load chunk
 // query fragments in LDS, K padded with zero fragments to whole chunks
-inline size_t stream_lds_bytes(int nqb, int DPB) {
-  return (size_t)nqb * ((DPB / 32 + kStreamChunk - 1) / kStreamChunk * kStreamChunk) * 64 * 16;
+constexpr int kStreamSlots = 32;   // filter: candidate slots per query in each workgroup's LDS buffer
+inline size_t stream_lds_bytes(int nqb, int DPB, bool i8 = false, bool cand = false) {
+  const int nk = DPB / (i8 ? 64 : 32);   // 16-B fragments per row: 32 bf16 / 64 int8 dims
+  return (size_t)nqb * ((nk + kStreamChunk - 1) / kStreamChunk * kStreamChunk) * 64 * 16 +
+         (cand ? (size_t)nqb * 16 * (2 + 3 * kStreamSlots) * 4 : 0);
 }
+// int8 operands of the stream filter pass (built on the first small-batch call, launch_rows_i8):
+// per row r, s_r = max_d |mu'_d| / 127, q = rint(mu' / s_r) (int8, DPB wide, zero padded),
+// RowF = iso_rf[r] with beta = |mu' - s_r q|, delta = |s_r q| + beta and R0 = s_r.  The
+// products are exact (int32 sums), so the bound has no accumulation term (gamma = 0).
+hipError_t launch_rows_i8(const float* Mf, int DP, int D, const float* c, int DPB, int64_t ld, const RowF* rf,
+                          void* Mq, RowF* rf8, hipStream_t s);
+// queries likewise: Xq [nq16][DPB], qinfo8 {|x'|^2, |x_hi|, |x_lo|, s_x}
+hipError_t launch_query_prep_i8(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq16, void* Xq,
+                                float4* qinfo8, hipStream_t s);
 struct StreamArgs {
   int DPB, nq, nqb;            // queries, 16-query blocks (nqb * 16 >= nq)
   int64_t nrows;               // isotropic filter rows
@@ -430,6 +465,8 @@ struct StreamArgs {
   int64_t ldlb;
   const float* T0;             // filter: initial threshold T0[q * ldT0 + K - 1] (select over lb)
   int64_t ldT0;
+  int i8;                      // filter: int8 operands (Xb, Mb int8; qinfo.w, rf.R0 the scales)
+  int slots;                   // filter: LDS candidate slots per query (set by launch_stream)
   const uint16_t* Xb;          // [>= nqb*16][DPB] bf16 hi of the centred queries
   const float4* qinfo;         // [>= nqb*16]
   const uint16_t* Mb;          // [ld_f][DPB] bf16 row panel
@@ -525,7 +562,8 @@ struct FwExpand {
   int k;
   int* hflags;
 };
-size_t final_wide_lds(int DP, int capq);   // dynamic LDS of final_wide_kernel (<= 64 KiB to run)
+size_t final_wide_lds(int DP, int capq);   // dynamic LDS of final_wide_kernel (SIZE_MAX: cannot run)
+int final_wide_rows(int DP, int capq);     // survivors per rerank round
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
                         int64_t ldT, const RowMeta* meta, const int* par, const float* P, int64_t ldP, int seg_base,

@@ -120,6 +120,93 @@ hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int
   return hipGetLastError();
 }
 
+// int8 split of one centred row or query (one wave; cwq_internal.h launch_rows_i8):
+// s = max|v| / 127, q = rint(v / s) clamped to +-127, hi = s q, lo = v - hi.  hi and lo are
+// formed in fp64, where both are exact (a 24-bit by 8-bit product; a difference within 31
+// bits), so the split is exact whatever s rounds to; the norms are rounded up by the callers.
+template <class F>
+__device__ __forceinline__ void i8_split_wave(F val, int DPB, int8_t* dst, double& sv, double& shi, double& slo,
+                                              float& sc) {
+  const int lane = threadIdx.x & 63;
+  float m = 0.f;
+  for (int d = lane; d < DPB; d += kWave) m = fmaxf(m, fabsf(val(d)));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  const float s = m / 127.f;
+  sv = shi = slo = 0.0;
+  for (int d = lane; d < DPB; d += kWave) {
+    const float v = val(d);
+    const int qv = s > 0.f ? max(-127, min(127, (int)rintf(v / s))) : 0;
+    dst[d] = (int8_t)qv;
+    const double hi = (double)s * (double)qv;
+    const double lo = (double)v - hi;
+    sv += (double)v * (double)v;
+    shi += hi * hi;
+    slo += lo * lo;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    sv += __shfl_xor(sv, off, 64);
+    shi += __shfl_xor(shi, off, 64);
+    slo += __shfl_xor(slo, off, 64);
+  }
+  sc = s;
+}
+
+// Rows (launch_rows_i8): the centred row as rows_prep forms it (Mf - c in fp32), one wave
+// per row; unusable rows (par < -1) get zeros and scale 0.
+__global__ void rows_i8_kernel(const float* __restrict__ Mf, int DP, int D, const float* __restrict__ c, int DPB,
+                               int64_t ld, const RowF* __restrict__ rf, int8_t* Mq, RowF* rf8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= ld) return;
+  RowF f = rf[r];
+  const bool ok = f.par >= -1;
+  double sv, shi, slo;
+  float sc;
+  i8_split_wave([&](int d) { return (ok && d < D) ? Mf[r * DP + d] - c[d] : 0.f; }, DPB, Mq + r * DPB, sv, shi, slo,
+                sc);
+  if (lane == 0) {
+    if (ok) {
+      const double bh = sqrt(shi), bl = sqrt(slo);
+      f.beta = up(bl);
+      f.delta = up(bh + bl);
+      f.R0 = sc;
+    } else {
+      f.R0 = 0.f;
+    }
+    rf8[r] = f;
+  }
+}
+
+hipError_t launch_rows_i8(const float* Mf, int DP, int D, const float* c, int DPB, int64_t ld, const RowF* rf,
+                          void* Mq, RowF* rf8, hipStream_t s) {
+  if (ld <= 0) return hipSuccess;
+  if (DPB % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_i8_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, Mf, DP, D, c, DPB, ld, rf,
+                     (int8_t*)Mq, rf8);
+  return hipGetLastError();
+}
+
+// Queries for the int8 pass, as query_prep_kernel forms the centred query.
+__global__ void query_prep_i8_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c,
+                                     int DPB, int64_t nq16, int8_t* Xq, float4* qinfo8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (r >= nq16) return;
+  double sv, shi, slo;
+  float sc;
+  i8_split_wave([&](int d) { return (r < nq && d < D) ? q[r * D + d] - c[d] : 0.f; }, DPB, Xq + r * DPB, sv, shi, slo,
+                sc);
+  if (lane == 0) qinfo8[r] = make_float4((float)sv, up(sqrt(shi)), up(sqrt(slo)), sc);
+}
+
+hipError_t launch_query_prep_i8(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq16, void* Xq,
+                                float4* qinfo8, hipStream_t s) {
+  if (DPB % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(query_prep_i8_kernel, dim3((unsigned)((nq16 + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DPB, nq16,
+                     (int8_t*)Xq, qinfo8);
+  return hipGetLastError();
+}
+
 // Queries: bf16 hi part of the centred query, and {|x'|^2, |x_hi|, |x_lo|}.
 __global__ void query_prep_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c,
                                   int DPB, int64_t nq_pad, __bf16* Xb, float4* qinfo) {
@@ -199,6 +286,13 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
       shi += __shfl_xor(shi, off, 64);
     }
     if (lane == 0) a.qinfo[r] = make_float4((float)sv, up(sqrt(shi)), up(sqrt(slo)), 0.f);
+  }
+  if (r < a.nq16 && a.Xq && tid >= 64 && tid < 128) {   // query_prep_i8_kernel (wave 1)
+    double sv, shi, slo;
+    float sc;
+    i8_split_wave([&](int d) { return (valid && d < a.D) ? xq[d] - cq[d] : 0.f; }, a.DPB,
+                  reinterpret_cast<int8_t*>(a.Xq) + r * a.DPB, sv, shi, slo, sc);
+    if (lane == 0) a.qinfo8[r] = make_float4((float)sv, up(sqrt(shi)), up(sqrt(slo)), sc);
   }
   if (!valid) return;
   if (tid < 5) a.qcnt[(size_t)tid * a.nq + r] = 0;
@@ -1789,6 +1883,9 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
 // count is known; entries past it are never used), and the survivors' row terms fly with
 // their partials' row loads.  fx (optional): the fused expansion + host flags (FwExpand).
 constexpr int kFwThreads = 512;
+constexpr int kFwCand = 4096;   // candidates whose l, u are staged in LDS (= kFgCapQ)
+constexpr int kFwMaxRows = 192;   // survivors per rerank round (three key waves)
+constexpr int kFwDynMax = 56 * 1024;   // dynamic LDS budget (the static part is ~103 KiB of 160)
 // Exact path prefixes of a round's survivor parents with the whole workgroup
 // (final_wide_kernel, hierarchical trees): the distinct ancestors of every parent go into an
 // LDS table (wave 0; a lane stops at the first node another lane has entered, whose
@@ -1919,15 +2016,19 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const RowMeta* __restrict__ meta, const int* __restrict__ par, const float* __restrict__ P, int64_t ldP,
     int seg_base, float* pkey, float* paux, int* prow, int64_t lstride, int* ok_flag, int* n_exact,
     const float* __restrict__ lkb, const int* __restrict__ lrb, const int* __restrict__ done, const IntChain chain,
-    int use_chain, int cat, float dconst, const FwExpand fx) {
+    int use_chain, int cat, float dconst, const FwExpand fx, int rows, int nopf) {
   extern __shared__ float s_dyn[];
   const int NV16 = DP / 16, LDP = NV16 + 1;                  // odd row pitch: conflict-free column reads
-  float* s_part = s_dyn;                                      // [64][LDP]
-  int* s_surv = reinterpret_cast<int*>(s_dyn + 64 * LDP);    // [capq] survivor positions
-  __shared__ float s_wl[kFwThreads], s_wu[kFwThreads];        // candidates 0..kFwThreads-1: l, u, row
-  __shared__ int s_wr[kFwThreads];
-  __shared__ int s_rr[64];
+  float* s_part = s_dyn;                                      // [rows][LDP]
+  int* s_surv = reinterpret_cast<int*>(s_dyn + rows * LDP);  // [capq] survivor positions
+  __shared__ float s_wl[kFwCand], s_wu[kFwCand];              // candidates' l, u (the first kFwCand)
+  __shared__ int s_wr[kFwThreads];                            // rows of candidates 0..kFwThreads-1
+  __shared__ float s_ml[kFwThreads], s_ma[kFwThreads];        // per-wave top-K lists (T2 and key merges)
+  __shared__ int s_mr[kFwThreads];
+  __shared__ int s_rr[kFwMaxRows];
+  __shared__ int s_nx;
   __shared__ int s_ns;
+  __shared__ float s_T2;
   __shared__ FwChainLds s_chain;   // exact parent chains (fw_chain_prefixes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
@@ -1942,83 +2043,139 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     s_wu[tid] = cu[base + tid];
     s_wr[tid] = crow[base + tid];
   }
+  if (tid == 0) {
+    s_ns = 0;
+    s_nx = 0;
+  }
   const bool ok = ov == 0 && n >= K && n <= capq && Tq > -CWQ_INF;   // uniform over the block
+  // the rest of the lists' l and u (one more round trip, every load of it in flight at once)
+  const int nst = ok ? min(n, kFwCand) : 0;
+  {
+    constexpr int B = kFwCand / kFwThreads - 1;
+    float tl[B], tu[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int j = kFwThreads * (i + 1) + tid;
+      if (j < nst) {
+        tl[i] = cl[base + j];
+        tu[i] = cu[base + j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const int j = kFwThreads * (i + 1) + tid;
+      if (j < nst) {
+        s_wl[j] = tl[i];
+        s_wu[j] = tu[i];
+      }
+    }
+  }
   float lk = -CWQ_INF, la = 0.f;
   int lr = 0x7fffffff, nx = 0;
   __syncthreads();
   if (ok) {
-    if (wave == 0) {
-      float tk = d ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
-      int tr = d ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
-      for (int j0 = d; j0 < n; j0 += 64) {
+    // T2 = K-th largest l: every wave keeps the top-K of its slice, wave 0 merges the lists
+    {
+      float tk = (d && wave == 0) ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
+      int tr = (d && wave == 0) ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
+      for (int j0 = d + wave * 64; j0 < n; j0 += kFwThreads) {
         const int j = j0 + lane;
-        const float lv = j >= n ? -CWQ_INF : j < kFwThreads ? s_wl[j] : cl[base + j];
+        const float lv = j >= n ? -CWQ_INF : j < kFwCand ? s_wl[j] : cl[base + j];
         list64_offer(tk, tr, lane, lv, j, K);
       }
-      const float T2 = rl_f2(tk, K - 1);
-      int ns = 0;
-      for (int j0 = 0; j0 < n; j0 += 64) {
-        const int j = j0 + lane;
-        const bool c = j < n && (j < kFwThreads ? s_wu[j] : cu[base + j]) >= T2;
-        const uint64_t bm = __ballot(c);
-        if (c) s_surv[ns + __popcll(bm & ((1ull << lane) - 1))] = j;
-        ns += __popcll(bm);
+      s_ml[tid] = lane < K ? tk : -CWQ_INF;
+      s_mr[tid] = lane < K ? tr : 0x7fffffff;
+      __syncthreads();
+      if (wave == 0) {
+        for (int w = 1; w < kFwThreads / 64; ++w) list64_offer(tk, tr, lane, s_ml[w * 64 + lane], s_mr[w * 64 + lane], K);
+        if (lane == 0) s_T2 = rl_f2(tk, K - 1);
       }
-      if (lane == 0) s_ns = ns;
+      __syncthreads();
+    }
+    const float T2 = s_T2;
+    // survivors u >= T2, compacted by all waves (their order does not matter: the top-K
+    // list below is ordered by (key, row))
+    for (int j0 = wave * 64; j0 < n; j0 += kFwThreads) {
+      const int j = j0 + lane;
+      const bool c = j < n && (j < kFwCand ? s_wu[j] : cu[base + j]) >= T2;
+      const uint64_t bm = __ballot(c);
+      int o = 0;
+      if (lane == 0 && bm) o = atomicAdd(&s_ns, __popcll(bm));
+      o = __shfl(o, 0, 64);
+      if (c) s_surv[o + __popcll(bm & ((1ull << lane) - 1))] = j;
     }
     __syncthreads();
     const int ns = s_ns;
     const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
-    for (int r0 = 0; r0 < ns; r0 += 64) {
-      const int cnt = min(64, ns - r0);
-      if (wave == 0 && lane < cnt) {
-        const int j = s_surv[r0 + lane];
-        s_rr[lane] = j < kFwThreads ? s_wr[j] : crow[base + j];
+    // survivors per round: `rows` (a multiple of 64: thread t < cnt forms survivor t's key in
+    // key wave t / 64, each key wave keeping its own top-K list, merged below); 64 with the
+    // exact parent chains (fw_chain_prefixes serves wave 0's lanes)
+    const int RR = use_chain ? 64 : rows;
+    for (int r0 = 0; r0 < ns; r0 += RR) {
+      const int cnt = min(RR, ns - r0);
+      if (tid < cnt) {
+        const int j = s_surv[r0 + tid];
+        s_rr[tid] = j < kFwThreads ? s_wr[j] : crow[base + j];
       }
       __syncthreads();   // s_rr visible; the previous round's partials consumed
-      // the survivors' row terms (wave 0), in flight with the partials' row loads
+      // the survivors' row terms (key threads), in flight with the partials' row loads
       RowMeta md;
       int p = -1, rr = 0;
-      if (wave == 0 && lane < cnt) {
-        rr = s_rr[lane];
+      if (tid < cnt) {
+        rr = s_rr[tid];
         md = meta[rr];
         p = par[rr];
       }
-      for (int t = tid; t < cnt * NV16; t += kFwThreads) {
-        const int sv = t / NV16, v = t - sv * NV16;
-        const float* __restrict__ mr = Mf + (size_t)s_rr[sv] * DP + v * 16;
-        float4 m4[4];
+      // FB items per thread per batch: every row load of the batch is in flight before the
+      // first partial is formed (one memory round trip per batch, not per item)
+      constexpr int FB = 4;
+      for (int t0 = tid; t0 < cnt * NV16; t0 += FB * kFwThreads) {
+        float4 m4[FB][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
-        const f32x16 xa = xg[(size_t)v * kXQ];
-        float part;
+        for (int b = 0; b < FB; ++b) {
+          const int t = t0 + b * kFwThreads;
+          if (t < cnt * NV16) {
+            const int sv = t / NV16, v = t - sv * NV16;
+            const float* __restrict__ mr = Mf + (size_t)s_rr[sv] * DP + v * 16;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float4 t4 = m4[j >> 2];
-          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
-          const float tt = xa[j] - mj;
-          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+            for (int j = 0; j < 4; ++j) m4[b][j] = *reinterpret_cast<const float4*>(mr + j * 4);
+          }
         }
-        s_part[sv * LDP + v] = part;
+#pragma unroll
+        for (int b = 0; b < FB; ++b) {
+          const int t = t0 + b * kFwThreads;
+          if (t >= cnt * NV16) break;
+          const int sv = t / NV16, v = t - sv * NV16;
+          const f32x16 xa = xg[(size_t)v * kXQ];
+          float part;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float4 t4 = m4[b][j >> 2];
+            const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+            const float tt = xa[j] - mj;
+            part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+          }
+          s_part[sv * LDP + v] = part;
+        }
       }
       float pp = 0.f;
       // exact parent chains (bounded internal prefixes): the whole workgroup, every distinct
       // ancestor once (fw_chain_prefixes); the per-lane chain if its table overflows
-      const bool chained = use_chain && fw_chain_prefixes(s_chain, xg, chain, DP, wave == 0 && lane < cnt && p > 0, p,
+      const bool chained = use_chain && fw_chain_prefixes(s_chain, xg, chain, DP, tid < cnt && p > 0, p,
                                                           P[(size_t)q * ldP]);
-      if (wave == 0 && lane < cnt) {
+      if (tid < cnt) {
         pp = p < 0 ? (cat ? CWQ_INF : 0.f)
                    : (use_chain && p > 0 ? (chained ? s_chain.pp[lane] : exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]))
                                          : P[(size_t)q * ldP + p]);
       }
       __syncthreads();
-      if (wave == 0) {
-        const bool act = lane < cnt;
+      if (wave * 64 < cnt) {
+        const bool act = tid < cnt;
         float key = -CWQ_INF, lp = 0.f;
         int rid = 0x7fffffff;
         if (act) {
           float acc = 0.f;
-          const float* pr = s_part + lane * LDP;
+          const float* pr = s_part + tid * LDP;
           int v = 0;
           for (; v + 8 <= NV16; v += 8) {   // 8 reads in flight, then the adds in slice order
             float t8[8];
@@ -2034,7 +2191,10 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           rid = seg_base + rr;
           ++nx;
         }
-        uint64_t mask = __ballot(act);
+        // only keys that beat the list's K-th entry can enter (insertions are serial)
+        const float tk = rl_f2(lk, K - 1);
+        const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+        uint64_t mask = __ballot(act && (nopf || key > tk || (key == tk && rid < tr)));
         while (mask) {
           const int b = __builtin_ctzll(mask);
           mask &= mask - 1;
@@ -2059,9 +2219,37 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         }
       }
     }
+    // the key waves' lists -> wave 0's (same insertion; a no-op with one key wave)
+    const int nkw = ns > 0 ? (min(RR, ns) + 63) / 64 : 0;
+    if (nkw > 1) {
+      __syncthreads();
+      if (wave > 0 && wave < nkw) {
+        s_ml[tid] = lane < K ? lk : -CWQ_INF;
+        s_ma[tid] = la;
+        s_mr[tid] = lane < K ? lr : 0x7fffffff;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        for (int w = 1; w < nkw; ++w) {
+          const float key = s_ml[w * 64 + lane], lp = s_ma[w * 64 + lane];
+          const int rid = s_mr[w * 64 + lane];
+          const float tk = rl_f2(lk, K - 1);
+          const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+          uint64_t mask = __ballot(rid != 0x7fffffff && (key > tk || (key == tk && rid < tr)));
+          while (mask) {
+            const int b = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K);
+          }
+        }
+      }
+    }
   }
-  if (wave != 0) return;
   for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
+  if (lane == 0 && nx) atomicAdd(&s_nx, nx);
+  __syncthreads();
+  if (wave != 0) return;
+  nx = s_nx;
   if (fx.ids) {
     // merge_expand_kernel's expansion of the (already sorted) top-K rows, in place
     if (!ok) {
@@ -2112,7 +2300,17 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   }
 }
 
-size_t final_wide_lds(int DP, int capq) { return ((size_t)64 * (DP / 16 + 1) + (size_t)capq) * 4; }
+// survivors per rerank round of final_wide_kernel: a multiple of 64 (<= kFwMaxRows) whose
+// partials fit the dynamic LDS budget next to the survivor list; 0: the kernel cannot run
+int final_wide_rows(int DP, int capq) {
+  const int64_t avail = (int64_t)kFwDynMax - (int64_t)capq * 4;
+  const int64_t r = avail > 0 ? avail / ((int64_t)(DP / 16 + 1) * 4) / 64 * 64 : 0;
+  return (int)std::min<int64_t>(r, kFwMaxRows);
+}
+size_t final_wide_lds(int DP, int capq) {
+  const int rows = final_wide_rows(DP, capq);
+  return rows > 0 ? ((size_t)rows * (DP / 16 + 1) + (size_t)capq) * 4 : SIZE_MAX;
+}
 
 hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, int capq, const int* qcnt,
                         const int* qover, const int* crow, const float* cu, const float* cl, const float* T,
@@ -2125,10 +2323,13 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
   const char* we = getenv("CWQ_FINAL_WIDE");   // largest nq for the workgroup-per-query form
   const int wide_max = we && *we ? atoi(we) : kFinalWideMaxQ;
   const size_t lds = final_wide_lds(DP, capq);
-  if ((fx || nq <= wide_max) && lds <= 65536) {
+  if ((fx || nq <= wide_max) && lds <= (size_t)kFwDynMax) {
     hipLaunchKernelGGL(final_wide_kernel, dim3((unsigned)nq), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
                        qover, crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag,
-                       n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst, fe);
+                       n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst, fe,
+                       getenv("CWQ_FW_ROWS") ? std::min(final_wide_rows(DP, capq), atoi(getenv("CWQ_FW_ROWS")))
+                                             : final_wide_rows(DP, capq),
+                       getenv("CWQ_FW_NOPF") ? 1 : 0);
     return hipGetLastError();
   }
   if (fx) return hipErrorInvalidValue;   // the fused tail exists in the workgroup-per-query form only

@@ -40,6 +40,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "cwq_internal.h"
 
@@ -47,6 +48,7 @@ namespace cwq {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #define CWQ_INF __builtin_inff()
 
@@ -64,20 +66,43 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 // rows for a few queries (run_internal_bounds' small-batch form: rows x <= 64 queries
 // streamed once instead of 256-query fgemm tiles that are mostly padding).
 // MQB: query blocks the instantiation holds (1: nq <= 16, the per-call case, fewer live
-// registers; SK_MAXQB otherwise)
-template <int MODE, int MQB>
+// registers; SK_MAXQB otherwise).  I8 (filter only): int8 operands (launch_rows_i8) and
+// v_mfma_i32_16x16x64_i8 -- half the bytes of the bf16 panel per row.  A 16-B fragment
+// then holds 64 dims and the products are exact int32 sums; dot = acc * (s_x * s_r).  Both
+// operands are loaded with the same byte -> (lane, element) map, so the instruction's
+// internal k order inside a fragment does not matter for the dot product.
+// CH: K fragments per load chunk (8; 12 for int8 rows of 12 fragments, D = 768, so that no
+// chunk is partial and every wave keeps a whole chunk of HBM loads in flight).
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH>
 __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
+  static_assert(!I8 || MODE == 0, "int8 operands: filter pass only");
+  typedef typename std::conditional<I8, i32x4, bf16x8>::type frag_t;
+  typedef typename std::conditional<I8, i32x4, f32x4>::type acc_t;
+  constexpr int ES = I8 ? 1 : 2;   // operand bytes per dim
   extern __shared__ __attribute__((aligned(16))) char sq[];   // [nqb][nk][64 lanes][16 B]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int nk = a.DPB / 32;
-  const int nkp = (nk + SK_CH - 1) / SK_CH * SK_CH;   // K padded to whole chunks (zero fragments)
+  const int nk = a.DPB / (I8 ? 64 : 32);
+  const int nkp = (nk + CH - 1) / CH * CH;   // K padded to whole chunks (zero fragments)
   const int nqb = a.nqb;
-  // ---- stage the queries' bf16 fragments (B operand: k = 8*(l>>4).., query = l&15) ----
+  // filter: each workgroup collects its candidates in LDS (kStreamSlots per query) and
+  // appends them with one global atomic per query at its end -- per-candidate atomics on
+  // the query's counter serialise at ~1.5k candidates per query (int8 bounds, 64 queries:
+  // pass 300 -> 449 us); a full buffer falls back to the global append
+  const int SLB = MODE == 0 ? a.slots : 0;   // 0: no LDS buffer (it did not fit: per-candidate atomics)
+  int* s_cnt = reinterpret_cast<int*>(sq + (size_t)nqb * ((nk + kStreamChunk - 1) / kStreamChunk * kStreamChunk) * 1024);
+  int* s_base = s_cnt + nqb * 16;
+  int* s_crow = s_base + nqb * 16;
+  float* s_cu = reinterpret_cast<float*>(s_crow + nqb * 16 * SLB);
+  float* s_cl = s_cu + nqb * 16 * SLB;
+  if (SLB)
+    for (int i = threadIdx.x; i < nqb * 16; i += blockDim.x) s_cnt[i] = 0;
+  // ---- stage the queries' fragments (B operand: 16 B at k = (16/ES)*(l>>4).., query = l&15) ----
   for (int f = threadIdx.x; f < nqb * nkp * 64; f += blockDim.x) {
     const int l = f & 63, ks = (f >> 6) % nkp, qb = (f >> 6) / nkp;
     const int q = qb * 16 + (l & 15);
-    const uint4 v = ks < nk ? *reinterpret_cast<const uint4*>(a.Xb + ((size_t)q * a.DPB + ks * 32 + 8 * (l >> 4)))
+    const uint4 v = ks < nk ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.Xb) +
+                                                              ((size_t)q * a.DPB * ES + ks * 64 + 16 * (l >> 4)))
                             : make_uint4(0u, 0u, 0u, 0u);
     *reinterpret_cast<uint4*>(sq + (size_t)f * 16) = v;
   }
@@ -117,7 +142,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   const float* Pu = a.Phi ? a.Phi : a.P;
   auto panel = [&](int64_t gi) {
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
-    return reinterpret_cast<const char*>(a.Mb) + ((size_t)(grp * 16 + r16) * a.DPB + 8 * c16) * 2;
+    return reinterpret_cast<const char*>(a.Mb) + (size_t)(grp * 16 + r16) * a.DPB * ES + 16 * c16;
   };
   // row terms of the rows this lane's accumulator columns hold (r0 + 4*c16 + j)
   auto load_rf = [&](RowF (&dst)[4], int64_t g) {
@@ -129,8 +154,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
   };
   int64_t gi = (int64_t)blockIdx.x * SK_WAVES + wave;
-  if (gi >= ngroups) return;   // no barrier follows
-  // K runs in chunks of SK_CH fragments (16 B per lane each: row r0 + (lane & 15),
+  const bool idle = gi >= ngroups;   // no group for this wave (the filter's flush barrier follows)
+  if (idle) gi = 0;
+  // K runs in chunks of CH fragments (16 B per lane each: row r0 + (lane & 15),
   // k = ks*32 + 8*(lane >> 4)) over the wave's whole (group, chunk) sequence.  Two
   // register buffers alternate chunk by chunk: the loads of the next chunk (after a
   // group's last chunk, the first chunk of the wave's next group) go into one while the
@@ -141,26 +167,31 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   // a partial last chunk re-reads its last fragment (a cache hit) and multiplies the
   // extra copies by the zero query fragments of the LDS padding, and the wave's last
   // step re-reads its current chunk.
-  bf16x8 bA[SK_CH], bB[SK_CH];
-  auto issue = [&](bf16x8 (&b)[SK_CH], const char* p, int nfr) {
+  frag_t bA[CH], bB[CH];
+  auto issue = [&](frag_t (&b)[CH], const char* p, int nfr) {
 #pragma unroll
-    for (int i = 0; i < SK_CH; ++i) b[i] = *reinterpret_cast<const bf16x8*>(p + min(i, nfr - 1) * 64);
+    for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const frag_t*>(p + min(i, nfr - 1) * 64);
   };
-  f32x4 acc[MQB];
+  acc_t acc[MQB];
 #pragma unroll
-  for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&b)[SK_CH], int c0) {
+  for (int qb = 0; qb < MQB; ++qb) acc[qb] = acc_t{0, 0, 0, 0};
+  auto mma = [&](const frag_t (&b)[CH], int c0) {
 #pragma unroll
     for (int qb = 0; qb < MQB; ++qb) {
       if (qb >= nqb) break;
       const char* qs = sq + (((size_t)qb * nkp + c0) * 64 + lane) * 16;
 #pragma unroll
-      for (int i = 0; i < SK_CH; ++i)
-        acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[i], *reinterpret_cast<const bf16x8*>(qs + i * 1024),
-                                                          acc[qb], 0, 0, 0);
+      for (int i = 0; i < CH; ++i) {
+        if constexpr (I8)
+          acc[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[i], *reinterpret_cast<const i32x4*>(qs + i * 1024), acc[qb],
+                                                          0, 0, 0);
+        else
+          acc[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[i], *reinterpret_cast<const bf16x8*>(qs + i * 1024),
+                                                            acc[qb], 0, 0, 0);
+      }
     }
   };
-  issue(bA, panel(gi), min(SK_CH, nk));
+  issue(bA, panel(gi), min(CH, nk));
   // the group's row terms are loaded at its start and used at its end (in flight with
   // its chunks)
   RowF rf[4];
@@ -181,15 +212,15 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   // group's last chunk the epilogue runs and the wave moves to its next group.  Returns
   // false after the wave's last group.  The loop below alternates step(bA, bB) and
   // step(bB, bA), so which buffer is in flight is static in the code.
-  auto step = [&](const bf16x8 (&cur)[SK_CH], bf16x8 (&oth)[SK_CH]) -> bool {
+  auto step = [&](const frag_t (&cur)[CH], frag_t (&oth)[CH]) -> bool {
     int64_t gn = gi;
-    int cn = c0 + SK_CH;
+    int cn = c0 + CH;
     if (cn >= nk) {
       gn = gi + gstride;
       cn = 0;
     }
     const bool more = gn < ngroups;
-    issue(oth, more ? panel(gn) + cn * 64 : panel(gi) + c0 * 64, more ? min(SK_CH, nk - cn) : min(SK_CH, nk - c0));
+    issue(oth, more ? panel(gn) + cn * 64 : panel(gi) + c0 * 64, more ? min(CH, nk - cn) : min(CH, nk - c0));
     mma(cur, c0);
     if (cn != 0) {
       c0 = cn;
@@ -214,7 +245,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         for (int qb = 0; qb < MQB; ++qb) {
           if (qb >= nqb) break;
           if (!qok[qb]) continue;
-          a.pout[(size_t)rid * a.ldpout + qb * 16 + r16] = rf[j].par < 0 ? proot[qb] : acc[qb][j];
+          a.pout[(size_t)rid * a.ldpout + qb * 16 + r16] = rf[j].par < 0 ? proot[qb] : (float)acc[qb][j];
         }
       }
     }
@@ -242,7 +273,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         if (qb >= nqb) break;
         if (!rok || !qok[qb]) continue;
         float u, l;
-        fg_bounds2(acc[qb][j], 0x1p-23f * fabsf(acc[qb][j]), qi[qb], rf[j], cPh[qb] * rf[j].invL,
+        // int8: acc is exact; the two fp32 roundings of acc * (s_x * s_r) are within
+        // 2^-22 |dot| (2^-21 taken), and beta has no accumulation term
+        const float dot = I8 ? (float)acc[qb][j] * (qi[qb].w * rf[j].R0) : (float)acc[qb][j];
+        fg_bounds2(dot, (I8 ? 0x1p-21f : 0x1p-23f) * fabsf(dot), qi[qb], rf[j], cPh[qb] * rf[j].invL,
                    cP[qb] * rf[j].invL, a.eps_n, a.slack, u, l);
         if (MODE == 1) {
           pmax[qb] = fmaxf(pmax[qb], l);
@@ -257,6 +291,13 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
             for (int b = 0; b < a.K; ++b)
               m = min(m, __hip_atomic_load(&a.Tb[(size_t)b * a.nq + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             if (m != f2ord(-CWQ_INF)) atomicMax(&a.Tlive[q], m);
+          }
+          const int ls = SLB ? atomicAdd(&s_cnt[q], 1) : 0;
+          if (ls < SLB) {
+            s_crow[q * SLB + ls] = (int)(r0 + 4 * c16 + j);
+            s_cu[q * SLB + ls] = u;
+            s_cl[q * SLB + ls] = l;
+            continue;
           }
           const int slot = atomicAdd(&a.qcnt[q], 1);
           if (slot < a.capq) {
@@ -285,44 +326,72 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     load_rf(rf, gi);
     load_live(++it);
 #pragma unroll
-    for (int qb = 0; qb < MQB; ++qb) acc[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qb = 0; qb < MQB; ++qb) acc[qb] = acc_t{0, 0, 0, 0};
     return true;
   };
-  while (step(bA, bB) && step(bB, bA)) {
+  if (!idle)
+    while (step(bA, bB) && step(bB, bA)) {
+    }
+  if (MODE != 0 || !SLB) return;
+  // ---- flush the workgroup's candidate buffer: one global atomic per query ----
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.nq; i += blockDim.x) {
+    const int c = min(s_cnt[i], SLB);
+    s_base[i] = c > 0 ? atomicAdd(&a.qcnt[i], c) : 0;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < a.nq * SLB; e += blockDim.x) {
+    const int i = e / SLB, k = e - i * SLB;
+    if (k >= min(s_cnt[i], SLB)) continue;
+    const int slot = s_base[i] + k;
+    if (slot < a.capq) {
+      const size_t o = (size_t)i * a.capq + slot;
+      a.crow[o] = s_crow[e];
+      a.cu[o] = s_cu[e];
+      a.cl[o] = s_cl[e];
+    } else {
+      a.qover[i] = 1;
+    }
   }
 }
 
-hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s) {
-  const int nk = a.DPB / 32;
-  const size_t lds = stream_lds_bytes(a.nqb, a.DPB);
-  if (a.nq <= 0 || a.nqb * 16 < a.nq || a.nqb > SK_MAXQB || a.DPB % 32 || a.K < 1 || a.K > 64 ||
-      lds > (size_t)kStreamMaxLds)
-    return hipErrorInvalidValue;
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH>
+static hipError_t launch_one(const StreamArgs& a, int n_wg, size_t lds, hipStream_t s) {
   static bool attr = false;   // dynamic LDS above the 64 KiB default
   if (!attr) {
-    const void* fns[6] = {reinterpret_cast<const void*>(&stream_kernel<0, 1>),
-                          reinterpret_cast<const void*>(&stream_kernel<0, SK_MAXQB>),
-                          reinterpret_cast<const void*>(&stream_kernel<1, 1>),
-                          reinterpret_cast<const void*>(&stream_kernel<1, SK_MAXQB>),
-                          reinterpret_cast<const void*>(&stream_kernel<2, 1>),
-                          reinterpret_cast<const void*>(&stream_kernel<2, SK_MAXQB>)};
-    for (const void* f : fns) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
-      if (e != hipSuccess) return e;
-    }
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
+    if (e != hipSuccess) return e;
     attr = true;
   }
-  const dim3 grid((unsigned)n_wg), block(64 * SK_WAVES);
-  if (a.nqb == 1) {
-    if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, 1>), grid, block, lds, s, a);
-    else if (mode == 2) hipLaunchKernelGGL((stream_kernel<2, 1>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((stream_kernel<0, 1>), grid, block, lds, s, a);
-  } else {
-    if (mode == 1) hipLaunchKernelGGL((stream_kernel<1, SK_MAXQB>), grid, block, lds, s, a);
-    else if (mode == 2) hipLaunchKernelGGL((stream_kernel<2, SK_MAXQB>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((stream_kernel<0, SK_MAXQB>), grid, block, lds, s, a);
-  }
+  hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH>), dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
   return hipGetLastError();
+}
+
+template <int MQB>
+static hipError_t launch_mqb(const StreamArgs& a, int mode, bool i8, bool ch12, int n_wg, size_t lds, hipStream_t s) {
+  if (mode == 1) return launch_one<1, MQB>(a, n_wg, lds, s);
+  if (mode == 2) return launch_one<2, MQB>(a, n_wg, lds, s);
+  if (i8) return ch12 ? launch_one<0, MQB, true, 12>(a, n_wg, lds, s) : launch_one<0, MQB, true>(a, n_wg, lds, s);
+  return launch_one<0, MQB>(a, n_wg, lds, s);
+}
+
+hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s) {
+  const bool i8 = mode == 0 && a.i8;
+  // the filter's LDS candidate buffer when it fits next to the query image
+  StreamArgs b = a;
+  b.slots = mode == 0 && stream_lds_bytes(a.nqb, a.DPB, i8, true) <= (size_t)kStreamMaxLds && !getenv("CWQ_STREAM_NOBUF")
+                ? kStreamSlots
+                : 0;
+  const size_t lds = stream_lds_bytes(a.nqb, a.DPB, i8, b.slots > 0);
+  if (a.nq <= 0 || a.nqb * 16 < a.nq || a.nqb > SK_MAXQB || a.DPB % (i8 ? 64 : 32) || a.K < 1 || a.K > 64 ||
+      lds > (size_t)kStreamMaxLds || n_wg < 1 || (mode == 1 ? a.n_probe : a.nrows) < 1)
+    return hipErrorInvalidValue;
+  // int8 rows of a multiple of 12 fragments: 12-fragment chunks (their K padding, a whole
+  // number of chunks, is within stream_lds_bytes' 8-fragment padding)
+  const bool ch12 = i8 && (a.DPB / 64) % 12 == 0 && !getenv("CWQ_STREAM_CH8");
+  return a.nqb == 1 ? launch_mqb<1>(b, mode, i8, ch12, n_wg, lds, s)
+                    : launch_mqb<SK_MAXQB>(b, mode, i8, ch12, n_wg, lds, s);
 }
 
 // Tb[b][q] and Tlive[q] = ordered(-inf) for the filter's atomicMax (Tlive follows Tb)

@@ -256,6 +256,48 @@ def test_stream_path_equals_exact_scan(gpu, N, D, k, nq):
     assert st["fallback_queries"] == 0, st
 
 
+@pytest.mark.parametrize("N,D,nq", [(60000, 768, 1), (60000, 768, 16), (40000, 1536, 3), (30000, 200, 64),
+                                    (2000, 64, 5)])
+def test_stream_int8_pass_equals_bf16_pass(gpu, N, D, nq, monkeypatch):
+    """The stream filter's int8 pass (cwq_stream.hip I8: int8 rows and queries, exact int32
+    products, per-row / per-query scales; on by default) and its bf16 pass select different
+    candidate sets, never different answers: both bit-identical to the exact scan.  D = 200
+    and 64 leave a partial 8-fragment load chunk, D = 768 / 1536 take 12-fragment chunks."""
+    X = gpu.synth.synthetic_corpus(N, D, seed=N + D + 5)
+    ix = flat_index(gpu, X)
+    Q, _ = gpu.synth.synthetic_queries(X, nq, seed=nq + 2)
+    st = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("CWQ_STREAM_I8", v)
+        ids0, s0, ids1, s1, st[v] = both(ix, Q, 10)
+        assert st[v]["path"] == "stream" and st[v]["fallback_queries"] == 0, st[v]
+        assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    if N >= 30000:   # the int8 bounds are wider: more candidates (evidence the int8 pass ran)
+        assert st["1"]["candidates"] > st["0"]["candidates"], st
+
+
+@pytest.mark.parametrize("N", [4000, 20000])
+def test_stream_near_duplicate_rows(gpu, N, monkeypatch):
+    """Rows that nearly coincide: every row is a candidate.  N = 4000: the workgroups' LDS
+    candidate buffers (kStreamSlots per query) overflow into the global lists; N = 20000:
+    the query's list itself overflows and the exact fallback answers.  Still exact."""
+    D = 64
+    g = torch.Generator(device="cuda:0").manual_seed(N)
+    base = torch.randn(D, device="cuda:0", generator=g)
+    X = base + 1e-3 * torch.randn(N, D, device="cuda:0", generator=g)
+    ix = flat_index(gpu, X)
+    Q = X[:5] + 1e-4 * torch.randn(5, D, device="cuda:0", generator=g)
+    for v in ("0", "1"):
+        monkeypatch.setenv("CWQ_STREAM_I8", v)
+        ids0, s0, ids1, s1, st = both(ix, Q, 10)
+        assert st["path"] == "stream", st
+        assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+        if N == 20000:
+            assert st["fallback_queries"] == 5, st
+        else:
+            assert st["fallback_queries"] == 0 and st["candidates"] > 1000, st
+
+
 def test_stream_path_two_level_tree(gpu):
     """Stream filter on a hierarchical tree (per-row parent prefixes) and on a tree with
     anisotropic leaves (exact scan for those rows, merged with the stream candidates)."""
