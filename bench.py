@@ -160,12 +160,11 @@ def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
     """The reference harness's mode: one cobweb_predict_fast-sized call at a time with a
     host sync after each (benchmark_utils.py:801-805).  Median us per call; for the
     small-batch stream filter (cwq_stream.hip, nq <= 64) the HBM rate of its pass over
-    the row panel: bytes = isotropic rows x (2*DPB bf16 + 32 B row constants), divided by
-    the filter launch's HIP-event time, against the 8 TB/s HBM peak."""
+    the row panel: bytes = isotropic rows x (2*DPB bf16, or DPB for the int8 pass, + 32 B row
+    constants), divided by the filter launch's HIP-event time, against the 8 TB/s HBM peak."""
     NL, D = index.info["isotropic_rows"], index.dim
     DPB = max(128, -(-D // 64) * 64)                     # fgemm_dpb: whole 64-dim stage pairs
-    bytes_pass = NL * (2.0 * DPB + 32.0)
-    out = {"bytes_per_pass": bytes_pass}
+    out = {"bytes_per_pass_bf16": NL * (2.0 * DPB + 32.0), "bytes_per_pass_int8": NL * (1.0 * DPB + 32.0)}
     for nq in nqs:
         q = Q[:nq].contiguous()
         index.score_topk(q, k)
@@ -188,7 +187,8 @@ def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
         row = {"us_per_call": round(ts[len(ts) // 2] * 1e6, 1), "queries_per_s": round(nq / ts[len(ts) // 2], 1),
                "path": st["path"], "call_ms_events": round(med["call_ms"], 4)}
         if st["path"] == "stream":
-            gbs = bytes_pass / (med["fgemm_ms"] * 1e-3) / 1e9
+            row["pass"] = "int8" if st["int8_pass"] else "bf16"
+            gbs = out["bytes_per_pass_" + row["pass"]] / (med["fgemm_ms"] * 1e-3) / 1e9
             row.update({"stream_filter_ms": round(med["fgemm_ms"], 4), "probe_ms": round(med["sample_ms"], 4),
                         "rerank_ms": round(med["rerank_ms"], 4),
                         "hbm_roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,

@@ -189,7 +189,8 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  * filter (one HBM pass over the bf16 row panel; env CWQ_STREAM=0 disables it).
  * cwq_last_stats(out6): [queries served by the filter, of which re-run by the exact
  * scan (candidate list overflow / no threshold), filter used (0 exact scan, 1 batch
- * MFMA filter, 2 small-batch stream filter), mean candidate records per query, mean
+ * MFMA filter, 2 small-batch stream filter; + 256 when the stream filter's pass ran on
+ * the int8 row panel), mean candidate records per query, mean
  * exact reranks per query, threshold-sample rows].
  * After cwq_categorize, cwq_last_stats reports instead: [queries, queries re-run with
  * every leaf row materialised (DENSE), queries re-run after a filter list overflow,

@@ -1266,15 +1266,16 @@ bool use_stream(const cwq_index* ix, int64_t nq, int k) {
 // The stream filter's int8 row panel (half the bf16 panel's bytes per row; the per-call pass
 // is HBM-bound).  Built once, from the fp32 rerank copy, when the device has room for it.
 // Used when it pays: the pass saves ~half its HBM time, the wider int8 bounds cost the
-// exact rerank ~10x the reranks per query (one workgroup per query).  Measured at D = 768
-// (profiles/r03_i8_*): a win at 1M rows and nq = 1 (-75 us), a loss at 100k rows; so by
-// default for nq <= 16 and an int8 panel of >= kI8MinBytes.  CWQ_STREAM_I8=0 / 1: off /
-// forced on (read per call, for in-process A/Bs).
+// exact rerank ~9x the reranks per query (one workgroup per query).  Measured at D = 768
+// (profiles/r03_i8_*): 1M rows nq = 1 341 -> 271 us, nq = 64 385 -> 347 us; 100k rows
+// nq = 1 110 -> 126 us (a loss); so by default for an int8 panel of >= kI8MinBytes.
+// CWQ_STREAM_I8=0 / 1: off / forced on (read per call, for in-process A/Bs).
 constexpr int64_t kI8MinBytes = (int64_t)384 << 20;
 bool ensure_i8(cwq_index* ix, int64_t nq, hipStream_t s) {
   const char* e = getenv("CWQ_STREAM_I8");
   if (e && *e && atoi(e) == 0) return false;
-  if (!(e && *e && atoi(e) == 1) && (nq > 16 || (int64_t)ix->NL_iso * ix->DPB < kI8MinBytes)) return false;
+  (void)nq;
+  if (!(e && *e && atoi(e) == 1) && (int64_t)ix->NL_iso * ix->DPB < kI8MinBytes) return false;
   if (ix->i8_state) return ix->i8_state > 0;
   ix->i8_state = -1;
   if (ix->DPB % 64 || !ix->iso_Mf || !ix->iso_rf) return false;
@@ -1303,7 +1304,12 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                 (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
                 (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256 +
                 int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512;
-  const bool i8 = ensure_i8(ix, nq, s);
+  const bool ib = use_int_bounds(ix);
+  // int8 pass on flat trees only: with bounded internal prefixes the ~9x exact reranks pay
+  // the exact parent chains too (b4/L9 one query per call 692 -> 1166 us,
+  // profiles/r03_i8_ab_hier_*.log); CWQ_STREAM_I8=1 forces it
+  const char* e8 = getenv("CWQ_STREAM_I8");
+  const bool i8 = (!ib || (e8 && *e8 && atoi(e8) == 1)) && ensure_i8(ix, nq, s);
   int rc;
   if ((rc = ix->reserve(need))) return rc;
   Bump b(ix->ws, ix->ws_size);
@@ -1332,7 +1338,6 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
-  const bool ib = use_int_bounds(ix);
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
   // one fused prep launch when the exact internal pass is small (flat trees: the root)
   bool fused = !ib && ix->NI <= kSbMaxNI && (int)ix->levels.size() <= kSbMaxNI &&
@@ -1493,7 +1498,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   ix->ws_idle = true;   // synchronized above (rerun_exact synchronizes too): no end event
   ix->stats[0] = nq;
   ix->stats[1] = (int64_t)redo.size();
-  ix->stats[2] = 2;   // the stream filter
+  ix->stats[2] = 2 + (i8 ? 256 : 0);   // the stream filter (+256: its int8 pass)
   ix->stats[3] = (cand_sum + nq / 2) / nq;
   ix->stats[4] = (exact_sum + nq / 2) / nq;
   ix->stats[5] = a.n_probe * 16;

@@ -166,7 +166,8 @@ class CobwebIndex:
         out = np.zeros(6, np.int64)
         check(self._L.cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"filter_queries": int(out[0]), "fallback_queries": int(out[1]), "filter_used": bool(out[2]),
-                "path": {0: "scan", 1: "fgemm", 2: "stream"}.get(int(out[2]), "?"),
+                "path": {0: "scan", 1: "fgemm", 2: "stream"}.get(int(out[2]) & 255, "?"),
+                "int8_pass": bool(int(out[2]) & 256),
                 "candidates": int(out[3]), "exact_reranks": int(out[4]), "sample_rows": int(out[5])}
 
     def last_categorize_stats(self):

@@ -272,7 +272,8 @@ def test_stream_int8_pass_equals_bf16_pass(gpu, N, D, nq, monkeypatch):
         ids0, s0, ids1, s1, st[v] = both(ix, Q, 10)
         assert st[v]["path"] == "stream" and st[v]["fallback_queries"] == 0, st[v]
         assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
-    if N >= 30000:   # the int8 bounds are wider: more candidates (evidence the int8 pass ran)
+    assert st["1"]["int8_pass"] and not st["0"]["int8_pass"], st
+    if N >= 30000:   # the int8 bounds are wider: more candidates
         assert st["1"]["candidates"] > st["0"]["candidates"], st
 
 
@@ -298,9 +299,12 @@ def test_stream_near_duplicate_rows(gpu, N, monkeypatch):
             assert st["fallback_queries"] == 0 and st["candidates"] > 1000, st
 
 
-def test_stream_path_two_level_tree(gpu):
+@pytest.mark.parametrize("i8", ["0", "1"])
+def test_stream_path_two_level_tree(gpu, i8, monkeypatch):
     """Stream filter on a hierarchical tree (per-row parent prefixes) and on a tree with
-    anisotropic leaves (exact scan for those rows, merged with the stream candidates)."""
+    anisotropic leaves (exact scan for those rows, merged with the stream candidates);
+    bf16 and int8 filter passes."""
+    monkeypatch.setenv("CWQ_STREAM_I8", i8)
     N, D = 50000, 128
     X = gpu.synth.synthetic_corpus(N, D, seed=77)
     labels = torch.randint(0, 500, (N,), device="cuda:0", generator=torch.Generator(device="cuda:0").manual_seed(1))
