@@ -344,6 +344,30 @@ __device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, floa
   }
 }
 
+// Bitonic sort of one value per lane into a list64 list: descending by key, ascending row
+// on equal keys (the list order list64_insert keeps), an aux value carried along.  21
+// exchange steps instead of up to 64 serial inserts when a list is filled from empty.
+template <bool AUX>
+__device__ __forceinline__ void wave_sort64(float& k, int& r, float& a, int lane) {
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int st = size >> 1; st > 0; st >>= 1) {
+      const float pk = __shfl_xor(k, st, 64);
+      const int pr = __shfl_xor(r, st, 64);
+      const float pa = AUX ? __shfl_xor(a, st, 64) : 0.f;
+      const bool hold_better = ((lane & st) == 0) == ((lane & size) == 0);
+      const bool pbet = pk > k || (pk == k && pr < r);
+      const bool obet = k > pk || (k == pk && r < pr);
+      if (hold_better ? pbet : obet) {
+        k = pk;
+        r = pr;
+        if (AUX) a = pa;
+      }
+    }
+  }
+}
+
 // list64_insert with an aux value carried along (final_wide_kernel's (key, lp, row) lists)
 __device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr, int lane, float ck, float ca, int cr,
                                                   int K) {

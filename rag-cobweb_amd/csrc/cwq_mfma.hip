@@ -2076,19 +2076,35 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   if (ok) {
     // T2 = K-th largest l: every wave keeps the top-K of its slice, wave 0 merges the lists
     {
-      float tk = (d && wave == 0) ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
-      int tr = (d && wave == 0) ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
+      const bool pre = d && wave == 0;   // wave 0 continues the list of the first d candidates
+      float tk = pre ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
+      int tr = pre ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
       for (int j0 = d + wave * 64; j0 < n; j0 += kFwThreads) {
         const int j = j0 + lane;
         const float lv = j >= n ? -CWQ_INF : j < kFwCand ? s_wl[j] : cl[base + j];
-        list64_offer(tk, tr, lane, lv, j, K);
+        if (j0 == d + wave * 64 && !pre) {   // empty list: sort the first 64 (-inf never enters)
+          tk = lv;
+          tr = lv == -CWQ_INF ? 0x7fffffff : j;
+          float dummy = 0.f;
+          wave_sort64<false>(tk, tr, dummy, lane);
+        } else {
+          list64_offer(tk, tr, lane, lv, j, K);
+        }
       }
       s_ml[tid] = lane < K ? tk : -CWQ_INF;
-      s_mr[tid] = lane < K ? tr : 0x7fffffff;
       __syncthreads();
-      if (wave == 0) {
-        for (int w = 1; w < kFwThreads / 64; ++w) list64_offer(tk, tr, lane, s_ml[w * 64 + lane], s_mr[w * 64 + lane], K);
-        if (lane == 0) s_T2 = rl_f2(tk, K - 1);
+      // T2 = the K-th largest of the 8 lists' K entries: entry v is it when fewer than K
+      // entries exceed it and at least K reach it (all such entries are equal)
+      if (lane < K) {
+        const float v = s_ml[tid];
+        int cg = 0, cge = 0;
+        for (int w = 0; w < kFwThreads / 64; ++w)
+          for (int i = 0; i < K; ++i) {
+            const float u = s_ml[w * 64 + i];
+            cg += u > v;
+            cge += u >= v;
+          }
+        if (cg < K && cge >= K) s_T2 = v;
       }
       __syncthreads();
     }
@@ -2191,10 +2207,18 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           rid = seg_base + rr;
           ++nx;
         }
-        // only keys that beat the list's K-th entry can enter (insertions are serial)
+        // only keys that beat the list's K-th entry can enter (insertions are serial); the
+        // wave's first round fills its empty list by a sort
+        if (r0 == 0 && !nopf) {
+          lk = key;
+          la = lp;
+          lr = rid;
+          wave_sort64<true>(lk, lr, la, lane);
+        }
         const float tk = rl_f2(lk, K - 1);
         const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-        uint64_t mask = __ballot(act && (nopf || key > tk || (key == tk && rid < tr)));
+        uint64_t mask = __ballot(act && r0 != 0 && (nopf || key > tk || (key == tk && rid < tr)));
+        if (nopf && r0 == 0) mask = __ballot(act);
         while (mask) {
           const int b = __builtin_ctzll(mask);
           mask &= mask - 1;
