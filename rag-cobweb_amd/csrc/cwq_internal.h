@@ -427,7 +427,14 @@ __device__ __forceinline__ void select_wave(const float* __restrict__ uq, int nr
         const int r = r0 + t * 256 + lane * 4 + c;
         m = fmaxf(m, r < nrows ? vv[c] : -__builtin_inff());
         if (((t * 4 + c + 1) & (g - 1)) == 0) {
-          list64_offer(lk, lr, lane, m, r, Kp);
+          if (r0 == 0 && t * 4 + c + 1 == g) {   // the empty list: sort the first maxima
+            lk = m;
+            lr = m == -__builtin_inff() ? 0x7fffffff : r;
+            float dummy = 0.f;
+            wave_sort64<false>(lk, lr, dummy, lane);
+          } else {
+            list64_offer(lk, lr, lane, m, r, Kp);
+          }
           m = -__builtin_inff();
         }
       }
