@@ -197,6 +197,40 @@ def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
     return out
 
 
+class _Names:
+    """Sentence strings "s<i>" of the synthetic corpus, made on demand (no 1M-10M list)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return f"s{i}"
+
+
+def per_call_harness(pkg, index, Q, k, reps=200):
+    """The reference harness's own timed call (benchmark_utils.py:576-579, 801-805):
+    `latency = time.time()` around `cobweb.cobweb_predict_fast(query_emb, k)` with a numpy
+    query and sentence strings out -- the drop-in CobwebWrapper over this index, so the
+    host->device copy of the query, the result sync and the id -> sentence mapping
+    (wrapper.cobweb_predict_indexed) are inside the time."""
+    w = pkg.CobwebWrapper.from_index(index, _Names(index.n_sent))
+    Qh = Q[:reps].cpu().numpy()
+    w.cobweb_predict_fast(Qh[0], k)
+    ts = []
+    for i in range(reps):
+        t = time.perf_counter()
+        w.cobweb_predict_fast(Qh[i], k)
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    return {"call": "CobwebWrapper.cobweb_predict_fast(numpy_query, k) -> list of sentences",
+            "queries": reps, "us_per_call_median": round(ts[reps // 2] * 1e6, 1),
+            "us_per_call_p10": round(ts[reps // 10] * 1e6, 1), "us_per_call_mean": round(float(np.mean(ts)) * 1e6, 1),
+            "queries_per_s": round(reps / float(np.sum(ts)), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -357,8 +391,9 @@ def main():
            "peak_sampled": max(used_create, used_freed, used_steady),
            "device_total": torch.cuda.mem_get_info(dev)[1],
            "note": "device-wide used bytes (mem_get_info) on this rank, sampled after index create (caller's "
-                   "mean still resident), after the caller's copies are freed, and after the timed steps "
-                   "(index + the handle's workspace)"}
+                   "mean still resident; the per-call int8 panel is built with the index), after the caller's "
+                   "copies are freed, after the timed steps (index + the handle's workspace) and after the per-call "
+                   "legs"}
 
     rec_l2 = rec_ip = rec_tgt = None
     if gt is not None:
@@ -368,6 +403,10 @@ def main():
     pc = None
     if rank == 0 and not args.no_per_call:
         pc = per_call(index, Ql, k)
+        pc["harness_call_nq1"] = per_call_harness(pkg, index, Ql, k)
+        torch.cuda.empty_cache()
+        mem["device_used_after_per_call"] = dev_used()
+        mem["peak_sampled"] = max(mem["peak_sampled"], mem["device_used_after_per_call"])
 
     base = None
     if Xh is not None:

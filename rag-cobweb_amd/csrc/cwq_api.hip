@@ -157,7 +157,6 @@ struct cwq_index {
   size_t ws_budget = 0;   // query-chunk workspace budget, from the free memory at the first call
   hipEvent_t ws_ev = nullptr;
   bool ws_ev_live = false;
-  hipStream_t ws_ev_stream = nullptr;   // the stream ws_ev was last recorded on
   bool ws_idle = false;   // set by a call that ends with its stream synchronized: no event needed
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
   size_t hflags_n = 0;
@@ -211,9 +210,10 @@ struct cwq_index {
   int ws_begin(hipStream_t s) {
     if (!ws_ev && hipEventCreateWithFlags(&ws_ev, hipEventDisableTiming) != hipSuccess)
       return fail(CWQ_ERR_HIP, "hipEventCreate failed");
-    // a call on the stream of the previous one is ordered after it already (no barrier
-    // packet on the per-call path)
-    if (ws_ev_live && s != ws_ev_stream && hipStreamWaitEvent(s, ws_ev, 0) != hipSuccess)
+    // always wait, also on the previous call's stream handle: a destroyed stream's handle
+    // can come back as a new stream.  The per-call path ends synchronized (ws_idle), so
+    // it leaves no live event and queues no barrier packet here.
+    if (ws_ev_live && hipStreamWaitEvent(s, ws_ev, 0) != hipSuccess)
       return fail(CWQ_ERR_HIP, "hipStreamWaitEvent failed");
     return CWQ_OK;
   }
@@ -232,7 +232,6 @@ struct cwq_index {
       return fail(CWQ_ERR_HIP, "hipEventRecord failed");
     }
     ws_ev_live = true;
-    ws_ev_stream = s;
     return CWQ_OK;
   }
   ~cwq_index() {
@@ -451,6 +450,9 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
 namespace {
 // cwq_index_create / cwq_index_create_cv: `var` is either the full [n_nodes][D] array or
 // the compact per-node form (VarSrc); both give the same index.
+bool use_int_bounds(const cwq_index* ix);
+bool ensure_i8(cwq_index* ix, hipStream_t s);
+
 int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mean, const VarSrc& var,
                       const int64_t* parent, const int64_t* node_of_sentence, int64_t n_sent, const double* level_w,
                       int32_t n_w, hipStream_t s, cwq_index** out) {
@@ -704,6 +706,10 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
     ix->int_bounds = true;
   }
   if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
+  // the per-call path's int8 row panel is built here, with the index, when its policy
+  // holds (flat trees, >= kI8MinBytes of int8 rows, room on the device): no allocation or
+  // first-call latency inside a query
+  if (ix->NL_iso > 0 && !use_int_bounds(ix.get())) (void)ensure_i8(ix.get(), s);
   HIPCHK(hipStreamSynchronize(s));
   *out = ix.release();
   return CWQ_OK;
@@ -1269,12 +1275,13 @@ bool use_stream(const cwq_index* ix, int64_t nq, int k) {
 // exact rerank ~9x the reranks per query (one workgroup per query).  Measured at D = 768
 // (profiles/r03_i8_*): 1M rows nq = 1 341 -> 271 us, nq = 64 385 -> 347 us; 100k rows
 // nq = 1 110 -> 126 us (a loss); so by default for an int8 panel of >= kI8MinBytes.
-// CWQ_STREAM_I8=0 / 1: off / forced on (read per call, for in-process A/Bs).
+// CWQ_STREAM_I8=0 / 1: off / forced on (read per call, for in-process A/Bs).  The panel
+// is built by cwq_index_create when the policy holds there; a call that forces it on an
+// index created without it builds it then (A/B and test use only).
 constexpr int64_t kI8MinBytes = (int64_t)384 << 20;
-bool ensure_i8(cwq_index* ix, int64_t nq, hipStream_t s) {
+bool ensure_i8(cwq_index* ix, hipStream_t s) {
   const char* e = getenv("CWQ_STREAM_I8");
   if (e && *e && atoi(e) == 0) return false;
-  (void)nq;
   if (!(e && *e && atoi(e) == 1) && (int64_t)ix->NL_iso * ix->DPB < kI8MinBytes) return false;
   if (ix->i8_state) return ix->i8_state > 0;
   ix->i8_state = -1;
@@ -1309,7 +1316,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   // the exact parent chains too (b4/L9 one query per call 692 -> 1166 us,
   // profiles/r03_i8_ab_hier_*.log); CWQ_STREAM_I8=1 forces it
   const char* e8 = getenv("CWQ_STREAM_I8");
-  const bool i8 = (!ib || (e8 && *e8 && atoi(e8) == 1)) && ensure_i8(ix, nq, s);
+  const bool i8 = (!ib || (e8 && *e8 && atoi(e8) == 1)) && ensure_i8(ix, s);
   int rc;
   if ((rc = ix->reserve(need))) return rc;
   Bump b(ix->ws, ix->ws_size);

@@ -2083,8 +2083,8 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         const int j = j0 + lane;
         const float lv = j >= n ? -CWQ_INF : j < kFwCand ? s_wl[j] : cl[base + j];
         if (j0 == d + wave * 64 && !pre) {   // empty list: sort the first 64 (-inf never enters)
-          tk = lv;
-          tr = lv == -CWQ_INF ? 0x7fffffff : j;
+          tk = lv == lv ? lv : -CWQ_INF;      // a NaN bound never enters (as list64_offer)
+          tr = tk == -CWQ_INF ? 0x7fffffff : j;
           float dummy = 0.f;
           wave_sort64<false>(tk, tr, dummy, lane);
         } else {
@@ -2092,6 +2092,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         }
       }
       s_ml[tid] = lane < K ? tk : -CWQ_INF;
+      if (tid == 0) s_T2 = -CWQ_INF;   // defined even if no entry qualifies below
       __syncthreads();
       // T2 = the K-th largest of the 8 lists' K entries: entry v is it when fewer than K
       // entries exceed it and at least K reach it (all such entries are equal)
@@ -2210,9 +2211,9 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         // only keys that beat the list's K-th entry can enter (insertions are serial); the
         // wave's first round fills its empty list by a sort
         if (r0 == 0 && !nopf) {
-          lk = key;
+          lk = key == key ? key : -CWQ_INF;   // a NaN key never enters (as the insertions)
           la = lp;
-          lr = rid;
+          lr = lk == -CWQ_INF ? 0x7fffffff : rid;
           wave_sort64<true>(lk, lr, la, lane);
         }
         const float tk = rl_f2(lk, K - 1);

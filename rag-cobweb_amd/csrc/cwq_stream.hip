@@ -273,8 +273,11 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         if (qb >= nqb) break;
         if (!rok || !qok[qb]) continue;
         float u, l;
-        // int8: acc is exact; the two fp32 roundings of acc * (s_x * s_r) are within
-        // 2^-22 |dot| (2^-21 taken), and beta has no accumulation term
+        // int8: the int32 acc is exact (|acc| <= 127^2 * DPB); up to three fp32 roundings
+        // follow -- int32 -> fp32 (exact while |acc| < 2^24, i.e. DPB <= 1040; the D = 1536
+        // panels round here), s_x * s_r, and the product -- each within 2^-24 relative, so
+        // |err| <= (3 * 2^-24 + O(2^-48)) |dot| < 2^-22 |dot|; 2^-21 is taken, and beta has
+        // no accumulation term
         const float dot = I8 ? (float)acc[qb][j] * (qi[qb].w * rf[j].R0) : (float)acc[qb][j];
         fg_bounds2(dot, (I8 ? 0x1p-21f : 0x1p-23f) * fabsf(dot), qi[qb], rf[j], cPh[qb] * rf[j].invL,
                    cP[qb] * rf[j].invL, a.eps_n, a.slack, u, l);

@@ -19,6 +19,7 @@ module in the same order as the reference, so a run seeded like the reference ma
 the same tie-breaks.  Counts are kept on the host as well (exact small integers).
 """
 import ctypes
+import os
 import random as _random_mod
 
 import numpy as np
@@ -322,9 +323,32 @@ class DeviceTreeFitter:
         m2 = np.ascontiguousarray(np.stack([np.asarray(n.meanSq, F32) for n in nodes]))
         return nodes, parent, cptr, np.asarray(cidx if cidx else [0], np.int32), count, mean, m2
 
+    def _pool_cap(self, n_nodes, remaining):
+        """Node slots for one load: the existing nodes plus ~3 per remaining row (merges
+        and fringe splits add nodes), capped by a device-memory budget -- the kernel
+        stops for room (ROOM) and the host reloads into a fresh pool, so a cap only costs
+        reloads.  Budget: CWQ_FIT_POOL_MB, else 40% of the free device memory;
+        CWQ_FIT_POOL_SLOTS caps the slots beyond the loaded nodes (tests force reloads)."""
+        want = n_nodes + 3 * remaining + 1024
+        per_slot = 8 * self.D + 128          # mean + meanSq + links, arena, scratch (cwq_fitdev.hip)
+        mb = os.environ.get("CWQ_FIT_POOL_MB")
+        if mb:
+            budget = int(mb) << 20
+        else:
+            free, _ = torch.cuda.mem_get_info(self.dev)
+            budget = int(0.4 * free)
+        cap = min(want, max(budget // per_slot, n_nodes + 1024))
+        extra = os.environ.get("CWQ_FIT_POOL_SLOTS")
+        if extra:
+            cap = min(cap, n_nodes + max(int(extra), 80))
+        return int(min(cap, 2 ** 31 - 1))
+
     def fit_batch(self, X):
         """Insert the rows of X in order; returns the node each row ended in (ifit's
-        return value, CobwebTorchTree.py:123-141), as host Node objects."""
+        return value, CobwebTorchTree.py:123-141), as host Node objects.  If the device
+        pool cannot be allocated or runs out mid-insert, the remaining rows go through
+        the host-driven TreeFitter from the last exported tree and random() state (the
+        same tree either way)."""
         import time
         L = lib()
         X = torch.as_tensor(X if torch.is_tensor(X) else np.asarray(X, F32), dtype=torch.float32)
@@ -337,25 +361,33 @@ class DeviceTreeFitter:
         info = np.zeros(4, np.int64)
         sp = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
         out = [None] * n
-        done, t_kernel, draws, loads = 0, 0.0, 0, 0
+        done, t_kernel, draws, loads, fallback = 0, 0.0, 0, 0, None
 
-        def chk(rc):
-            if rc:
-                raise RuntimeError(f"libcwq device fit: {L.cwq_fit_last_error().decode()}")
+        def hand_back():   # the advanced random() state: the reference's draws, in its order
+            old = self.rng.getstate()
+            self.rng.setstate((old[0], tuple(int(v) for v in mt), old[2]))
 
         while done < n:
             nodes, parent, cptr, cidx, count, mean, m2 = self._flatten()
-            cap = int(len(nodes) + 3 * (n - done) + 1024)
+            cap = self._pool_cap(len(nodes), n - done)
             h = ctypes.c_void_p()
             with torch.cuda.device(self.dev):
-                chk(L.cwq_fit_create(self.dev.index, self.D, float(self.tree.prior_var), cap, ctypes.byref(h)))
+                if L.cwq_fit_create(self.dev.index, self.D, float(self.tree.prior_var), cap, ctypes.byref(h)):
+                    fallback = L.cwq_fit_last_error().decode()
+                    break
                 try:
-                    chk(L.cwq_fit_load(h, len(nodes), 0, _np_ptr(parent), _np_ptr(cptr), _np_ptr(cidx),
-                                       _np_ptr(count), _np_ptr(mean), _np_ptr(m2), _np_ptr(mt), sp))
+                    if L.cwq_fit_load(h, len(nodes), 0, _np_ptr(parent), _np_ptr(cptr), _np_ptr(cidx),
+                                      _np_ptr(count), _np_ptr(mean), _np_ptr(m2), _np_ptr(mt), sp):
+                        fallback = L.cwq_fit_last_error().decode()
+                        break
                     loads += 1
                     t0 = time.perf_counter()
-                    chk(L.cwq_fit_insert(h, ctypes.c_void_p(X[done:].data_ptr()), n - done,
-                                         ctypes.c_void_p(leaf[done:].data_ptr()), _np_ptr(info), sp))
+                    if L.cwq_fit_insert(h, ctypes.c_void_p(X[done:].data_ptr()), n - done,
+                                        ctypes.c_void_p(leaf[done:].data_ptr()), _np_ptr(info), sp):
+                        # e.g. the pool ran out inside one insert: the device tree is
+                        # mid-operation, so nothing of this load is kept
+                        fallback = L.cwq_fit_last_error().decode()
+                        break
                     t_kernel += time.perf_counter() - t0
                     used = int(info[3])
                     out2 = np.zeros(2, np.int32)
@@ -365,10 +397,14 @@ class DeviceTreeFitter:
                     CNT = np.zeros(used, F32)
                     MEAN = np.zeros((used, self.D), F32)
                     M2 = np.zeros((used, self.D), F32)
-                    chk(L.cwq_fit_export(h, _np_ptr(out2), _np_ptr(P), _np_ptr(CP), _np_ptr(CI), _np_ptr(CNT),
-                                         _np_ptr(MEAN), _np_ptr(M2), _np_ptr(mt), sp))
+                    mt_new = mt.copy()
+                    if L.cwq_fit_export(h, _np_ptr(out2), _np_ptr(P), _np_ptr(CP), _np_ptr(CI), _np_ptr(CNT),
+                                        _np_ptr(MEAN), _np_ptr(M2), _np_ptr(mt_new), sp):
+                        fallback = L.cwq_fit_last_error().decode()
+                        break
                 finally:
                     L.cwq_fit_destroy(h)
+            mt = mt_new
             objs = self._rebuild(nodes, out2, P, CP, CI, CNT, MEAN, M2)
             k = int(info[0])
             draws += int(info[1])
@@ -382,10 +418,15 @@ class DeviceTreeFitter:
                 if done != n:
                     raise RuntimeError(f"device fit stopped after {done} of {n} rows (status {int(info[2])})")
                 break
-        # hand the advanced random() state back: the reference's draws, in its order
-        old = self.rng.getstate()
-        self.rng.setstate((old[0], tuple(int(v) for v in mt), old[2]))
-        self.stats = {"rows": n, "kernel_s": round(t_kernel, 4), "random_draws": draws, "loads": loads}
+        hand_back()
+        if fallback is not None:
+            # the host tree and `mt` are the last export's: continue there on the host
+            fitter = TreeFitter(self.tree, device=self.dev, rng=self.rng)
+            for i in range(done, n):
+                out[i] = fitter.ifit(X[i].cpu().numpy())
+            fitter.sync_to_host()
+        self.stats = {"rows": n, "kernel_s": round(t_kernel, 4), "random_draws": draws, "loads": loads,
+                      "host_rows": n - done, "fallback": fallback}
         return out
 
     def _rebuild(self, nodes, out2, P, CP, CI, CNT, MEAN, M2):

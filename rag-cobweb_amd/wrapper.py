@@ -10,8 +10,10 @@ src/utils/benchmark_utils.py:576-581 (`retrieve_cobweb_basic`) runs unchanged:
 Differences (documented in DESIGN.md §6):
   * scoring runs on the GPU through libcwq; there is no CPU path;
   * exact score ties are broken deterministically (lower node / sentence id)
-    instead of by randn*1e-6 noise (CobwebWrapper.py:246-256) or random.shuffle
-    (:456);
+    instead of by randn*1e-6 noise (CobwebWrapper.py:246-256) or the heap's random()
+    key (CobwebTorchTree.py:243,285); the global random() stream is still advanced by
+    the draws the reference makes and the retrieved leaves' lists are shuffled with it
+    (CobwebWrapper.py:456), so add -> Basic query -> add builds the reference's tree;
   * `cobweb_rank_scores` returns a tensor without autograd history (training
     through the scores, src/training/cobweb_query_train.py, is out of scope);
   * batched entry points `cobweb_predict_batch` / `cobweb_categorize_batch` take a
@@ -19,8 +21,8 @@ Differences (documented in DESIGN.md §6):
 """
 import json
 import math
-
 import os
+import random
 
 import numpy as np
 import torch
@@ -29,6 +31,13 @@ from .index import CobwebIndex
 from .tree import CobwebTree
 
 MAX_INIT_SEARCH = 100000   # CobwebWrapper.py:24
+
+
+def advance_random(n, rng=random):
+    """Advance `rng` (the global `random` module by default) past `n` random() draws:
+    random() takes two 32-bit MT19937 outputs and getrandbits(64*n) takes exactly 2*n."""
+    if n > 0:
+        rng.getrandbits(64 * n)
 
 
 class CobwebWrapper:
@@ -241,7 +250,7 @@ class CobwebWrapper:
         """CobwebWrapper.py:210-265 ("Cobweb Fast")."""
         self.build_prediction_index()
         x = self._embed(input, is_embedding)
-        n = len(self._leaf_to_path_indices)
+        n = self._index.n_sent if self._leaf_to_path_indices is None else len(self._leaf_to_path_indices)
         if n == 0:
             return []
         ids, _ = self._index.score_topk(x[None, :], min(k, n))
@@ -269,12 +278,19 @@ class CobwebWrapper:
         nodes with sentences are retrieved (CobwebTorchTree.py:289)."""
         self.build_prediction_index()
         x = self._embed(input, is_embedding)
-        nodes, found, _ = self._index.categorize(x[None, :], k, self.max_init_search)
-        if int(found[0]) < k:
+        nodes, found, calls = self._index.categorize(x[None, :], k, self.max_init_search)
+        nf = int(found[0])
+        # the reference's search draws one random() per heap push (one per log_prob call)
+        # and one per retrieval (CobwebTorchTree.py:243,268,285) from the global stream
+        # that ifit also draws from; advance it by as many, before the IndexError too
+        advance_random(int(calls[0]) + nf)
+        if nf < k:
             raise IndexError("list index out of range")
         results = []
         for nid in nodes[0].tolist():
-            for sid in sorted(self._nodes[nid].sentence_id or []):
+            sid_lst = self._nodes[nid].sentence_id
+            random.shuffle(sid_lst)      # CobwebWrapper.py:456, mutating the leaf's list
+            for sid in sid_lst:
                 if sid is None or sid >= len(self.sentences):
                     continue
                 results.append(sid if return_ids else self.sentences[sid])
@@ -353,6 +369,17 @@ class CobwebWrapper:
             for s in n.sentence_id or []:
                 w.sentence_to_node[s] = n
             stack.extend(n.children)
+        return w
+
+    @classmethod
+    def from_index(cls, index, sentences, encode_func=lambda x: x):
+        """A query-only wrapper over a prebuilt CobwebIndex (e.g. a flat-synth tree at C3/C4
+        scale, where the host keeps no node objects): the Fast / rank-score / batch entry
+        points work; the add path and Basic's id expansion need the node tree."""
+        w = cls(device=index.device, encode_func=encode_func)
+        w.sentences = sentences          # any sequence (len + indexing); not copied
+        w._index = index
+        w._prediction_index_valid = True
         return w
 
     def __len__(self):

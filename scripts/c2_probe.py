@@ -1,0 +1,139 @@
+"""Config C2 (100k x 768, 1k queries, one MI355X) end to end on a tree built by the
+drop-in's own device ifit -- the reference's workflow: CobwebWrapper(corpus, embeddings)
+(CobwebWrapper.py:13-80) -> build_prediction_index -> queries (benchmark_utils.py:576-581,
+801-805).  Same corpus as tests/test_gpu_c2.py (100 Gaussian clusters).  Reports:
+  ifit seconds and tree shape; index build seconds;
+  Fast batch q/s (filter and exact scan), phases;
+  Fast one query per call: score_topk on a device tensor, and the harness's own call
+  cobweb_predict_fast(numpy_query, k) (H2D copy, sync, id -> sentence mapping);
+  Basic batch q/s with found-k and how the queries resolved; Basic one query per call.
+GPU only.   python scripts/c2_probe.py [--n 100000]
+"""
+import argparse
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cobweb_pkg  # noqa: E402
+
+
+def corpus(n, d, nc, nq, seed=2):
+    rng = np.random.default_rng(seed)
+    C = rng.standard_normal((nc, d)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, nc, n)] + 0.3 * rng.standard_normal((n, d))).astype(np.float32)
+    pick = rng.choice(n, nq // 2, replace=False)
+    Qp = X[pick] + 0.1 * rng.standard_normal((nq // 2, d))
+    Qf = C[rng.integers(0, nc, nq - nq // 2)] + 0.3 * rng.standard_normal((nq - nq // 2, d))
+    return X, np.concatenate([Qp, Qf]).astype(np.float32), pick
+
+
+def med(f, reps):
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--clusters", type=int, default=100)
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--calls", type=int, default=300, help="one-query calls timed per leg")
+    args = ap.parse_args()
+    pkg = cobweb_pkg.load()
+    X, Qn, pick = corpus(args.n, args.dim, args.clusters, args.nq)
+    random.seed(2)
+    w0 = pkg.CobwebWrapper(corpus=None, corpus_embeddings=X[:8])   # warm up libcwq
+    w0.build_prediction_index()
+    torch.cuda.synchronize()
+    random.seed(2)
+    t0 = time.perf_counter()
+    w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(args.n)], corpus_embeddings=X)
+    torch.cuda.synchronize()
+    t_fit = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    w.build_prediction_index()
+    torch.cuda.synchronize()
+    t_ix = time.perf_counter() - t0
+    ix = w._index
+    inf = ix.info
+    root_c = len(w.tree.root.children)
+    print(f"C2 corpus {args.n}x{args.dim} ({args.clusters} clusters): device ifit {t_fit:.2f} s "
+          f"({args.n / t_fit:.0f} inserts/s); tree {inf['n_nodes']} nodes, {inf['internal_nodes']} internal, "
+          f"max depth {inf['max_depth']}, root children {root_c}; index build {t_ix:.2f} s "
+          f"({inf['device_bytes'] / 1e9:.2f} GB)", flush=True)
+    Q = torch.from_numpy(Qn).cuda()
+    k = args.k
+    # Fast batch
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, k)
+    t_scan = med(lambda: ix.score_topk(Q, k), 5)
+    ix.set_filter(-1)
+    ids1, s1 = ix.score_topk(Q, k)
+    same = torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    ix.set_timing(True)
+    t_f = med(lambda: ix.score_topk(Q, k), 11)
+    tm = ix.last_timing()
+    ix.set_timing(False)
+    st = ix.last_stats()
+    top1 = float((ids1[:len(pick), 0].cpu().numpy() == pick).mean())
+    print(f"Fast batch nq={args.nq}: filter {t_f * 1e3:.3f} ms = {args.nq / t_f:.0f} q/s (exact scan "
+          f"{t_scan * 1e3:.3f} ms = {args.nq / t_scan:.0f} q/s); ids/scores == exact scan: {same}; "
+          f"candidates/query {st['candidates']}, exact reranks {st['exact_reranks']}; "
+          f"perturbed passage ranked first {top1:.3f}", flush=True)
+    print(f"  last call phases (HIP events, ms): " + ", ".join(f"{a} {b:.3f}" for a, b in tm.items()), flush=True)
+    # one query per call
+    for nq in (1, 8, 64):
+        qs = [Q[i:i + nq].contiguous() for i in range(0, min(args.nq, args.calls * nq), nq)][:args.calls]
+        ok = all(torch.equal(ix.score_topk(q, k)[0], ids0[i * nq:i * nq + nq]) for i, q in enumerate(qs[:20]))
+        ts = []
+        for q in qs:
+            t0 = time.perf_counter()
+            ix.score_topk(q, k)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        st = ix.last_stats()
+        print(f"Fast per call nq={nq} (score_topk, device tensor): median {ts[len(ts) // 2] * 1e6:.1f} us, "
+              f"p10 {ts[len(ts) // 10] * 1e6:.1f} us; path {st['path']} int8 {st['int8_pass']}; "
+              f"== exact {ok}", flush=True)
+    ts = []
+    for i in range(args.calls):
+        t0 = time.perf_counter()
+        w.cobweb_predict_fast(Qn[i % args.nq], k)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    print(f"Fast per call, the harness's cobweb_predict_fast(numpy, {k}) -> sentences: median "
+          f"{ts[len(ts) // 2] * 1e6:.1f} us, p10 {ts[len(ts) // 10] * 1e6:.1f} us", flush=True)
+    # Basic
+    nodes, found, calls = ix.categorize(Q, k, w.max_init_search)
+    t_b = med(lambda: ix.categorize(Q, k, w.max_init_search), 5)
+    cst = ix.last_categorize_stats()
+    print(f"Basic batch nq={args.nq}: {t_b * 1e3:.3f} ms = {args.nq / t_b:.0f} q/s; found-k "
+          f"{float((found == k).float().mean()):.3f}; log_prob calls/query mean {float(calls.float().mean()):.0f}; "
+          f"resolved {cst}", flush=True)
+    ts = []
+    for i in range(min(args.calls, 200)):
+        t0 = time.perf_counter()
+        w.cobweb_predict(Qn[i % args.nq], k)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    print(f"Basic per call cobweb_predict(numpy, {k}): median {ts[len(ts) // 2] * 1e6:.1f} us", flush=True)
+    print("done", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -98,13 +98,15 @@ def count_log_prob_calls():
     return orig, wrapped, box
 
 
-def query_outputs(w, Xq, pos, cat=True, k=K, tag=""):
-    """All reference outputs for a batch of query embeddings."""
+def query_outputs(w, Xq, pos, cat=True, k=K, tag="", n_dense=None):
+    """All reference outputs for a batch of query embeddings (the dense per-node /
+    per-sentence score arrays only for the first `n_dense` queries when given)."""
     res = {}
     with _Quiet():
         w.build_prediction_index()
-    res["node_lp"] = ref_node_lp(w, Xq)
-    res["rank_scores"] = np.stack([w.cobweb_rank_scores(x).detach().numpy() for x in Xq]).astype(np.float32)
+    Xd = Xq if n_dense is None else Xq[:n_dense]
+    res["node_lp"] = ref_node_lp(w, Xd)
+    res["rank_scores"] = np.stack([w.cobweb_rank_scores(x).detach().numpy() for x in Xd]).astype(np.float32)
     torch.manual_seed(1234)
     res["fast_ids"] = np.array([w.cobweb_predict_fast(x, k, return_ids=True) for x in Xq], np.int64)
     if cat:
@@ -154,11 +156,11 @@ def build_by_ifit(X, seed):
     return w, time.time() - t
 
 
-def case_ifit(name, X, Xq, pick, extra=None, cat=True, json_dump=False, weights_cases=False):
+def case_ifit(name, X, Xq, pick, extra=None, cat=True, json_dump=False, weights_cases=False, n_dense=None):
     w, secs = build_by_ifit(X, 0)
     nodes, pos, tree = export_tree(w.tree.root, len(X))
     print(f"[{name}] ifit N={len(X)} D={X.shape[1]} nodes={len(nodes)} in {secs:.1f}s", flush=True)
-    res = query_outputs(w, Xq, pos, cat=cat)
+    res = query_outputs(w, Xq, pos, cat=cat, n_dense=n_dense)
     data = dict(X=X, Xq=Xq, pick=pick, prior_var=np.float32(w.tree.prior_var), k=np.int64(K), **tree, **res)
     if cat:
         # edge cases: k larger than the number of retrievable leaves; a tiny max_nodes
@@ -293,8 +295,62 @@ def case_two_level(name, N, D, n_clusters, seed):
     print(f"[{name}] two-level N={N} D={D} nodes={len(nodes)}", flush=True)
 
 
+def case_interleaved(name, seed=9):
+    """add -> Basic query -> add -> Basic query -> add, all on ONE global random()
+    stream: categorize draws one random() per heap push and one per
+    retrieval (CobwebTorchTree.py:243,268,285), cobweb_predict shuffles every retrieved
+    leaf's sentence list (CobwebWrapper.py:456), and ifit draws its tie-breaks from the
+    same stream (CobwebTorchNode.py:362-368,406).  The corpus holds exact duplicates so
+    leaves carry several sentences (the shuffles draw), and one query runs with a tiny
+    max_init_search so that it raises IndexError after its draws."""
+    D, ncl = 16, 6
+    rng = np.random.default_rng(seed)
+    C = rng.normal(0, 3.0, (ncl, D)).astype(np.float32)
+
+    def block(n):
+        X = (C[rng.integers(0, ncl, n)] + rng.normal(0, 1.0, (n, D))).astype(np.float32)
+        dup = rng.choice(n, n // 6, replace=False)
+        X[dup] = X[rng.integers(0, n, len(dup))]
+        return X
+
+    XA, XB, XC = block(120), block(80), block(60)
+    XA = np.concatenate([XA, XA[:12]])               # repeats of earlier rows too
+    Q1 = (C[rng.integers(0, ncl, 6)] + rng.normal(0, 1.0, (6, D))).astype(np.float32)
+    Q2 = np.concatenate([XA[[0, 3, 5]], XB[[1, 2]], Q1[:1]]).astype(np.float32)
+    random.seed(seed)
+    torch.manual_seed(seed)
+    with _Quiet():
+        w = CobwebWrapper(corpus=[f"a{i}" for i in range(len(XA))], corpus_embeddings=XA)
+    out1 = [w.cobweb_predict(q, 4, return_ids=True) for q in Q1]
+    w.max_init_search = 3
+    err = 0
+    try:
+        w.cobweb_predict(Q1[0], 4, return_ids=True)
+    except IndexError:
+        err = 1
+    w.max_init_search = 100000
+    with _Quiet():
+        w.add_sentences([f"b{i}" for i in range(len(XB))], XB)
+    out2 = [w.cobweb_predict(q, 5, return_ids=True) for q in Q2]
+    with _Quiet():
+        w.add_sentences([f"c{i}" for i in range(len(XC))], XC)
+    after = random.random()
+    nodes, pos, tree = export_tree(w.tree.root, len(w.sentences))
+
+    def ragged(lists):
+        return (np.array([0] + list(np.cumsum([len(x) for x in lists])), np.int64),
+                np.array([s for x in lists for s in x], np.int64))
+    p1, l1 = ragged(out1)
+    p2, l2 = ragged(out2)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), XA=XA, XB=XB, XC=XC, Q1=Q1, Q2=Q2,
+                        seed=np.int64(seed), out1_ptr=p1, out1_ids=l1, out2_ptr=p2, out2_ids=l2,
+                        err_small_max=np.int64(err), random_after=np.float64(after),
+                        prior_var=np.float32(w.tree.prior_var), **tree)
+    print(f"[{name}] interleaved add/query N={len(w.sentences)} nodes={len(nodes)} err={err}", flush=True)
+
+
 def main():
-    which = sys.argv[1:] or ["g1", "g4", "g3", "g5", "g2"]
+    which = sys.argv[1:] or ["g1", "g4", "g3", "g5", "g2", "g8", "g9"]
     t0 = time.time()
     if "g1" in which:   # hierarchical, built by the reference ifit
         X, C = clusters(300, 32, 10, 0)
@@ -315,6 +371,13 @@ def main():
         X = rng.standard_normal((1000, 768)).astype(np.float32)
         Xq, pick = make_queries(X, 8, 8, 12, lambda r, n: r.standard_normal((n, 768)).astype(np.float32))
         case_ifit("g2_flat_d768", X, Xq, pick)
+    if "g9" in which:   # add / Basic query / add on one random() stream
+        case_interleaved("g9_interleaved_d16")
+    if "g8" in which:   # config C1's own shape: 1,500 x 384 N(0,I) by ifit, 300 queries
+        rng = np.random.default_rng(8)
+        X = rng.standard_normal((1500, 384)).astype(np.float32)
+        Xq, pick = make_queries(X, 150, 150, 18, lambda r, n: r.standard_normal((n, 384)).astype(np.float32))
+        case_ifit("g8_c1_d384", X, Xq, pick, n_dense=32)
     print(f"done in {time.time() - t0:.0f}s")
 
 

@@ -143,3 +143,96 @@ def test_device_fit_matches_oracle_2k_clustered_768(pkg, monkeypatch):
     np.testing.assert_array_equal(mean, np.stack([x.mean for x in onodes]))
     np.testing.assert_array_equal(m2, np.stack([x.meanSq for x in onodes]))
     assert len(onodes) > 2 * k and max(len(x.children) for x in onodes) > 1
+
+
+@pytest.mark.parametrize("fitter", ["device", "host"])
+def test_interleaved_add_query_add_matches_reference(pkg, fitter, monkeypatch):
+    """Golden G9 from the real reference: add -> Basic query (cobweb_predict) -> add ->
+    query -> add on one global random() stream.  The drop-in's cobweb_predict advances
+    the stream by the reference's categorize draws (CobwebTorchTree.py:243,268,285) and
+    shuffles the retrieved leaves' lists with it (CobwebWrapper.py:456), so the returned
+    ids, the tree the later inserts build and the final stream position all equal the
+    reference's -- including a query that raises IndexError (max_init_search = 3)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1" if fitter == "device" else "0")
+    g = load_golden("g9_interleaved_d16")
+
+    def ragged(ptr, ids):
+        return [list(ids[ptr[i]:ptr[i + 1]]) for i in range(len(ptr) - 1)]
+
+    random.seed(int(g["seed"]))
+    w = pkg.CobwebWrapper(corpus=[f"a{i}" for i in range(len(g["XA"]))], corpus_embeddings=g["XA"])
+    assert [w.cobweb_predict(q, 4, return_ids=True) for q in g["Q1"]] == ragged(g["out1_ptr"], g["out1_ids"])
+    w.max_init_search = 3
+    with pytest.raises(IndexError):
+        w.cobweb_predict(g["Q1"][0], 4, return_ids=True)
+    w.max_init_search = 100000
+    w.add_sentences([f"b{i}" for i in range(len(g["XB"]))], g["XB"])
+    assert [w.cobweb_predict(q, 5, return_ids=True) for q in g["Q2"]] == ragged(g["out2_ptr"], g["out2_ids"])
+    w.add_sentences([f"c{i}" for i in range(len(g["XC"]))], g["XC"])
+    assert random.random() == float(g["random_after"])
+    p, cnt, mean, m2, sids = _tree_arrays(w.tree.root)
+    np.testing.assert_array_equal(p, g["parent"])
+    np.testing.assert_array_equal([s for x in sids for s in x], g["sid_list"])
+    np.testing.assert_array_equal(cnt, g["count"])
+    np.testing.assert_array_equal(mean, g["mean"])
+    np.testing.assert_array_equal(m2, g["meanSq"])
+
+
+@pytest.mark.parametrize("fail_at", [0, 3])
+def test_device_fit_small_pool_reloads_and_fallback(pkg, fail_at, monkeypatch):
+    """A node pool capped far below the batch (CWQ_FIT_POOL_SLOTS) makes the device fit
+    stop for room many times; every reload exports the tree and the random() state and
+    loads them into a fresh pool, with leaf identity kept across reloads.  fail_at > 0:
+    the pool allocation of the fail_at-th load fails, and the remaining rows go through
+    the host-driven fitter from the last export.  Either way the tree, its statistics,
+    the sentence placement and the random() position equal the host fitter's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(77)
+    n, D, ncl = 600, 64, 8
+    C = rng.standard_normal((ncl, D)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, ncl, n)] + 0.4 * rng.standard_normal((n, D))).astype(np.float32)
+    X[n // 2] = X[n // 7]
+    res = {}
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "0")
+    random.seed(11)
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(n)], corpus_embeddings=X)
+    res["host"] = (_tree_arrays(w.tree.root), random.random())
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1")
+    monkeypatch.setenv("CWQ_FIT_POOL_SLOTS", "100")
+    fitmod = __import__(type(w).__module__.rsplit(".", 1)[0] + ".fit", fromlist=["DeviceTreeFitter"])
+    L = fitmod.lib()
+    calls = {"n": 0}
+    real_create = L.cwq_fit_create
+    if fail_at:
+        def create(*a):
+            calls["n"] += 1
+            return -3 if calls["n"] == fail_at else real_create(*a)
+        monkeypatch.setattr(L, "cwq_fit_create", create)
+    seen = []
+    real_fit = fitmod.DeviceTreeFitter.fit_batch
+
+    def fit_batch(self, Xb):
+        r = real_fit(self, Xb)
+        seen.append(dict(self.stats))
+        return r
+    monkeypatch.setattr(fitmod.DeviceTreeFitter, "fit_batch", fit_batch)
+    random.seed(11)
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(n // 3)], corpus_embeddings=X[:n // 3])
+    w.add_sentences([f"s{i}" for i in range(n // 3, n)], X[n // 3:])
+    res["dev"] = (_tree_arrays(w.tree.root), random.random())
+    (pa, ca, ma, sa, ia), ra = res["host"]
+    (pb, cb, mb, sb, ib), rb = res["dev"]
+    np.testing.assert_array_equal(pa, pb)
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(sa, sb)
+    assert ia == ib and ra == rb
+    loads = sum(st["loads"] for st in seen)
+    if fail_at:
+        assert sum(st["fallback"] is not None for st in seen) == 1
+        assert sum(st["host_rows"] for st in seen) > 0 and calls["n"] == loads + 1
+    else:
+        assert all(st["fallback"] is None for st in seen) and loads > 3

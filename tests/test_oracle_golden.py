@@ -169,3 +169,40 @@ def test_torch_fast_restatement(name):
     for qi, x in enumerate(g["Xq"]):
         got = T.predict(x, k)
         assert_topk_equiv(got, g["fast_ids"][qi], g["rank_scores"][qi])
+
+
+def test_interleaved_add_query_add_g9():
+    """add -> Basic query -> add on ONE random() stream (golden G9 from the real
+    reference): the oracle's predict advances its stream by the draws categorize makes
+    (one per heap push and per retrieval, CobwebTorchTree.py:243,268,285, also when it
+    raises IndexError) and shuffles each retrieved leaf's list (CobwebWrapper.py:456);
+    the later inserts then build the reference's tree and the stream ends where the
+    reference's did."""
+    g = load_golden("g9_interleaved_d16")
+    D = g["XA"].shape[1]
+    t = O.OTree(D, random.Random(int(g["seed"])))
+    n = 0
+
+    def add(X):
+        nonlocal n
+        for x in X:
+            t.ifit(x).sentence_id.append(n)
+            n += 1
+
+    def ragged(ptr, ids):
+        return [list(ids[ptr[i]:ptr[i + 1]]) for i in range(len(ptr) - 1)]
+
+    add(g["XA"])
+    assert [t.predict(q, 4) for q in g["Q1"]] == ragged(g["out1_ptr"], g["out1_ids"])
+    with pytest.raises(IndexError):
+        t.predict(g["Q1"][0], 4, max_nodes=3)
+    assert int(g["err_small_max"]) == 1
+    add(g["XB"])
+    assert [t.predict(q, 5) for q in g["Q2"]] == ragged(g["out2_ptr"], g["out2_ids"])
+    add(g["XC"])
+    assert t.rng.random() == float(g["random_after"])
+    nodes = O.bfs_nodes(t.root)
+    pos = {id(x): i for i, x in enumerate(nodes)}
+    np.testing.assert_array_equal([-1 if x.parent is None else pos[id(x.parent)] for x in nodes], g["parent"])
+    np.testing.assert_array_equal([s for x in nodes for s in x.sentence_id], g["sid_list"])
+    np.testing.assert_array_equal([x.count for x in nodes], g["count"])
