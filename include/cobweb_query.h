@@ -245,8 +245,10 @@ int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_
  * Device-resident incremental fit (F1): CobwebTorchTree.cobweb's insert loop
  * (CobwebTorchTree.py:143-233; CobwebTorchNode.py:57-85, 374-666) run entirely on the
  * GPU -- the tree (statistics, parent links, ordered child lists) in device memory, one
- * workgroup per handle inserting the rows in order, every decision on the device, the
- * reference's random() draws from Python's MT19937 stream run on the device.  Builds the
+ * master workgroup inserting the rows in order, every decision on the device, the
+ * reference's random() draws from Python's MT19937 stream run on the device; a level with
+ * many children (>= CWQ_FIT_FORK_MIN, default 256) has its KL terms computed by helper
+ * workgroups on every CU (CWQ_FIT_HELPERS, default CUs - 1; 0 = one workgroup).  Builds the
  * same trees as the host-driven cwq_fit_kl / cwq_fit_node_op path (fit.py).  dim <= 1024.
  *   cwq_fit_create   a handle with room for cap_nodes nodes
  *   cwq_fit_load     the tree in slots 0..n_nodes-1: parent (host, -1 at the root),
@@ -262,6 +264,8 @@ int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_
  *                    child CSR, count, mean, meanSq (host, [cap] / [cap*dim]) and the
  *                    random() state after the draws (host [625])
  *   cwq_mt19937_draw n draws of Python's random.random() from state625 (host; updates it)
+ *   cwq_mt19937_words n 32-bit outputs (Python's getrandbits(32)) from state625 through the
+ *                    chain-form twist the device's parallel generator runs (host; updates it)
  */
 typedef struct cwq_fit cwq_fit;
 int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t cap_nodes, cwq_fit** out);
@@ -274,6 +278,7 @@ int cwq_fit_export(cwq_fit* h, int32_t* out2, int32_t* parent, int32_t* child_pt
                    float* mean, float* meanSq, uint32_t* mt_state, void* stream);
 const char* cwq_fit_last_error(void);
 int cwq_mt19937_draw(uint32_t* state625, int64_t n, double* out);
+int cwq_mt19937_words(uint32_t* state625, int64_t n, uint32_t* out);
 
 /*
  * PCA + ICA whitening transform (F4).  Replaces PCAICAWhiteningModel.transform

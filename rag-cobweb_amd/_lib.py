@@ -51,6 +51,7 @@ SIGNATURES = {
     "cwq_fit_export": (_c.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwq_fit_last_error": (_c.c_char_p, []),
     "cwq_mt19937_draw": (_c.c_int, [_P, _I64, _P]),
+    "cwq_mt19937_words": (_c.c_int, [_P, _I64, _P]),
 }
 
 _lock = threading.Lock()

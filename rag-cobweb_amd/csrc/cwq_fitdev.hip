@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <memory>
@@ -65,6 +66,53 @@ __host__ __device__ inline double mt_random(uint32_t* mt, int& idx) {
   const uint32_t a = mt_u32(mt, idx) >> 5, b = mt_u32(mt, idx) >> 6;
   return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
+__host__ __device__ inline double mt_res53(uint32_t a, uint32_t b) {   // random() from two outputs
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+__host__ __device__ inline uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+__host__ __device__ inline uint32_t mt_step(uint32_t a, uint32_t b, uint32_t m) {   // the twist of one word
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+// The twist as 227 independent chains: word kk < 227 reads old words only (kk, kk+1,
+// kk+397); word kk in [227, 623) reads old kk, kk+1 and the NEW word kk-227 -- the same
+// chain's previous step -- so chain t owns t, t+227, t+454; word 623 reads new 0 and 396.
+// o: the 7 old words chain t reads (t, t+1, t+397, t+227, t+228, t+454, t+455); nw: its
+// up to 3 new words.
+constexpr int kMtChains = kMtN - kMtM;   // 227
+__host__ __device__ inline int mt_chain_len(int t) { return t + 454 < kMtN - 1 ? 3 : 2; }
+__host__ __device__ inline void mt_chain_load(const uint32_t* mt, int t, uint32_t o[7]) {
+  o[0] = mt[t];
+  o[1] = mt[t + 1];
+  o[2] = mt[t + kMtM];
+  o[3] = mt[t + 227];
+  o[4] = mt[t + 228];
+  o[5] = t + 454 < kMtN - 1 ? mt[t + 454] : 0u;
+  o[6] = t + 454 < kMtN - 1 ? mt[t + 455] : 0u;
+}
+__host__ __device__ inline void mt_chain_run(const uint32_t o[7], int t, uint32_t nw[3]) {
+  nw[0] = mt_step(o[0], o[1], o[2]);
+  nw[1] = mt_step(o[3], o[4], nw[0]);
+  nw[2] = t + 454 < kMtN - 1 ? mt_step(o[5], o[6], nw[1]) : 0u;
+}
+// Host form of the chain twist (the device runs the chains across a wave's lanes); the
+// CPU test cwq_mt19937_words checks it against Python's own getrandbits(32) stream.
+inline void mt_twist_chains_host(uint32_t* mt) {
+  uint32_t o[kMtChains][7], n[kMtChains][3];
+  const uint32_t old623 = mt[kMtN - 1];
+  for (int t = 0; t < kMtChains; ++t) mt_chain_load(mt, t, o[t]);
+  for (int t = 0; t < kMtChains; ++t) {
+    mt_chain_run(o[t], t, n[t]);
+    for (int s = 0; s < mt_chain_len(t); ++s) mt[t + 227 * s] = n[t][s];
+  }
+  mt[kMtN - 1] = mt_step(old623, mt[0], mt[kMtM - 1]);
+}
 
 // ---------------------------------------------------------------------------
 // Device tree
@@ -83,29 +131,112 @@ struct FitDev {
   uint32_t* mt;                 // [624]
   float *kres, *gain, *tall, *tins, *ncv;   // per-level scratch [cap]
   int* jobs;                    // [cap] split job nodes
+  // the chip-wide KL pass (fork / join between the master workgroup and its helpers)
+  struct FdJob* job;
+  float* pvec;                  // [3][D] the job's reference vectors (mean, var, log var)
+  uint32_t* rnd;                // [2*cap + 8] a level's tempered MT outputs (the sort's draws)
+  int fork_min;                 // fork a level's KL pass when it has >= fork_min children
 };
 
 constexpr int kFdThreads = 1024;
 constexpr int kFdWaves = kFdThreads / 64;
 constexpr int kFdMaxD = 1024;   // 7 D-vectors + the MT state stay within 64 KiB of LDS
 constexpr int kFdChunk = 1024;
-enum { FD_OK = 0, FD_ROOM = 1, FD_FULL = 2 };
+constexpr int kFdRing = 64;     // per-job claim / completion counters, by epoch
+constexpr int kFdWaveClaim = 4; // children per claim of a master wave
+constexpr int kFdHelperPer = 2; // children per helper wave per workgroup claim
+constexpr int kFdForkMin = 256; // default fork threshold (children of a level)
+enum { FD_OK = 0, FD_ROOM = 1, FD_FULL = 2, FD_HANG = 3 };
+// bounded spins (s_memrealtime runs at 100 MHz): a helper with no new job for this long
+// leaves (the master never depends on helpers: it claims work itself); the master gives up
+// a join after this long (status FD_HANG)
+constexpr uint64_t kFdIdleTicks = 2000000000ull;   // 20 s
+constexpr uint64_t kFdJoinTicks = 2000000000ull;
+
+// The job a forked level hands to the helper workgroups: zeroed before every launch
+// (cwq_fit_insert).  epoch = job number (1, 2, ...), polled by the helpers; the claim /
+// completion counters live in a ring by epoch, so a helper that is late for job e can
+// only ever touch job e's own counters.
+struct FdJob {
+  int epoch;
+  int quit;
+  int type;        // 0: U, T of the children arena[base .. base+n) vs (P + x); 1: KL(c || P) of jobs[0..n)
+  int n;
+  int64_t base;
+  int64_t row;     // the row being inserted (x = X[row])
+  int kofs;        // type 1: output offset in kres
+  int pad[25];
+  int next[kFdRing];
+  int done[kFdRing];
+};
 
 struct FdShared {
   float x[kFdMaxD], mu2[kFdMaxD], v2[kFdMaxD], lv2[kFdMaxD];
   float muP[kFdMaxD], vP[kFdMaxD], lvP[kFdMaxD];
   uint32_t mt[kMtN];
+  uint32_t mtn[kMtN];   // the parallel twist's new words
   float cg[kFdChunk], cn[kFdChunk];
   int ci[8];
   float cf[8];
   double cr[2];   // random() of "best" and "new"
   int flag;
+  int epoch;      // master: the last job published
+  // parallel top-2: every wave's two best (gain, count, random, index)
+  float tg[kFdWaves][2], tn[kFdWaves][2];
+  double tr[kFdWaves][2];
+  int ti[kFdWaves][2];
 };
+
+__device__ __forceinline__ int ld_agent(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_f(float* p, float v) {   // write-through (sc1) store
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ONE wave: advance the MT19937 state (mt in LDS, idx) by n outputs exactly as n mt_u32
+// calls would, writing the tempered outputs to out[0..n).  Every lane passes the same idx.
+// A twist is 227 chains over the 64 lanes (mt_chain_*), the new words into tmp (LDS) while
+// mt still holds the old ones, then copied back with word 623.
+__device__ __forceinline__ void mt_gen_wave(uint32_t* mt, uint32_t* tmp, int& idx, int64_t n, uint32_t* out, int lane) {
+  int64_t done = 0;
+  while (done < n) {
+    if (idx >= kMtN) {
+      for (int t = lane; t < kMtChains; t += 64) {
+        uint32_t o[7], nw[3];
+        mt_chain_load(mt, t, o);
+        mt_chain_run(o, t, nw);
+        tmp[t] = nw[0];
+        tmp[t + 227] = nw[1];
+        if (t + 454 < kMtN - 1) tmp[t + 454] = nw[2];
+      }
+      wave_sync();
+      if (lane == 0) tmp[kMtN - 1] = mt_step(mt[kMtN - 1], tmp[0], tmp[kMtM - 1]);
+      wave_sync();
+      for (int i = lane; i < kMtN; i += 64) mt[i] = tmp[i];
+      wave_sync();
+      idx = 0;
+    }
+    const int take = (int)((int64_t)(kMtN - idx) < n - done ? (int64_t)(kMtN - idx) : n - done);
+    for (int i = lane; i < take; i += 64) out[done + i] = mt_temper(mt[idx + i]);
+    wave_sync();
+    idx += take;
+    done += take;
+  }
+}
 
 #pragma clang fp contract(off)
 
 // WG-wide node operations (every thread calls; barriers inside)
-__device__ void fd_zero(const FitDev& f, int s) {
+__device__ __forceinline__ void fd_zero(const FitDev& f, int s) {
 #pragma clang fp contract(off)
   for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
     f.mean[(size_t)s * f.D + d] = 0.f;
@@ -116,7 +247,7 @@ __device__ void fd_zero(const FitDev& f, int s) {
 }
 
 // increment_counts (CobwebTorchNode.py:57-68)
-__device__ void fd_increment(const FitDev& f, int s, const float* x) {
+__device__ __forceinline__ void fd_increment(const FitDev& f, int s, const float* x) {
 #pragma clang fp contract(off)
   const float cd = f.count[s];
   for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
@@ -133,7 +264,7 @@ __device__ void fd_increment(const FitDev& f, int s, const float* x) {
 }
 
 // update_counts_from_node (CobwebTorchNode.py:70-85)
-__device__ void fd_combine(const FitDev& f, int dst, int src) {
+__device__ __forceinline__ void fd_combine(const FitDev& f, int dst, int src) {
 #pragma clang fp contract(off)
   const float cd = f.count[dst], cs = f.count[src];
   for (int d = threadIdx.x; d < f.D; d += kFdThreads) {
@@ -149,7 +280,7 @@ __device__ void fd_combine(const FitDev& f, int dst, int src) {
 }
 
 // is_exact_match (CobwebTorchNode.py:652-666, torch.isclose defaults)
-__device__ bool fd_exact(const FitDev& f, FdShared& sh, int s) {
+__device__ __forceinline__ bool fd_exact(const FitDev& f, FdShared& sh, int s) {
 #pragma clang fp contract(off)
   if (threadIdx.x == 0) sh.flag = 1;
   __syncthreads();
@@ -171,7 +302,7 @@ __device__ bool fd_exact(const FitDev& f, FdShared& sh, int s) {
 // thread 0; -1: pool full.  Slots are never reused within a load (a node freed by a split
 // keeps its slot, marked parent = -2), so the host maps every slot it loaded to the same
 // node object afterwards; slot numbers never enter a decision.
-__device__ int fd_alloc(const FitDev& f) {
+__device__ __forceinline__ int fd_alloc(const FitDev& f) {
   if (f.ctrl[0] >= f.cap) return -1;
   const int s = f.ctrl[0]++;
   f.parent[s] = -1;
@@ -182,7 +313,7 @@ __device__ int fd_alloc(const FitDev& f) {
 }
 
 // a new zeroed node (WG-wide); s_out via LDS
-__device__ int fd_new_node(const FitDev& f, FdShared& sh) {
+__device__ __forceinline__ int fd_new_node(const FitDev& f, FdShared& sh) {
   if (threadIdx.x == 0) {
     sh.ci[0] = fd_alloc(f);
     if (sh.ci[0] < 0) f.ctrl[3] = FD_FULL;
@@ -195,7 +326,7 @@ __device__ int fd_new_node(const FitDev& f, FdShared& sh) {
 }
 
 // children[p].append(c)
-__device__ void fd_append(const FitDev& f, FdShared& sh, int p, int c) {
+__device__ __forceinline__ void fd_append(const FitDev& f, FdShared& sh, int p, int c) {
   if (threadIdx.x == 0) {
     sh.ci[1] = 0;
     if (f.ccnt[p] == f.ccap[p]) {   // grow: a new slab of twice the capacity at the arena top
@@ -229,7 +360,7 @@ __device__ void fd_append(const FitDev& f, FdShared& sh, int p, int c) {
 }
 
 // children[p].remove(c): first occurrence, the tail shifted left by one
-__device__ void fd_remove(const FitDev& f, FdShared& sh, int p, int c) {
+__device__ __forceinline__ void fd_remove(const FitDev& f, FdShared& sh, int p, int c) {
   const int n = f.ccnt[p];
   const int64_t base = f.coff[p];
   if (threadIdx.x == 0) sh.ci[4] = n;
@@ -276,6 +407,89 @@ __device__ __forceinline__ void fd_insert_mv(float c, float m, float m2, float x
   vo = mm2 / cnt + pv;
 }
 
+// U = KL(c + x || P + x), T = KL(c || P + x) of child slot c: ONE wave (all lanes return
+// them); reference P + x = (sh.mu2, sh.v2, sh.lv2), x = sh.x
+__device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, int c, int lane, float& U, float& T) {
+#pragma clang fp contract(off)
+  const int D = f.D;
+  const float pv = f.pv;
+  double sU = 0.0, tU = 0.0, sT = 0.0, tT = 0.0;
+  const float cc = f.count[c];
+  for (int d = lane; d < D; d += 64) {
+    const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
+    const float mu2 = sh.mu2[d], v2 = sh.v2[d], lv2 = sh.lv2[d];
+    float mu1, v1;
+    fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
+    {
+      const float a = lv2 - logf(v1);
+      const float df = mu1 - mu2;
+      const float bb = (v1 + df * df) / v2;
+      sU += (double)a;
+      tU += (double)bb;
+    }
+    mu1 = m;
+    v1 = m2 / cc + pv;
+    {
+      const float a = lv2 - logf(v1);
+      const float df = mu1 - mu2;
+      const float bb = (v1 + df * df) / v2;
+      sT += (double)a;
+      tT += (double)bb;
+    }
+  }
+  U = fd_kl_finish(sU, tU, D);
+  T = fd_kl_finish(sT, tT, D);
+}
+
+// KL(c || ref) of node slot c, ref = (mu, v, lv) in LDS: ONE wave
+__device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, const float* v, const float* lv, int c,
+                                           int lane) {
+#pragma clang fp contract(off)
+  const int D = f.D;
+  const float cc = f.count[c];
+  double sa = 0.0, sb = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float mu1 = f.mean[(size_t)c * D + d], v1 = f.meanSq[(size_t)c * D + d] / cc + f.pv;
+    const float a = lv[d] - logf(v1);
+    const float df = mu1 - mu[d];
+    const float bb = (v1 + df * df) / v[d];
+    sa += (double)a;
+    sb += (double)bb;
+  }
+  return fd_kl_finish(sa, sb, D);
+}
+
+// KL(new || P + x) of the would-be new leaf N(x, pv): ONE wave
+__device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, int lane) {
+#pragma clang fp contract(off)
+  double sU = 0.0, tU = 0.0;
+  for (int d = lane; d < f.D; d += 64) {
+    const float mu1 = sh.x[d], v1 = 0.f + f.pv;
+    const float a = sh.lv2[d] - logf(v1);
+    const float df = mu1 - sh.mu2[d];
+    const float bb = (v1 + df * df) / sh.v2[d];
+    sU += (double)a;
+    tU += (double)bb;
+  }
+  return fd_kl_finish(sU, tU, f.D);
+}
+
+// one child of a job (ONE wave): its KL terms to kres by write-through stores
+__device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh, int type, int64_t base, int kofs, int j,
+                                             int lane) {
+  if (type == 0) {
+    float U, T;
+    fd_kl_UT(f, sh, f.arena[base + j], lane, U, T);
+    if (lane == 0) {
+      st_agent_f(&f.kres[2 * j], U);
+      st_agent_f(&f.kres[2 * j + 1], T);
+    }
+  } else {
+    const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
+    if (lane == 0) st_agent_f(&f.kres[kofs + j], K);
+  }
+}
+
 // (gain, count, random) descending; ties keep list order (Python's stable sort)
 __device__ __forceinline__ bool fd_rel_before(float g1, float n1, double r1, int i1, float g2, float n2, double r2,
                                               int i2) {
@@ -285,14 +499,216 @@ __device__ __forceinline__ bool fd_rel_before(float g1, float n1, double r1, int
   return i1 < i2;
 }
 
+// ---------------------------------------------------------------------------
+// The chip-wide KL pass.  The master workgroup (block 0) runs the insert loop; the other
+// workgroups are helpers.  A level with >= fork_min children is forked: the master writes
+// the job (the reference vectors, the child list) and publishes its epoch behind an agent
+// release; helpers poll the epoch, acquire, and claim children per workgroup; every result
+// goes out by a write-through store, and each claim's count is added to the job's done
+// counter after its stores have drained; the master claims too (per wave), waits until done
+// covers every child, acquires, and reads the results.  Protocol: cdna_hip_programming.md
+// §6 Guideline 16 (R1 producer/consumer forms; every spin bounded).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fd_help_job(const FitDev& f, FdShared& sh, const float* X, int e) {
+  FdJob* job = f.job;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, D = f.D;
+  const int type = job->type, n = job->n, kofs = job->kofs;
+  const int64_t base = job->base, row = job->row;
+  float* mu = type ? sh.muP : sh.mu2;
+  float* v = type ? sh.vP : sh.v2;
+  float* lv = type ? sh.lvP : sh.lv2;
+  for (int d = tid; d < D; d += kFdThreads) {
+    mu[d] = f.pvec[d];
+    v[d] = f.pvec[D + d];
+    lv[d] = f.pvec[2 * D + d];
+    if (type == 0) sh.x[d] = X[row * D + d];
+  }
+  __syncthreads();
+  const int slot = e % kFdRing;
+  constexpr int per = kFdWaves * kFdHelperPer;
+  for (;;) {
+    if (tid == 0) sh.ci[0] = ld_agent(&job->epoch) == e ? atomicAdd(&job->next[slot], per) : n;
+    __syncthreads();
+    const int j0 = sh.ci[0];
+    __syncthreads();
+    if (j0 >= n) break;
+    const int j1 = j0 + per < n ? j0 + per : n;
+    for (int j = j0 + wave; j < j1; j += kFdWaves) fd_job_child(f, sh, type, base, kofs, j, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave's stores drained
+    __syncthreads();
+    if (tid == 0) atomicAdd(&job->done[slot], j1 - j0);
+  }
+}
+
+__device__ __forceinline__ void fd_helper(const FitDev& f, FdShared& sh, const float* X) {
+  const int tid = threadIdx.x;
+  int seen = 0;
+  for (;;) {
+    if (tid == 0) {
+      int e = -1;
+      const uint64_t t0 = wall_clock64();
+      for (;;) {
+        if (ld_agent(&f.job->quit)) break;
+        const int ep = ld_agent(&f.job->epoch);
+        if (ep != seen) {
+          e = ep;
+          break;
+        }
+        if (wall_clock64() - t0 > kFdIdleTicks) break;   // bounded: the master needs no helper
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (e > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      sh.ci[1] = e;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int e = sh.ci[1];
+    __syncthreads();
+    if (e <= 0) return;
+    seen = e;
+    fd_help_job(f, sh, X, e);
+  }
+}
+
+// master (all threads): fork a job over n items and join it.  Wave 0 first generates
+// `nrnd` MT outputs of the level's sort draws into f.rnd (advancing thread 0's mt_idx),
+// wave 1 first computes the new leaf's term (type 0, into kres[2n]); then every master
+// wave claims items too.  false: the join timed out.
+__device__ __forceinline__ bool fd_fork(const FitDev& f, FdShared& sh, int64_t row, int type, int n, int64_t base, int kofs,
+                        int64_t nrnd, int& mt_idx) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, D = f.D;
+  FdJob* job = f.job;
+  const float* mu = type ? sh.muP : sh.mu2;
+  const float* v = type ? sh.vP : sh.v2;
+  const float* lv = type ? sh.lvP : sh.lv2;
+  for (int d = tid; d < D; d += kFdThreads) {
+    f.pvec[d] = mu[d];
+    f.pvec[D + d] = v[d];
+    f.pvec[2 * D + d] = lv[d];
+  }
+  const int e = sh.epoch + 1;
+  const int slot = e % kFdRing;
+  if (tid == 0) {
+    job->type = type;
+    job->n = n;
+    job->base = base;
+    job->row = row;
+    job->kofs = kofs;
+    job->next[slot] = 0;
+    job->done[slot] = 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {   // publish: agent release of everything the master wrote, then the epoch
+    sh.epoch = e;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_agent(&job->epoch, e);
+  }
+  if (wave == 0 && nrnd > 0) {
+    int idx = __shfl(mt_idx, 0);
+    mt_gen_wave(sh.mt, sh.mtn, idx, nrnd, f.rnd, lane);
+    if (lane == 0) mt_idx = idx;
+  }
+  if (wave == 1 && type == 0) {
+    const float K = fd_kl_new(f, sh, lane);
+    if (lane == 0) f.kres[2 * n] = K;
+  }
+  for (;;) {
+    int j0 = 0;
+    if (lane == 0) j0 = atomicAdd(&job->next[slot], kFdWaveClaim);
+    j0 = __shfl(j0, 0);
+    if (j0 >= n) break;
+    const int j1 = j0 + kFdWaveClaim < n ? j0 + kFdWaveClaim : n;
+    for (int j = j0; j < j1; ++j) fd_job_child(f, sh, type, base, kofs, j, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) atomicAdd(&job->done[slot], j1 - j0);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint64_t t0 = wall_clock64();
+    int ok = 1;
+    while (ld_agent(&job->done[slot]) < n) {
+      if (wall_clock64() - t0 > kFdJoinTicks) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    sh.ci[1] = ok;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool ok = sh.ci[1] != 0;
+  __syncthreads();
+  return ok;
+}
+
+// top-2 lists of (gain, count, random, index), best first; index -1 = empty
+struct FdTop2 {
+  float g1, n1, g2, n2;
+  double r1, r2;
+  int i1, i2;
+};
+__device__ __forceinline__ bool fd_before(float g, float n, double r, int i, float g2, float n2, double r2, int i2) {
+  if (i2 < 0) return i >= 0;
+  if (i < 0) return false;
+  return fd_rel_before(g, n, r, i, g2, n2, r2, i2);
+}
+__device__ __forceinline__ void fd_top2_offer(FdTop2& t, float g, float n, double r, int i) {
+  if (fd_before(g, n, r, i, t.g1, t.n1, t.r1, t.i1)) {
+    t.g2 = t.g1; t.n2 = t.n1; t.r2 = t.r1; t.i2 = t.i1;
+    t.g1 = g; t.n1 = n; t.r1 = r; t.i1 = i;
+  } else if (fd_before(g, n, r, i, t.g2, t.n2, t.r2, t.i2)) {
+    t.g2 = g; t.n2 = n; t.r2 = r; t.i2 = i;
+  }
+}
+
+// two_best_children over b children in parallel (master, all threads): the same order as
+// the sequential sort (gain, count, random() descending, list order), the random() of child
+// j being the level's draws 2j, 2j+1 in f.rnd.  Returns the indices in sh.ci[2], sh.ci[3].
+__device__ __forceinline__ void fd_top2_parallel(const FitDev& f, FdShared& sh, int b) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  FdTop2 t{0.f, 0.f, 0.f, 0.f, 0.0, 0.0, -1, -1};
+  for (int j = tid; j < b; j += kFdThreads)
+    fd_top2_offer(t, f.gain[j], f.ncv[j], mt_res53(f.rnd[2 * j], f.rnd[2 * j + 1]), j);
+  for (int off = 32; off > 0; off >>= 1) {
+    const float og1 = __shfl_xor(t.g1, off, 64), on1 = __shfl_xor(t.n1, off, 64);
+    const float og2 = __shfl_xor(t.g2, off, 64), on2 = __shfl_xor(t.n2, off, 64);
+    const double or1 = __shfl_xor(t.r1, off, 64), or2 = __shfl_xor(t.r2, off, 64);
+    const int oi1 = __shfl_xor(t.i1, off, 64), oi2 = __shfl_xor(t.i2, off, 64);
+    fd_top2_offer(t, og1, on1, or1, oi1);
+    fd_top2_offer(t, og2, on2, or2, oi2);
+  }
+  if (lane == 0) {
+    sh.tg[wave][0] = t.g1; sh.tn[wave][0] = t.n1; sh.tr[wave][0] = t.r1; sh.ti[wave][0] = t.i1;
+    sh.tg[wave][1] = t.g2; sh.tn[wave][1] = t.n2; sh.tr[wave][1] = t.r2; sh.ti[wave][1] = t.i2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    FdTop2 r{0.f, 0.f, 0.f, 0.f, 0.0, 0.0, -1, -1};
+    for (int w = 0; w < kFdWaves; ++w)
+      for (int k = 0; k < 2; ++k) fd_top2_offer(r, sh.tg[w][k], sh.tn[w][k], sh.tr[w][k], sh.ti[w][k]);
+    sh.ci[2] = r.i1;
+    sh.ci[3] = r.i2;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, const float* __restrict__ X, int64_t n,
                                                                 int* leaf_out) {
 #pragma clang fp contract(off)
   extern __shared__ char fd_smem[];
   FdShared& sh = *reinterpret_cast<FdShared*>(fd_smem);
+  if (blockIdx.x > 0) {   // a helper of the chip-wide KL passes
+    fd_helper(f, sh, X);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = f.D;
   const float pv = f.pv;
+  if (tid == 0) sh.epoch = 0;
   for (int i = tid; i < kMtN; i += kFdThreads) sh.mt[i] = f.mt[i];
   int mt_idx = f.ctrl[4];   // thread 0's copy is the live one
   double drawn = 0;
@@ -355,50 +771,30 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       }
       __syncthreads();
       const int64_t cbase = f.coff[cur];
-      // per child: U = KL(c + x || P + x), T = KL(c || P + x); the new leaf's KL(new || P + x)
-      for (int j = wave; j <= b; j += kFdWaves) {
-        double sU = 0.0, tU = 0.0, sT = 0.0, tT = 0.0;
-        if (j < b) {
-          const int c = f.arena[cbase + j];
-          const float cc = f.count[c];
-          for (int d = lane; d < D; d += 64) {
-            const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
-            const float mu2 = sh.mu2[d], v2 = sh.v2[d], lv2 = sh.lv2[d];
-            float mu1, v1;
-            fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
-            {
-              const float a = lv2 - logf(v1);
-              const float df = mu1 - mu2;
-              const float bb = (v1 + df * df) / v2;
-              sU += (double)a;
-              tU += (double)bb;
+      // per child: U = KL(c + x || P + x), T = KL(c || P + x); the new leaf's KL(new || P + x).
+      // A level of >= fork_min children goes over the whole chip (fd_fork), the level's b
+      // sort draws generated meanwhile; a smaller one stays in this workgroup (one wave per
+      // child, the draws sequential below)
+      const bool forked = f.job != nullptr && b >= f.fork_min;
+      if (forked) {
+        if (!fd_fork(f, sh, row, 0, b, cbase, 0, 2 * (int64_t)b, mt_idx)) {
+          if (tid == 0) f.ctrl[3] = FD_HANG;
+          break;
+        }
+        if (tid == 0) drawn += b;
+      } else {
+        for (int j = wave; j <= b; j += kFdWaves) {
+          if (j < b) {
+            float U, T;
+            fd_kl_UT(f, sh, f.arena[cbase + j], lane, U, T);
+            if (lane == 0) {
+              f.kres[2 * j] = U;
+              f.kres[2 * j + 1] = T;
             }
-            mu1 = m;
-            v1 = m2 / cc + pv;
-            {
-              const float a = lv2 - logf(v1);
-              const float df = mu1 - mu2;
-              const float bb = (v1 + df * df) / v2;
-              sT += (double)a;
-              tT += (double)bb;
-            }
+          } else {
+            const float K = fd_kl_new(f, sh, lane);
+            if (lane == 0) f.kres[2 * b] = K;
           }
-          const float U = fd_kl_finish(sU, tU, D), T = fd_kl_finish(sT, tT, D);
-          if (lane == 0) {
-            f.kres[2 * j] = U;
-            f.kres[2 * j + 1] = T;
-          }
-        } else {
-          for (int d = lane; d < D; d += 64) {
-            const float mu1 = sh.x[d], v1 = 0.f + pv;
-            const float a = sh.lv2[d] - logf(v1);
-            const float df = mu1 - sh.mu2[d];
-            const float bb = (v1 + df * df) / sh.v2[d];
-            sU += (double)a;
-            tU += (double)bb;
-          }
-          const float K = fd_kl_finish(sU, tU, D);
-          if (lane == 0) f.kres[2 * b] = K;
         }
       }
       __syncthreads();
@@ -415,52 +811,73 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         f.ncv[j] = nc;
       }
       __syncthreads();
-      // two_best_children: one random() per child, in list order (chunks staged in LDS)
+      // two_best_children: one random() per child, in list order
       int i1 = -1, i2 = -1;
-      float g1 = 0.f, n1 = 0.f, g2 = 0.f, n2 = 0.f;
-      double r1 = 0.0, r2 = 0.0;
-      for (int c0 = 0; c0 < b; c0 += kFdChunk) {
-        const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
-        for (int j = tid; j < m; j += kFdThreads) {
-          sh.cg[j] = f.gain[c0 + j];
-          sh.cn[j] = f.ncv[c0 + j];
-        }
+      if (forked) {
+        fd_top2_parallel(f, sh, b);   // the draws are in f.rnd already
+        i1 = sh.ci[2];
+        i2 = sh.ci[3];
         __syncthreads();
-        if (tid == 0) {
-          for (int j = 0; j < m; ++j) {
-            const double r = mt_random(sh.mt, mt_idx);
-            drawn += 1;
-            const float g = sh.cg[j], nn = sh.cn[j];
-            const int id = c0 + j;
-            if (i1 < 0 || fd_rel_before(g, nn, r, id, g1, n1, r1, i1)) {
-              i2 = i1; g2 = g1; n2 = n1; r2 = r1;
-              i1 = id; g1 = g; n1 = nn; r1 = r;
-            } else if (i2 < 0 || fd_rel_before(g, nn, r, id, g2, n2, r2, i2)) {
-              i2 = id; g2 = g; n2 = nn; r2 = r;
+      } else {
+        float g1 = 0.f, n1 = 0.f, g2 = 0.f, n2 = 0.f;
+        double r1 = 0.0, r2 = 0.0;
+        for (int c0 = 0; c0 < b; c0 += kFdChunk) {   // chunks staged in LDS
+          const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
+          for (int j = tid; j < m; j += kFdThreads) {
+            sh.cg[j] = f.gain[c0 + j];
+            sh.cn[j] = f.ncv[c0 + j];
+          }
+          __syncthreads();
+          if (tid == 0) {
+            for (int j = 0; j < m; ++j) {
+              const double r = mt_random(sh.mt, mt_idx);
+              drawn += 1;
+              const float g = sh.cg[j], nn = sh.cn[j];
+              const int id = c0 + j;
+              if (i1 < 0 || fd_rel_before(g, nn, r, id, g1, n1, r1, i1)) {
+                i2 = i1; g2 = g1; n2 = n1; r2 = r1;
+                i1 = id; g1 = g; n1 = nn; r1 = r;
+              } else if (i2 < 0 || fd_rel_before(g, nn, r, id, g2, n2, r2, i2)) {
+                i2 = id; g2 = g; n2 = nn; r2 = r;
+              }
             }
           }
+          __syncthreads();
         }
-        __syncthreads();
       }
-      // pu sums (sequential float32, list order) and the operation choice: thread 0
-      if (tid == 0) {
-        float s_all = 0.f, s_ins = 0.f, s_keep = 0.f;
+      // pu sums (sequential float32 in list order -- Python's `score += ...`): chunks of
+      // the terms staged in LDS, the three sums run side by side by thread 0
+      float q_all = 0.f, q_ins = 0.f, q_keep = 0.f;
+      {
         bool first_all = true, first_ins = true, first_keep = true;
-        for (int j = 0; j < b; ++j) {
-          const float ta = f.tall[j];
-          const float ti = j == i1 ? f.tins[j] : ta;
-          s_all = first_all ? ta : s_all + ta;
-          first_all = false;
-          s_ins = first_ins ? ti : s_ins + ti;
-          first_ins = false;
-          if (j != i1 && j != i2) {
-            s_keep = first_keep ? ta : s_keep + ta;
-            first_keep = false;
+        for (int c0 = 0; c0 < b; c0 += kFdChunk) {
+          const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
+          for (int j = tid; j < m; j += kFdThreads) sh.cg[j] = f.tall[c0 + j];
+          __syncthreads();
+          if (tid == 0) {
+            const float tins1 = (i1 >= c0 && i1 < c0 + m) ? f.tins[i1] : 0.f;
+            for (int jj = 0; jj < m; ++jj) {
+              const int j = c0 + jj;
+              const float ta = sh.cg[jj];
+              const float ti = j == i1 ? tins1 : ta;
+              q_all = first_all ? ta : q_all + ta;
+              first_all = false;
+              q_ins = first_ins ? ti : q_ins + ti;
+              first_ins = false;
+              if (j != i1 && j != i2) {
+                q_keep = first_keep ? ta : q_keep + ta;
+                first_keep = false;
+              }
+            }
           }
+          __syncthreads();
         }
+      }
+      // the operation choice: thread 0
+      if (tid == 0) {
         const float knew = f.kres[2 * b];
-        const float pu_best = s_ins / (float)b;
-        const float pu_new = (s_all + (1.0f / nP1) * knew) / (float)(b + 1);
+        const float pu_best = q_ins / (float)b;
+        const float pu_new = (q_all + (1.0f / nP1) * knew) / (float)(b + 1);
         const double r_best = mt_random(sh.mt, mt_idx), r_new = mt_random(sh.mt, mt_idx);
         drawn += 2;
         sh.ci[0] = f.arena[cbase + i1];
@@ -471,7 +888,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         sh.ci[6] = f.ccnt[sh.ci[0]] > 0 ? 1 : 0;        // split applies
         sh.cf[0] = pu_best;
         sh.cf[1] = pu_new;
-        sh.cf[2] = s_keep;
+        sh.cf[2] = q_keep;
         sh.cr[0] = r_best;
         sh.cr[1] = r_new;
       }
@@ -526,21 +943,17 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         const float K = fd_kl_finish(sa, sb, D);
         if (lane == 0) sh.cf[3] = K;
       }
-      if (do_split) {
-        for (int j = wave; j < n_split; j += kFdWaves) {   // KL(c || P) (cand type 0, ref P)
-          const int c = f.jobs[j];
-          const float cc = f.count[c];
-          double sa = 0.0, sb = 0.0;
-          for (int d = lane; d < D; d += 64) {
-            const float mu1 = f.mean[(size_t)c * D + d], v1 = f.meanSq[(size_t)c * D + d] / cc + pv;
-            const float a = sh.lvP[d] - logf(v1);
-            const float df = mu1 - sh.muP[d];
-            const float bb = (v1 + df * df) / sh.vP[d];
-            sa += (double)a;
-            sb += (double)bb;
+      if (do_split) {   // KL(c || P) of the split's nodes
+        if (f.job != nullptr && n_split >= f.fork_min) {
+          if (!fd_fork(f, sh, row, 1, n_split, 0, 2 * b + 1, 0, mt_idx)) {
+            if (tid == 0) f.ctrl[3] = FD_HANG;
+            break;
           }
-          const float K = fd_kl_finish(sa, sb, D);
-          if (lane == 0) f.kres[2 * b + 1 + j] = K;
+        } else {
+          for (int j = wave; j < n_split; j += kFdWaves) {
+            const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
+            if (lane == 0) f.kres[2 * b + 1 + j] = K;
+          }
         }
       }
       __syncthreads();
@@ -630,11 +1043,11 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         }
         __syncthreads();
       }
-      if (f.ctrl[3] == FD_FULL) break;
+      if (f.ctrl[3] >= FD_FULL) break;
       __syncthreads();
     }
     __syncthreads();
-    if (f.ctrl[3] == FD_FULL) break;
+    if (f.ctrl[3] >= FD_FULL) break;
     if (tid == 0) {
       leaf_out[row] = leaf;
       f.ctrl64[1] = row + 1;
@@ -646,6 +1059,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
   if (tid == 0) {
     f.ctrl[4] = mt_idx;
     f.ctrl64[2] += (int64_t)drawn;
+    if (f.job != nullptr) st_agent(&f.job->quit, 1);   // the helpers leave
   }
 }
 
@@ -693,7 +1107,8 @@ extern "C" int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t 
             al((void**)&f.ctrl, 64) && al((void**)&f.ctrl64, 64) &&
             al((void**)&f.mt, kMtN * 4) && al((void**)&f.kres, (3 * C + 8) * 4) && al((void**)&f.gain, C * 4) &&
             al((void**)&f.tall, C * 4) && al((void**)&f.tins, C * 4) && al((void**)&f.ncv, C * 4) &&
-            al((void**)&f.jobs, (2 * C + 8) * 4);
+            al((void**)&f.jobs, (2 * C + 8) * 4) && al((void**)&f.job, sizeof(FdJob)) &&
+            al((void**)&f.pvec, (size_t)3 * dim * 4) && al((void**)&f.rnd, (2 * C + 8) * 4);
   if (!ok) {
     for (void* p : h->allocs) (void)hipFree(p);
     return fit_fail(CWQ_ERR_OOM, "cwq_fit_create: device allocation failed");
@@ -774,7 +1189,18 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   if (hipSetDevice(h->device) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "hipSetDevice failed");
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = sizeof(FdShared);
-  hipLaunchKernelGGL(fit_insert_kernel, dim3(1), dim3(kFdThreads), lds, s, h->f, X, n, leaf_out);
+  // helper workgroups for the chip-wide KL passes: one per other CU (CWQ_FIT_HELPERS
+  // overrides; 0 = the single-workgroup loop); levels of >= CWQ_FIT_FORK_MIN children fork
+  int cus = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) cus = 1;
+  int helpers = cus > 1 ? cus - 1 : 0;
+  if (const char* e = getenv("CWQ_FIT_HELPERS")) helpers = atoi(e) < 0 ? 0 : atoi(e);
+  FitDev f = h->f;
+  f.fork_min = kFdForkMin;
+  if (const char* e = getenv("CWQ_FIT_FORK_MIN")) f.fork_min = atoi(e) < 2 ? 2 : atoi(e);
+  if (helpers == 0) f.job = nullptr;
+  else if (hipMemsetAsync(f.job, 0, sizeof(FdJob), s) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "job reset failed");
+  hipLaunchKernelGGL(fit_insert_kernel, dim3(1 + helpers), dim3(kFdThreads), lds, s, f, X, n, leaf_out);
   if (hipGetLastError() != hipSuccess) return fit_fail(CWQ_ERR_HIP, "fit_insert_kernel launch failed");
   int ctrl[16];
   int64_t c64[8];
@@ -787,6 +1213,7 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   info[2] = ctrl[3];
   info[3] = ctrl[0];
   if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");
+  if (ctrl[3] == FD_HANG) return fit_fail(CWQ_ERR_HIP, "cwq_fit_insert: a chip-wide KL pass did not complete");
   // the next call resumes: clear the room flag
   if (ctrl[3] == FD_ROOM) {
     const int z = 0;
@@ -839,6 +1266,22 @@ extern "C" int cwq_fit_export(cwq_fit* h, int32_t* out2, int32_t* parent, int32_
   }
   out2[0] = used;
   out2[1] = ctrl[2];
+  return CWQ_OK;
+}
+
+// Host run of the chain-form twist (mt_twist_chains_host, the device's mt_gen_wave
+// arithmetic): n 32-bit outputs -- Python's getrandbits(32) stream -- from state625 (updated).
+extern "C" int cwq_mt19937_words(uint32_t* state625, int64_t n, uint32_t* out) {
+  if (!state625 || n < 0 || (n > 0 && !out)) return CWQ_ERR_ARG;
+  int idx = (int)state625[kMtN];
+  for (int64_t i = 0; i < n; ++i) {
+    if (idx >= kMtN) {
+      mt_twist_chains_host(state625);
+      idx = 0;
+    }
+    out[i] = mt_temper(state625[idx++]);
+  }
+  state625[kMtN] = (uint32_t)idx;
   return CWQ_OK;
 }
 

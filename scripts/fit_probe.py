@@ -1,11 +1,15 @@
 """GPU ifit (add path) throughput: inserts/s of CobwebWrapper's
-incremental fit (CU scoring on libcwq, host-driven operation choice) for N(0,I) data
-(a flat tree: every insert scores all root children, the reference's O(N^2 D) case)
-and clustered data (hierarchical trees).  GPU only.
+incremental fit (the device-resident insert loop, cwq_fitdev.hip) for N(0,I) data (a flat
+tree: every insert scores all root children, the reference's O(N^2 D) case) and clustered
+data (hierarchical trees).  Rows go in chunks (one add_sentences call each, progress
+printed per chunk); with --compare-every, a short chunk at that cadence is also run with
+one workgroup (CWQ_FIT_HELPERS=0, the round-3 loop) and the tree it builds is checked
+against the chip-wide fit's (same rows, same random() state).  GPU only.
 
-    python scripts/fit_probe.py --n 2000 --dim 768 --clusters 0
+    python scripts/fit_probe.py --n 20000 --dim 768 --clusters 0 --chunk 2000 --compare-every 5000
 """
 import argparse
+import copy
 import os
 import random
 import sys
@@ -31,12 +35,28 @@ def depth_stats(root):
     return n, nint, mx, len(root.children)
 
 
+def arrays(root):
+    out, q, h = [], [root], 0
+    while h < len(q):
+        x = q[h]
+        h += 1
+        out.append(x)
+        q.extend(x.children)
+    pos = {id(x): i for i, x in enumerate(out)}
+    return ([-1 if x.parent is None else pos[id(x.parent)] for x in out], np.stack([x.mean for x in out]),
+            np.stack([x.meanSq for x in out]), [list(x.sentence_id) for x in out])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2000)
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--clusters", type=int, default=0, help="0: X ~ N(0,I); else Gaussian clusters (sd 0.3)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--chunk", type=int, default=0, help="rows per add_sentences call (0: one call)")
+    ap.add_argument("--compare-every", type=int, default=0,
+                    help="every this many rows, also time --compare-rows rows with one workgroup")
+    ap.add_argument("--compare-rows", type=int, default=100)
     ap.add_argument("--host", action="store_true", help="the host-driven fitter (CWQ_FIT_DEVICE=0)")
     args = ap.parse_args()
     if args.host:
@@ -53,14 +73,61 @@ def main():
     w = pkg.CobwebWrapper(corpus=None, corpus_embeddings=X[:8])   # warm up libcwq + the device pool
     torch.cuda.synchronize()
     random.seed(args.seed)
-    t0 = time.perf_counter()
-    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(args.n)], corpus_embeddings=X)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    chunk = args.chunk or args.n
+    w = None
+    t_all, done = 0.0, 0
+    mode = "host-driven" if args.host else f"device-resident, helpers={os.environ.get('CWQ_FIT_HELPERS', 'CUs-1')}"
+    next_cmp = args.compare_every
+    while done < args.n:
+        m = min(chunk, args.n - done)
+        if next_cmp and done >= next_cmp and done + args.compare_rows <= args.n:
+            # the same rows from the same tree and random() state with one workgroup
+            tree0, st0 = copy.deepcopy(w.tree), random.getstate()
+            rows = X[done:done + args.compare_rows]
+            fan = len(w.tree.root.children)
+            os.environ["CWQ_FIT_HELPERS"] = "0"
+            w1 = pkg.CobwebWrapper.__new__(pkg.CobwebWrapper)
+            w1.__dict__.update(w.__dict__)
+            w1.tree = tree0
+            w1.sentences, w1.sentence_to_node = list(w.sentences), dict(w.sentence_to_node)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            w1.add_sentences([f"s{i}" for i in range(done, done + len(rows))], rows)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter() - t0
+            st1 = random.getstate()
+            del os.environ["CWQ_FIT_HELPERS"]
+            random.setstate(st0)
+            t0 = time.perf_counter()
+            w.add_sentences([f"s{i}" for i in range(done, done + len(rows))], rows)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter() - t0
+            same = random.getstate() == st1 and all(
+                (np.array_equal(a, b) if isinstance(a, np.ndarray) else a == b)
+                for a, b in zip(arrays(w.tree.root), arrays(w1.tree.root)))
+            print(f"  at {done} rows (root fan-out {fan}): {len(rows)} inserts -- one workgroup "
+                  f"{1e3 * t1 / len(rows):.3f} ms/insert, chip-wide {1e3 * t2 / len(rows):.3f} ms/insert "
+                  f"= {t1 / t2:.1f}x; trees and random() state identical: {same}", flush=True)
+            done += len(rows)
+            t_all += t2
+            next_cmp += args.compare_every
+            del w1, tree0
+            continue
+        t0 = time.perf_counter()
+        if w is None:
+            w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(m)], corpus_embeddings=X[:m])
+        else:
+            w.add_sentences([f"s{i}" for i in range(done, done + m)], X[done:done + m])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        t_all += dt
+        done += m
+        fan = len(w.tree.root.children)
+        print(f"  rows {done - m}..{done}: {m / dt:.0f} inserts/s ({1e3 * dt / m:.3f} ms/insert), root fan-out now "
+              f"{fan}", flush=True)
     n, nint, mx, rootc = depth_stats(w.tree.root)
-    mode = "host-driven" if args.host else "device-resident"
-    print(f"ifit ({mode}) n={args.n} d={args.dim} clusters={args.clusters}: {dt:.2f} s  {args.n / dt:.0f} inserts/s  "
-          f"{1e3 * dt / args.n:.2f} ms/insert  tree: {n} nodes ({nint} internal), depth {mx}, root children {rootc}",
+    print(f"ifit ({mode}) n={args.n} d={args.dim} clusters={args.clusters}: {t_all:.2f} s  {args.n / t_all:.0f} inserts/s  "
+          f"{1e3 * t_all / args.n:.2f} ms/insert  tree: {n} nodes ({nint} internal), depth {mx}, root children {rootc}",
           flush=True)
 
 

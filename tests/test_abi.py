@@ -120,3 +120,21 @@ def test_device_mt19937_is_pythons_random(pkg):
     want = np.array([r.random() for _ in range(2000)])
     np.testing.assert_array_equal(out, want)
     assert tuple(int(v) for v in st) == r.getstate()[1]
+
+
+def test_device_mt19937_chain_twist_is_pythons_stream(pkg):
+    """The parallel generator of the chip-wide fit (mt_gen_wave: the twist as 227
+    independent chains over a wave's lanes, run here in its host form) gives Python's
+    getrandbits(32) outputs from the same state -- across many twists, from a mid-block
+    index -- and leaves random()'s state behind."""
+    import random
+    r = random.Random(77)
+    for _ in range(101):
+        r.random()
+    st = np.ascontiguousarray(np.asarray(r.getstate()[1], np.uint32))
+    n = 624 * 9 + 313
+    out = np.zeros(n, np.uint32)
+    assert pkg.lib().cwq_mt19937_words(st.ctypes.data_as(ctypes.c_void_p), n, out.ctypes.data_as(ctypes.c_void_p)) == 0
+    want = np.array([r.getrandbits(32) for _ in range(n)], np.uint32)
+    np.testing.assert_array_equal(out, want)
+    assert tuple(int(v) for v in st) == r.getstate()[1]

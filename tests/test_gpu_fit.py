@@ -85,13 +85,18 @@ def _tree_arrays(root):
             np.stack([n.meanSq for n in nodes]), [list(n.sentence_id) for n in nodes])
 
 
-@pytest.mark.parametrize("D,n,clusters", [(48, 1500, 12), (384, 600, 6), (768, 400, 0)])
-def test_device_fit_equals_host_fit(pkg, D, n, clusters, monkeypatch):
+@pytest.mark.parametrize("D,n,clusters,fork_min", [(48, 1500, 12, None), (384, 600, 6, None), (768, 400, 0, None),
+                                                   (64, 1200, 10, "2"), (96, 1500, 0, "64"), (768, 700, 0, "2")])
+def test_device_fit_equals_host_fit(pkg, D, n, clusters, fork_min, monkeypatch):
     """Device-resident ifit == host-driven ifit: structure, sentence placement, statistics
     bit for bit, and the random() stream position afterwards; with a batch split in two
-    add_sentences calls (state carried over)."""
+    add_sentences calls (state carried over).  The device loop forks levels of >= 256
+    children over every CU (flat N(0,I) rows: the root); fork_min forces forks at smaller
+    levels -- every level, split passes included, at "2"."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if fork_min:
+        monkeypatch.setenv("CWQ_FIT_FORK_MIN", fork_min)
     rng = np.random.default_rng(D + n)
     if clusters:
         C = rng.standard_normal((clusters, D)).astype(np.float32) * 2.0
@@ -236,3 +241,38 @@ def test_device_fit_small_pool_reloads_and_fallback(pkg, fail_at, monkeypatch):
         assert sum(st["host_rows"] for st in seen) > 0 and calls["n"] == loads + 1
     else:
         assert all(st["fallback"] is None for st in seen) and loads > 3
+
+
+def test_chip_wide_fit_flat_768_matches_oracle_1k_prefix(pkg, monkeypatch):
+    """The chip-wide device ifit on flat N(0,I) 768-d rows -- the reference's high fan-out
+    regime (every insert scores every root child, CobwebTorchNode.py:374-420) -- builds the
+    oracle's tree over a 1,000-insert prefix of a 20k-row set (oracle/cobweb_oracle.py
+    OTree.ifit, pinned to the reference's own trees G1/G5/G8): same structure, counts,
+    sentence placement and statistics bit for bit, and the same random() position; and the
+    one-workgroup loop (CWQ_FIT_HELPERS=0) builds the same tree."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import cobweb_oracle as O
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1")
+    X = np.random.default_rng(20_000).standard_normal((20_000, 768)).astype(np.float32)[:1000]
+    ot = O.OTree(768, rng=random.Random(8))
+    for i in range(len(X)):
+        ot.ifit(X[i]).sentence_id.append(i)
+    onodes = O.bfs_nodes(ot.root)
+    opos = {id(x): i for i, x in enumerate(onodes)}
+    want_r = ot.rng.random()
+    for helpers in (None, "0"):
+        if helpers is None:
+            monkeypatch.delenv("CWQ_FIT_HELPERS", raising=False)
+        else:
+            monkeypatch.setenv("CWQ_FIT_HELPERS", helpers)
+        random.seed(8)
+        w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(len(X))], corpus_embeddings=X)
+        p, cnt, mean, m2, sids = _tree_arrays(w.tree.root)
+        np.testing.assert_array_equal(p, [-1 if x.parent is None else opos[id(x.parent)] for x in onodes])
+        np.testing.assert_array_equal(cnt, np.array([x.count for x in onodes], np.float32))
+        assert sids == [list(x.sentence_id) for x in onodes]
+        np.testing.assert_array_equal(mean, np.stack([x.mean for x in onodes]))
+        np.testing.assert_array_equal(m2, np.stack([x.meanSq for x in onodes]))
+        assert random.random() == want_r
+    assert len(ot.root.children) > 900
