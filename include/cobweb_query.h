@@ -106,6 +106,13 @@ int cwq_index_destroy(cwq_index* idx);
  * mean/var tensors after cwq_index_create). */
 int cwq_index_info(const cwq_index* idx, int64_t* out8);
 
+/* How the filters centre their rows (no reference counterpart: a property of this
+ * index's bf16 filter operands): out[0] = 1 when isotropic rows are stored centred at
+ * their depth-1 ancestor's mean (clustered trees, cwq_group.hip; CWQ_GROUP_CENTRE=0 / 1 at
+ * index creation: off / on wherever it applies), out[1] = groups, out[2] = group-centred
+ * rows, out[3] = 1 when the per-call int8 panel was built. */
+int cwq_index_filter_info(const cwq_index* idx, int64_t* out4);
+
 /*
  * "Cobweb Fast" batched top-k (A6).  Replaces CobwebWrapper.cobweb_predict_indexed
  * (CobwebWrapper.py:210-265, alias cobweb_predict_fast :428-433) for nq queries:

@@ -121,6 +121,16 @@ struct cwq_index {
   std::vector<int> cat_uni_prefix;
   float cat_dconst = 0.f;
   int n_samp = 0, ld_s = 0;                    // sample rows, padded to 256
+  // group-centred filter rows (cwq_group.hip; clustered trees): the isotropic rows below a
+  // depth-1 internal node g are centred at its mean grp_c[g]; grp_par[p] = the group of
+  // internal node p's rows (-1: root-centred), grp_F[p] = hs / invL of p's rows (Fast),
+  // grp_Fc[p] = their categorize hs.  grp_mode: the filters read the shifted prefix tables.
+  bool grp_mode = false;
+  int G = 0;
+  int64_t n_grp_rows = 0;
+  float* grp_c = nullptr;
+  int* grp_par = nullptr;
+  double *grp_F = nullptr, *grp_Fc = nullptr;
   // internal-node bounds (hierarchical trees): bf16 operand rows, their RowF constants,
   // row-major fp32 A/B copies for the exact chain in final_kernel.  int_path (default):
   // the Fast filter reads the path prefix P of leaf parents only, so there is one row per
@@ -299,27 +309,126 @@ float round_up_f(double v) {
 
 // bf16 operands, fp32 rerank copy, per-row and per-tile bound constants, and the
 // strided threshold sample of the isotropic rows.
+// Group-centred rows (cwq_group.hip): which isotropic rows get centred at their depth-1
+// internal ancestor's mean.  A group qualifies when every one of its rows is at most twice
+// as far from the group mean as from the root mean (then the rounding terms stay within the
+// bound's eps and beta margins) and all rows of each of its parents share the key coefficients (the
+// group term is folded into the parent's prefix); the mode is on when the qualifying
+// groups cut the rows' summed squared norms at least 4x (CWQ_GROUP_CENTRE=0 / 1: off /
+// every qualifying group).  rgrp[r] = group index or -1.
+int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const std::vector<RowMeta>& meta,
+                const std::vector<int>& row_par, const std::vector<int64_t>& int_nodes, const std::vector<int>& par_int,
+                std::vector<int>& rgrp, hipStream_t s) {
+  int rc;
+  const int NLi = ix->NL_iso, NI = ix->NI, D = ix->D;
+  rgrp.assign(NLi, -1);
+  const char* ge = getenv("CWQ_GROUP_CENTRE");
+  const int force = ge && *ge ? atoi(ge) : -1;
+  if (force == 0 || NI < 2 || NLi == 0) return CWQ_OK;
+  // group of every internal node: its depth-1 ancestor (internal ids are BFS: parents first)
+  std::vector<int> gint(NI, -1);
+  std::vector<int64_t> gnode;
+  for (int i = 1; i < NI; ++i) {
+    if (par_int[i] == 0) {
+      gint[i] = (int)gnode.size();
+      gnode.push_back(int_nodes[i]);
+    } else if (par_int[i] > 0) {
+      gint[i] = gint[par_int[i]];
+    }
+  }
+  const int G = (int)gnode.size();
+  if (G == 0) return CWQ_OK;
+  std::vector<int> cand(NLi, -1);
+  for (int r = 0; r < NLi; ++r) cand[r] = row_par[r] > 0 ? gint[row_par[r]] : -1;
+  int64_t* d_gnode = nullptr;
+  int* d_cand = nullptr;
+  float* cent = nullptr;
+  double *r2 = nullptr, *g2 = nullptr;
+  if ((rc = ix->upload(&d_gnode, gnode, s)) || (rc = ix->upload(&d_cand, cand, s)) ||
+      (rc = ix->alloc(&cent, (size_t)G * D)) || (rc = ix->alloc(&r2, NLi)) || (rc = ix->alloc(&g2, NLi)))
+    return rc;
+  HIPCHK(launch_gather_rows_f32(mean, D, d_gnode, G, cent, s));
+  HIPCHK(launch_group_norms(mean, D, d_rows, NLi, ix->iso_c, cent, d_cand, r2, g2, s));
+  std::vector<double> hr2(NLi), hg2(NLi);
+  HIPCHK(hipMemcpyAsync(hr2.data(), r2, (size_t)NLi * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hg2.data(), g2, (size_t)NLi * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<char> gok(G, 1);
+  std::vector<float> pcw(NI, NAN), piv(NI, NAN), pinvL(NI, NAN);
+  for (int r = 0; r < NLi; ++r) {
+    const int g = cand[r];
+    if (g < 0) continue;
+    if (!(hg2[r] <= 4.0 * hr2[r])) gok[g] = 0;   // |M_g| <= 2 |M_0|: the rounding cross term stays in eps
+    const int p = row_par[r];
+    if (std::isnan(pcw[p])) {
+      pcw[p] = meta[r].cw;
+      piv[p] = meta[r].iv;
+      pinvL[p] = meta[r].invL;
+    } else if (pcw[p] != meta[r].cw || piv[p] != meta[r].iv || pinvL[p] != meta[r].invL) {
+      gok[g] = 0;
+    }
+  }
+  double sum_root = 0.0, sum_sel = 0.0;
+  for (int r = 0; r < NLi; ++r) {
+    sum_root += hr2[r];
+    sum_sel += (cand[r] >= 0 && gok[cand[r]]) ? hg2[r] : hr2[r];
+  }
+  const bool on = force == 1 ? sum_sel < sum_root : sum_sel * 4.0 <= sum_root;
+  if (!on) return CWQ_OK;
+  for (int r = 0; r < NLi; ++r) {
+    rgrp[r] = (cand[r] >= 0 && gok[cand[r]]) ? cand[r] : -1;
+    ix->n_grp_rows += rgrp[r] >= 0;
+  }
+  std::vector<int> gpar(NI, -1);
+  std::vector<double> F(NI, 0.0), Fc(NI, 0.0);
+  for (int p = 1; p < NI; ++p) {
+    const int g = gint[p];
+    if (g < 0 || !gok[g] || std::isnan(pcw[p])) continue;
+    gpar[p] = g;
+    const double hs = (double)(float)(-0.5 * (double)pcw[p] * (double)piv[p]);   // RowF.hs (fp32)
+    const double hsc = (double)(float)(-0.5 * (double)piv[p]);                    // categorize RowF.hs
+    F[p] = hs / (double)pinvL[p];
+    Fc[p] = hsc;
+  }
+  ix->grp_mode = true;
+  ix->G = G;
+  ix->grp_c = cent;
+  if ((rc = ix->upload(&ix->grp_par, gpar, s)) || (rc = ix->upload(&ix->grp_F, F, s)) ||
+      (rc = ix->upload(&ix->grp_Fc, Fc, s)))
+    return rc;
+  HIPCHK(hipStreamSynchronize(s));
+  return CWQ_OK;
+}
+
 int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const std::vector<RowMeta>& meta,
-                 const std::vector<int>& row_par, const std::vector<int>& row_flags, hipStream_t s) {
+                 const std::vector<int>& row_par, const std::vector<int>& row_flags,
+                 const std::vector<int64_t>& int_nodes, const std::vector<int>& par_int, hipStream_t s) {
   int rc;
   const int DP = ix->DP, D = ix->D, NLi = ix->NL_iso;
   ix->DPB = fgemm_dpb(D);   // whole fgemm stages (cwq_mfma.hip)
   const int DPB = ix->DPB;
   ix->ld_f = round_up(NLi, kFgTile);
   const int64_t ld = ix->ld_f;
-  float *n2 = nullptr, *nlo = nullptr, *nhi = nullptr;
+  float *n2 = nullptr, *nlo = nullptr, *nhi = nullptr, *nm = nullptr;
   if ((rc = ix->alloc(&ix->iso_Mf, (size_t)DP * ld))) return rc;
   if ((rc = ix->alloc(&ix->iso_Mb, (size_t)DPB * ld))) return rc;
   if ((rc = ix->alloc(&n2, ld))) return rc;
   if ((rc = ix->alloc(&nlo, ld))) return rc;
   if ((rc = ix->alloc(&nhi, ld))) return rc;
+  if ((rc = ix->alloc(&nm, ld))) return rc;
   if ((rc = ix->alloc(&ix->iso_c, D))) return rc;
   HIPCHK(hipMemcpyAsync(ix->iso_c, mean, (size_t)D * 4, hipMemcpyDeviceToDevice, s));   // root mean
-  HIPCHK(launch_rows_prep(mean, D, d_rows, NLi, ix->iso_c, DP, DPB, ld, ix->iso_Mf, ix->iso_Mb, n2, nlo, nhi, s));
-  std::vector<float> hn2(ld), hlo(ld), hhi(ld);
+  std::vector<int> rgrp;
+  if ((rc = plan_groups(ix, mean, d_rows, meta, row_par, int_nodes, par_int, rgrp, s))) return rc;
+  int* d_rgrp = nullptr;
+  if (ix->grp_mode && (rc = ix->upload(&d_rgrp, rgrp, s))) return rc;
+  HIPCHK(launch_rows_prep(mean, D, d_rows, NLi, ix->iso_c, DP, DPB, ld, ix->iso_Mf, ix->iso_Mb, n2, nlo, nhi, s,
+                          ix->grp_c, d_rgrp, nm));
+  std::vector<float> hn2(ld), hlo(ld), hhi(ld), hnm(ld);
   HIPCHK(hipMemcpyAsync(hn2.data(), n2, ld * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(hlo.data(), nlo, ld * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(hhi.data(), nhi, ld * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hnm.data(), nm, ld * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const FiltConsts fc = filt_consts(DPB);
   // per-row and per-tile constants.  Fast key (cat = false): pi + hs*S + hl with
@@ -349,12 +458,17 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
       const double ldet = cat ? (double)(m.logdet + dfull) : (double)m.logdet;   // fp32 add, as the scan
       const double hs = -0.5 * cw * (double)m.iv, hl = -0.5 * cw * ldet;
       const double g = cw * (double)m.iv;
-      f.beta = round_up_f((double)hlo[r] + fc.gamma * (double)hhi[r]);
-      f.delta = round_up_f((double)hhi[r] + (double)hlo[r]);
+      const bool grow = ix->grp_mode && rgrp[r] >= 0;
+      // group-centred rows: the fp32 rounding of M = fl(mu - c_g) enters the dot through
+      // |x'| |M| -- 2^-23 |M| on both split norms covers it (cwq_group.hip)
+      const double ge = grow ? std::ldexp((double)hnm[r], -23) * (1.0 + std::ldexp(1.0, -20)) : 0.0;
+      f.beta = round_up_f((double)hlo[r] + fc.gamma * (double)hhi[r] + ge);
+      f.delta = round_up_f((double)hhi[r] + (double)hlo[r] + ge);
       f.rn2 = hn2[r];
       f.hs = (float)hs;
       f.hl = (float)hl;
-      f.invL = cat ? 0.f : m.invL;
+      // categorize reads a prefix term only for group-centred rows: their group term
+      f.invL = cat ? (grow ? 1.f : 0.f) : m.invL;
       f.par = row_par[r];
       gr[r] = g;
       if (g > 0.0 && std::isfinite(g) && std::isfinite(hl)) {
@@ -372,17 +486,21 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
       TileF& T = tf[t];
       T = TileF{1, -1, 1.f, 1.f, 0.f, 0.f, -1, 0.f};
       bool first = true, same_par = true;
-      int plo = INT32_MAX, phi = -1;
+      int plo = INT32_MAX, phi = -1, tgrp = -1;
       for (int64_t r = (int64_t)t * kFgTile; r < (int64_t)(t + 1) * kFgTile; ++r) {
         if (rf[r].par < -1) continue;
         const double g = gr[r];
         if (!(g > 0.0) || !std::isfinite(g) || !std::isfinite(rf[r].R0)) T.uniform = 0;
+        // categorize tiles: parent-free, or (group-centred rows) all rows of one group,
+        // whose term any of their parents carries
+        const int cg = ix->grp_mode && r < NLi ? rgrp[r] : -1;
         if (first) {
-          T.par = cat ? -1 : rf[r].par;
+          T.par = cat ? (cg >= 0 ? rf[r].par : -1) : rf[r].par;
           T.invL = rf[r].invL;
           T.g = (float)g;
+          tgrp = cg;
           first = false;
-        } else if (rf[r].invL != T.invL || (float)g != T.g) {
+        } else if (rf[r].invL != T.invL || (float)g != T.g || (cat && cg != tgrp)) {
           T.uniform = 0;
         }
         if (!cat && rf[r].par != T.par) same_par = false;
@@ -620,7 +738,8 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
     meta[r].iv = ivh[r];
   }
   if ((rc = ix->upload(&ix->row_meta, meta, s))) return rc;
-  if (ix->NL_iso > 0 && (rc = build_filter(ix.get(), mean, d_rows, meta, row_par, row_flags, s))) return rc;
+  if (ix->NL_iso > 0 && (rc = build_filter(ix.get(), mean, d_rows, meta, row_par, row_flags, int_nodes, par_int, s)))
+    return rc;
   if ((rc = ix->upload(&ix->row_par, row_par, s))) return rc;
   if ((rc = ix->upload(&ix->row_flags, row_flags, s))) return rc;
   if ((rc = ix->upload(&ix->row_bfs, row_bfs, s))) return rc;
@@ -788,6 +907,15 @@ extern "C" int cwq_index_info(const cwq_index* idx, int64_t* o) {
   return CWQ_OK;
 }
 
+extern "C" int cwq_index_filter_info(const cwq_index* idx, int64_t* o) {
+  if (!idx || !o) return fail(CWQ_ERR_ARG, "NULL argument");
+  o[0] = idx->grp_mode ? 1 : 0;
+  o[1] = idx->G;
+  o[2] = idx->n_grp_rows;
+  o[3] = idx->i8_state > 0 ? 1 : 0;
+  return CWQ_OK;
+}
+
 // Scan configuration of one query call (cwq_kernels.hip scan_cfg_begin): fixed from the
 // call's total query count, so every chunk and workspace estimate of the call agrees.
 struct ScanCfgScope {
@@ -812,7 +940,21 @@ struct Chunk {
   int64_t ldP = 1;
   int pT = 0;
   const float4* qi2 = nullptr;   // path-sum bounds: the queries' [x'^2, x'] norms (PathB)
+  // group-centred rows (grp_mode): the filters' prefix tables [nq_pad][NI] -- Fast
+  // [Pg_lo, Pg_hi] and categorize [Pc_lo, Pc_hi] -- and the per-(query, group) shifts
+  float *Pg_lo = nullptr, *Pg_hi = nullptr, *Pc_lo = nullptr, *Pc_hi = nullptr;
+  double* gsh = nullptr;
 };
+
+// The group-centred rows' prefix tables of a chunk (after the exact internal pass wrote
+// c.P): q = the chunk's [nq][D] queries.  No-op without grp_mode.
+int group_tables(cwq_index* ix, Chunk& c, const float* q, bool cat, hipStream_t s) {
+  if (!ix->grp_mode || ix->NI == 0) return CWQ_OK;
+  HIPCHK(launch_group_prefixes(q, c.nq, ix->D, ix->iso_c, ix->grp_c, ix->G, c.P, c.ldP, ix->NI, ix->grp_par, ix->grp_F,
+                               ix->grp_Fc, c.gsh, c.Pg_lo, c.Pg_hi, cat ? c.Pc_lo : nullptr, cat ? c.Pc_hi : nullptr,
+                               s));
+  return CWQ_OK;
+}
 
 // The path-sum dots of a chunk after run_internal_bounds (int_path), or none.
 PathB path_b(const cwq_index* ix, const Chunk& c) {
@@ -906,7 +1048,8 @@ void fg_groups(int n_qt, int& qg, int& rg);
 // internal pass (CWQ_INT_BOUND=0 disables).  Anisotropic leaf rows need exact prefixes
 // (the exact scan reads them), so such trees keep the exact pass.
 bool use_int_bounds(const cwq_index* ix) {
-  if (!ix->int_bounds || ix->NL_an > 0) return false;
+  // group-centred rows need the exact prefixes (their group terms are folded into them)
+  if (!ix->int_bounds || ix->NL_an > 0 || ix->grp_mode) return false;
   const char* e = getenv("CWQ_INT_BOUND");
   return !(e && *e && atoi(e) == 0);
 }
@@ -1098,8 +1241,12 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
 // Workspace for one chunk: X + internal arrays.
 // Workspace of one chunk: X + the [nq][NI] internal arrays -- S_int and P always; BF and
 // LPF (path bottleneck, full log_prob) only for categorize / log_prob (`full`).
+size_t group_bytes_per_query(const cwq_index* ix) {
+  return ix->grp_mode ? (size_t)ix->G * 8 + (size_t)4 * std::max(ix->NI, 1) * 4 + 5 * 256 : 0;
+}
 size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad, bool full = true) {
-  return (size_t)nq_pad * ix->DP * 4 + (full ? 4 : 2) * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256;
+  return (size_t)nq_pad * ix->DP * 4 + (full ? 4 : 2) * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256 +
+         (size_t)nq_pad * group_bytes_per_query(ix);
 }
 
 void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
@@ -1116,6 +1263,13 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
       c.BF = b.take<float>(n);
       c.LPF = b.take<float>(n);
     }
+    if (ix->grp_mode) {
+      c.gsh = b.take<double>((size_t)c.nq_pad * ix->G);
+      c.Pg_lo = b.take<float>(n);
+      c.Pg_hi = b.take<float>(n);
+      c.Pc_lo = b.take<float>(n);
+      c.Pc_hi = b.take<float>(n);
+    }
   }
 }
 
@@ -1123,7 +1277,8 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
 // default -- 288 GB of HBM hold it beside the largest indexes; CWQ_WS_BUDGET_MB; at
 // least 128 queries).
 int64_t chunk_queries(const cwq_index* ix, int64_t nq, size_t per_query_extra, bool full = true) {
-  const size_t per_q = (size_t)ix->DP * 4 + (full ? 4 : 2) * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra;
+  const size_t per_q = (size_t)ix->DP * 4 + (full ? 4 : 2) * (size_t)std::max(ix->NI, 1) * 4 + per_query_extra +
+                       group_bytes_per_query(ix);
   // budget: CWQ_WS_BUDGET_MB, else 40% of what the device has free (plus the workspace
   // already held), between 2 and 48 GiB -- one chunk for 10k queries over trees with
   // ~350k internal nodes (whose [lo, hi] prefix matrices alone are 28 GB), which beats two
@@ -1281,7 +1436,7 @@ bool use_stream(const cwq_index* ix, int64_t nq, int k) {
 constexpr int64_t kI8MinBytes = (int64_t)384 << 20;
 bool ensure_i8(cwq_index* ix, hipStream_t s) {
   const char* e = getenv("CWQ_STREAM_I8");
-  if (e && *e && atoi(e) == 0) return false;
+  if ((e && *e && atoi(e) == 0) || ix->grp_mode) return false;   // the int8 rows are root-centred
   if (!(e && *e && atoi(e) == 1) && (int64_t)ix->NL_iso * ix->DPB < kI8MinBytes) return false;
   if (ix->i8_state) return ix->i8_state > 0;
   ix->i8_state = -1;
@@ -1399,6 +1554,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (i8) HIPCHK(launch_query_prep_i8(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xq, qinfo8, s));
     HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
   }
+  if ((rc = group_tables(ix, c, q, false, s))) return rc;
   const FiltConsts fc = filt_consts(ix->DPB);
   StreamArgs a;
   memset(&a, 0, sizeof(a));
@@ -1414,6 +1570,10 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.P = c.P ? c.P : ix->dummy;
   a.pb = ib ? path_b(ix, c) : PathB{nullptr, 0, nullptr, nullptr};
   a.Phi = ib && !a.pb.dot ? c.S_int : nullptr;
+  if (ix->grp_mode && c.Pg_lo) {   // group-centred rows: the shifted prefix tables
+    a.P = c.Pg_lo;
+    a.Phi = c.Pg_hi;
+  }
   a.ldP = c.ldP;
   a.pT = c.pT;
   a.eps_n = (float)fc.eps_n;
@@ -1563,8 +1723,10 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   float2* pmm = (!cat && ix->n_multi_tiles) ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
   HIPCHK(launch_query_prep(qsrc, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
   const PathB pb = (!cat && ib) ? path_b(ix, c) : PathB{nullptr, 0, nullptr, nullptr};
+  const bool grp = ix->grp_mode && c.Pg_lo;   // group-centred rows: the shifted prefix tables
   if (pmm)   // multi-parent tiles: parent-prefix range per (tile, query) for the pretest
-    HIPCHK(launch_tile_prange(c.P, ib ? c.S_int : nullptr, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s, &pb));
+    HIPCHK(launch_tile_prange(grp ? c.Pg_lo : c.P, grp ? c.Pg_hi : ib ? c.S_int : nullptr, c.ldP, c.pT, nqc, ix->iso_tf,
+                              n_rt, pmm, nqf, s, &pb));
   FgArgs g;
   memset(&g, 0, sizeof(g));
   g.DPB = ix->DPB;
@@ -1583,6 +1745,11 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.P = cat ? (c.BF ? c.BF : ix->dummy) : (c.P ? c.P : ix->dummy);
   g.pb = pb;
   g.Phi = (!cat && ib && !pb.dot) ? c.S_int : nullptr;
+  if (grp) {
+    g.P = cat ? c.Pc_lo : c.Pg_lo;
+    g.Phi = cat ? c.Pc_hi : c.Pg_hi;
+    g.BFt = cat ? (c.BF ? c.BF : ix->dummy) : nullptr;
+  }
   g.ldP = cat ? std::max(ix->NI, 1) : c.ldP;
   g.pT = cat ? 0 : c.pT;
   g.gamma = (float)fc.gamma;
@@ -1717,6 +1884,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     } else if ((rc = run_internal(ix, c, s, false))) {
       return rc;
     }
+    if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, false, s))) return rc;
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
     if (!general) {
       float* pkey = b.take<float>((size_t)nq_pad * slabs * K);
@@ -2008,6 +2176,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     int* status = b.take<int>((size_t)nq_pad);
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if ((rc = run_internal(ix, c, s))) return rc;
+    if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, true, s))) return rc;
     int nst = 0;
     std::vector<char> fbad(nqc, 0);
     if (filt) {

@@ -24,7 +24,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <unistd.h>
 #include <string.h>
 
 #include <memory>
@@ -136,6 +138,8 @@ struct FitDev {
   float* pvec;                  // [3][D] the job's reference vectors (mean, var, log var)
   uint32_t* rnd;                // [2*cap + 8] a level's tempered MT outputs (the sort's draws)
   int fork_min;                 // fork a level's KL pass when it has >= fork_min children
+  uint64_t spin_ticks;          // bound of every spin (100 MHz steady counter ticks)
+  int* dbg;                     // [16] progress words (read back by the host on FD_HANG)
 };
 
 constexpr int kFdThreads = 1024;
@@ -147,27 +151,35 @@ constexpr int kFdWaveClaim = 4; // children per claim of a master wave
 constexpr int kFdHelperPer = 2; // children per helper wave per workgroup claim
 constexpr int kFdForkMin = 256; // default fork threshold (children of a level)
 enum { FD_OK = 0, FD_ROOM = 1, FD_FULL = 2, FD_HANG = 3 };
-// bounded spins (s_memrealtime runs at 100 MHz): a helper with no new job for this long
-// leaves (the master never depends on helpers: it claims work itself); the master gives up
-// a join after this long (status FD_HANG)
-constexpr uint64_t kFdIdleTicks = 2000000000ull;   // 20 s
-constexpr uint64_t kFdJoinTicks = 2000000000ull;
+// bounded spins (the steady counter runs at 100 MHz): a helper with no new job for
+// spin_ticks leaves (the master never depends on helpers: it claims work itself); the master
+// gives up a join after spin_ticks (status FD_HANG).  Default 20 s; CWQ_FIT_SPIN_MS.
+constexpr uint64_t kFdSpinTicks = 2000000000ull;
+// dbg words: 0 row, 1 forks, 2 last fork size, 3 phase, 4 done at the last join, 5 helper
+// job starts, 6 helper exits, 7 helper claims
 
-// The job a forked level hands to the helper workgroups: zeroed before every launch
-// (cwq_fit_insert).  epoch = job number (1, 2, ...), polled by the helpers; the claim /
-// completion counters live in a ring by epoch, so a helper that is late for job e can
-// only ever touch job e's own counters.
+// The job a forked level hands to the helper workgroups.  Every word here is shared
+// between workgroups and is only ever accessed by agent-scope atomics (loads, stores,
+// adds) -- never plain (cdna_hip_programming.md §6 Guideline 16): the block is zeroed by
+// a memset before every launch; epoch = job number (1, 2, ...), polled by the helpers; the
+// job's descriptor and its claim / completion counters live in rings by epoch (each
+// counter on a 128-B line of its own), so a helper late for job e only ever touches job
+// e's own words.
+struct FdDesc {
+  int type;        // 0: U, T of the children arena[base .. base+n) vs (P + x); 1: KL(c || P) of jobs[0..n)
+  int n;
+  int kofs;        // type 1: output offset in kres
+  int pad;
+  int64_t base;
+  int64_t row;     // the row being inserted (x = X[row])
+};
 struct FdJob {
   int epoch;
   int quit;
-  int type;        // 0: U, T of the children arena[base .. base+n) vs (P + x); 1: KL(c || P) of jobs[0..n)
-  int n;
-  int64_t base;
-  int64_t row;     // the row being inserted (x = X[row])
-  int kofs;        // type 1: output offset in kres
-  int pad[25];
-  int next[kFdRing];
-  int done[kFdRing];
+  int pad0[30];
+  FdDesc desc[kFdRing];
+  int next[kFdRing][32];
+  int done[kFdRing][32];
 };
 
 struct FdShared {
@@ -192,6 +204,16 @@ __device__ __forceinline__ int ld_agent(const int* p) {
 }
 __device__ __forceinline__ void st_agent(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t ld_agent64(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent64(int64_t* p, int64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent_f(const float* p) {   // L1-bypassing (sc1) load
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ __forceinline__ void st_agent_f(float* p, float v) {   // write-through (sc1) store
   __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -219,7 +241,9 @@ __device__ __forceinline__ void mt_gen_wave(uint32_t* mt, uint32_t* tmp, int& id
         if (t + 454 < kMtN - 1) tmp[t + 454] = nw[2];
       }
       wave_sync();
-      if (lane == 0) tmp[kMtN - 1] = mt_step(mt[kMtN - 1], tmp[0], tmp[kMtM - 1]);
+      const uint32_t last = mt_step(mt[kMtN - 1], tmp[0], tmp[kMtM - 1]);   // every lane: the same word
+      wave_sync();
+      tmp[kMtN - 1] = last;
       wave_sync();
       for (int i = lane; i < kMtN; i += 64) mt[i] = tmp[i];
       wave_sync();
@@ -477,16 +501,16 @@ __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, 
 // one child of a job (ONE wave): its KL terms to kres by write-through stores
 __device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh, int type, int64_t base, int kofs, int j,
                                              int lane) {
+  // the butterfly leaves the sums in every lane: every lane stores the same words (no
+  // lane-divergent region inside the claim loops -- cf. fd_fork)
   if (type == 0) {
     float U, T;
     fd_kl_UT(f, sh, f.arena[base + j], lane, U, T);
-    if (lane == 0) {
-      st_agent_f(&f.kres[2 * j], U);
-      st_agent_f(&f.kres[2 * j + 1], T);
-    }
+    st_agent_f(&f.kres[2 * j], U);
+    st_agent_f(&f.kres[2 * j + 1], T);
   } else {
     const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
-    if (lane == 0) st_agent_f(&f.kres[kofs + j], K);
+    st_agent_f(&f.kres[kofs + j], K);
   }
 }
 
@@ -512,8 +536,11 @@ __device__ __forceinline__ bool fd_rel_before(float g1, float n1, double r1, int
 __device__ __forceinline__ void fd_help_job(const FitDev& f, FdShared& sh, const float* X, int e) {
   FdJob* job = f.job;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, D = f.D;
-  const int type = job->type, n = job->n, kofs = job->kofs;
-  const int64_t base = job->base, row = job->row;
+  const int slot = e % kFdRing;
+  FdDesc* dd = &job->desc[slot];
+  const int type = ld_agent(&dd->type), n = ld_agent(&dd->n), kofs = ld_agent(&dd->kofs);
+  const int64_t base = ld_agent64(&dd->base), row = ld_agent64(&dd->row);
+  if (n <= 0 || n > 3 * f.cap || base < 0 || row < 0) return;   // never: a descriptor not (yet) seen
   float* mu = type ? sh.muP : sh.mu2;
   float* v = type ? sh.vP : sh.v2;
   float* lv = type ? sh.lvP : sh.lv2;
@@ -524,19 +551,29 @@ __device__ __forceinline__ void fd_help_job(const FitDev& f, FdShared& sh, const
     if (type == 0) sh.x[d] = X[row * D + d];
   }
   __syncthreads();
-  const int slot = e % kFdRing;
   constexpr int per = kFdWaves * kFdHelperPer;
   for (;;) {
-    if (tid == 0) sh.ci[0] = ld_agent(&job->epoch) == e ? atomicAdd(&job->next[slot], per) : n;
+    // wave 0 claims for the workgroup: every lane takes part in the atomic (lane 0 adds
+    // `per`, the others 0) -- no lane-divergent region in these loops: the compiler's
+    // restructuring of one (an atomic under `if (lane == 0)` plus a readlane in the loop
+    // head) re-ran an iteration without its claim
+    if (wave == 0) {
+      const bool live = ld_agent(&job->epoch) == e;
+      const int v = atomicAdd(&job->next[slot][0], (lane == 0 && live) ? per : 0);
+      sh.ci[0] = live ? __builtin_amdgcn_readlane(v, 0) : n;
+    }
     __syncthreads();
-    const int j0 = sh.ci[0];
+    const int j0 = __builtin_amdgcn_readfirstlane(sh.ci[0]);   // uniform loop control
     __syncthreads();
     if (j0 >= n) break;
     const int j1 = j0 + per < n ? j0 + per : n;
     for (int j = j0 + wave; j < j1; j += kFdWaves) fd_job_child(f, sh, type, base, kofs, j, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave's stores drained
     __syncthreads();
-    if (tid == 0) atomicAdd(&job->done[slot], j1 - j0);
+    if (wave == 0) {
+      atomicAdd(&job->done[slot][0], lane == 0 ? j1 - j0 : 0);
+      atomicAdd(&f.dbg[7], lane == 0 ? 1 : 0);
+    }
   }
 }
 
@@ -546,7 +583,7 @@ __device__ __forceinline__ void fd_helper(const FitDev& f, FdShared& sh, const f
   for (;;) {
     if (tid == 0) {
       int e = -1;
-      const uint64_t t0 = wall_clock64();
+      const uint64_t t0 = (uint64_t)wall_clock64();
       for (;;) {
         if (ld_agent(&f.job->quit)) break;
         const int ep = ld_agent(&f.job->epoch);
@@ -554,7 +591,7 @@ __device__ __forceinline__ void fd_helper(const FitDev& f, FdShared& sh, const f
           e = ep;
           break;
         }
-        if (wall_clock64() - t0 > kFdIdleTicks) break;   // bounded: the master needs no helper
+        if ((uint64_t)wall_clock64() - t0 > f.spin_ticks) break;   // bounded: the master needs no helper
         __builtin_amdgcn_s_sleep(2);
       }
       if (e > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -562,10 +599,14 @@ __device__ __forceinline__ void fd_helper(const FitDev& f, FdShared& sh, const f
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int e = sh.ci[1];
+    const int e = __builtin_amdgcn_readfirstlane(sh.ci[1]);
     __syncthreads();
-    if (e <= 0) return;
+    if (e <= 0) {
+      if (tid == 0) atomicAdd(&f.dbg[6], 1);
+      return;
+    }
     seen = e;
+    if (tid == 0) atomicAdd(&f.dbg[5], 1);
     fd_help_job(f, sh, X, e);
   }
 }
@@ -589,24 +630,28 @@ __device__ __forceinline__ bool fd_fork(const FitDev& f, FdShared& sh, int64_t r
   const int e = sh.epoch + 1;
   const int slot = e % kFdRing;
   if (tid == 0) {
-    job->type = type;
-    job->n = n;
-    job->base = base;
-    job->row = row;
-    job->kofs = kofs;
-    job->next[slot] = 0;
-    job->done[slot] = 0;
+    FdDesc* dd = &job->desc[slot];
+    st_agent(&dd->type, type);
+    st_agent(&dd->n, n);
+    st_agent(&dd->kofs, kofs);
+    st_agent64(&dd->base, base);
+    st_agent64(&dd->row, row);
+    st_agent(&job->next[slot][0], 0);
+    st_agent(&job->done[slot][0], 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {   // publish: agent release of everything the master wrote, then the epoch
+    st_agent(&f.dbg[1], e);
+    st_agent(&f.dbg[2], n);
+    st_agent(&f.dbg[3], 1);
     sh.epoch = e;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     st_agent(&job->epoch, e);
   }
   if (wave == 0 && nrnd > 0) {
-    int idx = __shfl(mt_idx, 0);
+    int idx = __builtin_amdgcn_readlane(mt_idx, 0);
     mt_gen_wave(sh.mt, sh.mtn, idx, nrnd, f.rnd, lane);
     if (lane == 0) mt_idx = idx;
   }
@@ -614,28 +659,30 @@ __device__ __forceinline__ bool fd_fork(const FitDev& f, FdShared& sh, int64_t r
     const float K = fd_kl_new(f, sh, lane);
     if (lane == 0) f.kres[2 * n] = K;
   }
-  for (;;) {
-    int j0 = 0;
-    if (lane == 0) j0 = atomicAdd(&job->next[slot], kFdWaveClaim);
-    j0 = __shfl(j0, 0);
+  for (;;) {   // per wave; every lane in every atomic (fd_help_job)
+    const int v = atomicAdd(&job->next[slot][0], lane == 0 ? kFdWaveClaim : 0);
+    const int j0 = __builtin_amdgcn_readlane(v, 0);   // wave-uniform (scalar) loop control
     if (j0 >= n) break;
     const int j1 = j0 + kFdWaveClaim < n ? j0 + kFdWaveClaim : n;
     for (int j = j0; j < j1; ++j) fd_job_child(f, sh, type, base, kofs, j, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) atomicAdd(&job->done[slot], j1 - j0);
+    atomicAdd(&job->done[slot][0], lane == 0 ? j1 - j0 : 0);
   }
   __syncthreads();
   if (tid == 0) {
-    const uint64_t t0 = wall_clock64();
+    st_agent(&f.dbg[3], 2);
+    const uint64_t t0 = (uint64_t)wall_clock64();
     int ok = 1;
-    while (ld_agent(&job->done[slot]) < n) {
-      if (wall_clock64() - t0 > kFdJoinTicks) {
+    while (ld_agent(&job->done[slot][0]) < n) {
+      if ((uint64_t)wall_clock64() - t0 > f.spin_ticks) {
         ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    st_agent(&f.dbg[4], ld_agent(&job->done[slot][0]));
+    st_agent(&f.dbg[3], ok ? 3 : 4);
     sh.ci[1] = ok;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -721,6 +768,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       break;
     }
     for (int d = tid; d < D; d += kFdThreads) sh.x[d] = X[row * D + d];
+    if (tid == 0 && f.dbg) st_agent(&f.dbg[0], (int)row);
     __syncthreads();
     int cur = f.ctrl[2];
     int leaf = -1;
@@ -803,7 +851,8 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       for (int j = tid; j < b; j += kFdThreads) {
         const int c = f.arena[cbase + j];
         const float nc = f.count[c];
-        const float U = f.kres[2 * j], T = f.kres[2 * j + 1];
+        const float U = forked ? ld_agent_f(&f.kres[2 * j]) : f.kres[2 * j];
+        const float T = forked ? ld_agent_f(&f.kres[2 * j + 1]) : f.kres[2 * j + 1];
         const float p1 = (nc + 1.0f) / nP1, p2 = nc / nP1;
         f.gain[j] = p1 * U - p2 * T;
         f.tall[j] = p2 * T;
@@ -943,8 +992,9 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         const float K = fd_kl_finish(sa, sb, D);
         if (lane == 0) sh.cf[3] = K;
       }
+      const bool split_forked = do_split && f.job != nullptr && n_split >= f.fork_min;
       if (do_split) {   // KL(c || P) of the split's nodes
-        if (f.job != nullptr && n_split >= f.fork_min) {
+        if (split_forked) {
           if (!fd_fork(f, sh, row, 1, n_split, 0, 2 * b + 1, 0, mt_idx)) {
             if (tid == 0) f.ctrl[3] = FD_HANG;
             break;
@@ -982,7 +1032,8 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           float s = 0.f;
           bool first = true;
           for (int j = 0; j < n_split; ++j) {
-            const float t = (f.count[f.jobs[j]] / cP) * f.kres[2 * b + 1 + j];
+            const float ks = split_forked ? ld_agent_f(&f.kres[2 * b + 1 + j]) : f.kres[2 * b + 1 + j];
+            const float t = (f.count[f.jobs[j]] / cP) * ks;
             s = first ? t : s + t;
             first = false;
           }
@@ -1108,7 +1159,8 @@ extern "C" int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t 
             al((void**)&f.mt, kMtN * 4) && al((void**)&f.kres, (3 * C + 8) * 4) && al((void**)&f.gain, C * 4) &&
             al((void**)&f.tall, C * 4) && al((void**)&f.tins, C * 4) && al((void**)&f.ncv, C * 4) &&
             al((void**)&f.jobs, (2 * C + 8) * 4) && al((void**)&f.job, sizeof(FdJob)) &&
-            al((void**)&f.pvec, (size_t)3 * dim * 4) && al((void**)&f.rnd, (2 * C + 8) * 4);
+            al((void**)&f.pvec, (size_t)3 * dim * 4) && al((void**)&f.rnd, (2 * C + 8) * 4) &&
+            al((void**)&f.dbg, 64);
   if (!ok) {
     for (void* p : h->allocs) (void)hipFree(p);
     return fit_fail(CWQ_ERR_OOM, "cwq_fit_create: device allocation failed");
@@ -1198,10 +1250,29 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   FitDev f = h->f;
   f.fork_min = kFdForkMin;
   if (const char* e = getenv("CWQ_FIT_FORK_MIN")) f.fork_min = atoi(e) < 2 ? 2 : atoi(e);
+  f.spin_ticks = kFdSpinTicks;
+  if (const char* e = getenv("CWQ_FIT_SPIN_MS")) f.spin_ticks = (uint64_t)(atoll(e) > 0 ? atoll(e) : 1) * 100000ull;
   if (helpers == 0) f.job = nullptr;
-  else if (hipMemsetAsync(f.job, 0, sizeof(FdJob), s) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "job reset failed");
+  else if (hipMemsetAsync(f.job, 0, sizeof(FdJob), s) != hipSuccess || hipMemsetAsync(f.dbg, 0, 64, s) != hipSuccess)
+    return fit_fail(CWQ_ERR_HIP, "job reset failed");
   hipLaunchKernelGGL(fit_insert_kernel, dim3(1 + helpers), dim3(kFdThreads), lds, s, f, X, n, leaf_out);
   if (hipGetLastError() != hipSuccess) return fit_fail(CWQ_ERR_HIP, "fit_insert_kernel launch failed");
+  if (getenv("CWQ_FIT_WATCH") && f.dbg) {
+    // diagnostics: the kernel's progress words, read on a second stream while it runs
+    hipStream_t ws = nullptr;
+    int* hd = nullptr;
+    if (hipStreamCreateWithFlags(&ws, hipStreamNonBlocking) == hipSuccess &&
+        hipHostMalloc((void**)&hd, 64, hipHostMallocDefault) == hipSuccess) {
+      for (int it = 0; hipStreamQuery(s) == hipErrorNotReady; ++it) {
+        if (hipMemcpyAsync(hd, f.dbg, 64, hipMemcpyDeviceToHost, ws) == hipSuccess && hipStreamSynchronize(ws) == hipSuccess)
+          fprintf(stderr, "[fit watch %d] row %d forks %d n %d phase %d done %d hjobs %d hexits %d hclaims %d\n", it, hd[0],
+                  hd[1], hd[2], hd[3], hd[4], hd[5], hd[6], hd[7]);
+        usleep(500000);
+      }
+    }
+    if (hd) (void)hipHostFree(hd);
+    if (ws) (void)hipStreamDestroy(ws);
+  }
   int ctrl[16];
   int64_t c64[8];
   if (hipMemcpyAsync(ctrl, h->f.ctrl, 64, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1213,7 +1284,13 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   info[2] = ctrl[3];
   info[3] = ctrl[0];
   if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");
-  if (ctrl[3] == FD_HANG) return fit_fail(CWQ_ERR_HIP, "cwq_fit_insert: a chip-wide KL pass did not complete");
+  if (ctrl[3] == FD_HANG) {
+    int dbg[16];
+    std::string m = "cwq_fit_insert: a chip-wide KL pass did not complete; state";
+    if (hipMemcpy(dbg, h->f.dbg, 64, hipMemcpyDeviceToHost) == hipSuccess)
+      for (int i = 0; i < 8; ++i) m += " " + std::to_string(dbg[i]);
+    return fit_fail(CWQ_ERR_HIP, m);
+  }
   // the next call resumes: clear the room flag
   if (ctrl[3] == FD_ROOM) {
     const int z = 0;

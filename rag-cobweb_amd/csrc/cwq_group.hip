@@ -1,0 +1,156 @@
+// libcwq: group-centred filter rows for clustered (real-structure) trees.
+//
+// The bf16-MFMA filters bound x'.mu' for root-centred query and row (x' = x - c0,
+// mu' = mu - c0); the error bound grows with |x'| |mu'|.  On a clustered corpus every row
+// sits far from the root mean (|mu'| ~ the cluster spread between clusters) while the keys
+// that decide the top-k differ by the spread WITHIN a cluster, so the bound admits most of
+// a cluster (C2-shaped ifit tree, 100k x 768: ~1,160 candidates and ~1,000 exact reranks
+// per query).  Rows in a group g (the subtree of a depth-1 internal node, mean c_g) are
+// therefore stored centred at c_g instead: M = fl(mu - c_g), d = c_g - c0 (exact in fp64),
+//   S = |x - mu|^2 = |x'|^2 + |M + d|^2 - 2 x'.M - 2 x'.d      (x' = fl(x - c0) as before)
+// so the kernels keep their arithmetic -- n2 = |x'|^2 + rn2 with rn2 = |M + d|^2, the dot
+// x'.M on the matrix cores, whose bound now scales with |M| (the within-group spread) --
+// and the per-(query, group) term -2 x'.d moves into the parent-prefix table the filters
+// already read: P'[q][p] = P[q][p] + (hs_p / invL_p) * sh[q][g(p)], sh = -2 x'.d in fp64,
+// rounded outward into [P'lo, P'hi] (categorize: P'c = hs_c * sh with invL = 1, the
+// bottleneck min taken from BF separately).  The exact rerank keeps the exact P and the
+// uncentred fp32 rows, so results stay the exact scan's bit for bit.  The rounding of M
+// adds 2^-23 |M| to the rows' beta / delta (cwq_api.hip build_filter); its row-only cross
+// term 2^-23 |M| |M + d| stays within eps_n * rn2 for groups whose rows all have
+// |M| <= 2 |M + d| (plan_groups).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "cwq_internal.h"
+
+namespace cwq {
+
+// Rows of `mean` by node id into a dense [n][D] array (group centres).
+__global__ void gather_rows_f32_kernel(const float* __restrict__ mean, int D, const int64_t* __restrict__ nodes,
+                                       int64_t n, float* out) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) out[r * D + d] = mean[nodes[r] * (int64_t)D + d];
+}
+
+hipError_t launch_gather_rows_f32(const float* mean, int D, const int64_t* nodes, int64_t n, float* out,
+                                  hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows_f32_kernel, dim3((unsigned)n), dim3(256), 0, s, mean, D, nodes, n, out);
+  return hipGetLastError();
+}
+
+// Per row (one wave): |fl(mu - c0)|^2 and |fl(mu - c_g)|^2 (g = grp[r], -1: none) in fp64.
+__global__ void group_norms_kernel(const float* __restrict__ mean, int D, const int64_t* __restrict__ nodes, int64_t n,
+                                   const float* __restrict__ c0, const float* __restrict__ cent,
+                                   const int* __restrict__ grp, double* root2, double* grp2) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int g = grp[r];
+  double a = 0.0, b = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float v = mean[nodes[r] * (int64_t)D + d];
+    const float u0 = v - c0[d];
+    a += (double)u0 * (double)u0;
+    if (g >= 0) {
+      const float ug = v - cent[(int64_t)g * D + d];
+      b += (double)ug * (double)ug;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  if (lane == 0) {
+    root2[r] = a;
+    grp2[r] = g >= 0 ? b : a;
+  }
+}
+
+hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c0,
+                              const float* cent, const int* grp, double* root2, double* grp2, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(group_norms_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, mean, D, nodes, n, c0, cent,
+                     grp, root2, grp2);
+  return hipGetLastError();
+}
+
+// sh[q][g] = -2 x'.d_g in fp64 (x' = fl(x - c0) exactly as query_prep forms it; d_g = c_g - c0
+// in fp64, exact).  One wave per (query, group).
+__global__ void group_shift_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c0,
+                                   const float* __restrict__ cent, int G, double* sh) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (w >= nq * (int64_t)G) return;
+  const int64_t qi = w / G;
+  const int g = (int)(w % G);
+  double a = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float xc = q[qi * D + d] - c0[d];
+    const double dd = (double)cent[(int64_t)g * D + d] - (double)c0[d];
+    a += (double)xc * dd;
+  }
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+  if (lane == 0) sh[qi * G + g] = -2.0 * a;
+}
+
+// Outward-rounded fp32 interval of t (fp64), widened by e.
+__device__ __forceinline__ void out_round(double t, double e, float& lo, float& hi) {
+  lo = __double2float_rd(t - e);
+  hi = __double2float_ru(t + e);
+}
+
+// The filters' prefix tables for group-centred rows: per (query, internal node p),
+// Fast [P'lo, P'hi] = P + F[p] * sh[q][grp[p]] (F = hs / invL of p's rows) and, when
+// Pclo is set, categorize [P'c lo, hi] = Fc[p] * sh (zero for nodes without a group).
+__global__ void group_pprime_kernel(const float* __restrict__ P, int64_t ldP, int nq, int NI,
+                                    const int* __restrict__ grp, const double* __restrict__ F,
+                                    const double* __restrict__ Fc, const double* __restrict__ sh, int G, float* Plo,
+                                    float* Phi, float* Pclo, float* Pchi) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nq * NI) return;
+  const int64_t qi = i / NI;
+  const int p = (int)(i % NI);
+  const int g = grp[p];
+  const size_t o = (size_t)qi * ldP + p;
+  const float pv = P[o];
+  if (g < 0) {
+    Plo[o] = pv;
+    Phi[o] = pv;
+    if (Pclo) {
+      Pclo[o] = 0.f;
+      Pchi[o] = 0.f;
+    }
+    return;
+  }
+  const double s = sh[qi * G + g];
+  const double a = F[p] * s;
+  const double t = (double)pv + a;
+  float lo, hi;
+  out_round(t, (fabs((double)pv) + fabs(a)) * 0x1p-50, lo, hi);
+  Plo[o] = lo;
+  Phi[o] = hi;
+  if (Pclo) {
+    const double c = Fc[p] * s;
+    out_round(c, fabs(c) * 0x1p-50, lo, hi);
+    Pclo[o] = lo;
+    Pchi[o] = hi;
+  }
+}
+
+hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0, const float* cent, int G,
+                                 const float* P, int64_t ldP, int NI, const int* grp, const double* F, const double* Fc,
+                                 double* sh, float* Plo, float* Phi, float* Pclo, float* Pchi, hipStream_t s) {
+  if (nq <= 0 || NI <= 0 || G <= 0) return hipSuccess;
+  const int64_t nw = (int64_t)nq * G;
+  hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, q, (int64_t)nq, D, c0, cent,
+                     G, sh);
+  const int64_t n = (int64_t)nq * NI;
+  hipLaunchKernelGGL(group_pprime_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, ldP, nq, NI, grp, F,
+                     Fc, sh, G, Plo, Phi, Pclo, Pchi);
+  return hipGetLastError();
+}
+
+}  // namespace cwq

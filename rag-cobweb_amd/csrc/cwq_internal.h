@@ -300,6 +300,8 @@ struct FgArgs {
   const int* rowmap;                      // sample pass: operand row -> filter row (-1 pad)
   const float* P;                         // [nq][ldP] path prefixes of internal nodes (lower bounds when Phi)
   const float* Phi;                       // [nq][ldP] upper bounds of the prefixes (NULL: P is exact)
+  const float* BFt;                       // categorize with group-centred rows: the bottleneck table (P then
+                                          // holds the rows' group terms); NULL: P is the bottleneck
   PathB pb;                               // path-sum bounds (pb.dot set: read instead of P / Phi)
   int64_t ldP;
   int pT;                                 // P / Phi (and mode-2 lb / lb_hi) node-major: [node][ldP] (pidx)
@@ -531,7 +533,15 @@ hipError_t launch_stream_init(int* Tb, int n, hipStream_t s);
 
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
                             int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,
-                            hipStream_t s);
+                            hipStream_t s, const float* cent = nullptr, const int* grp = nullptr, float* nm = nullptr);
+// Group-centred filter rows (cwq_group.hip)
+hipError_t launch_gather_rows_f32(const float* mean, int D, const int64_t* nodes, int64_t n, float* out,
+                                  hipStream_t s);
+hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c0,
+                              const float* cent, const int* grp, double* root2, double* grp2, hipStream_t s);
+hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0, const float* cent, int G,
+                                 const float* P, int64_t ldP, int NI, const int* grp, const double* F, const double* Fc,
+                                 double* sh, float* Plo, float* Phi, float* Pclo, float* Pchi, hipStream_t s);
 hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int64_t n, void* Sb, hipStream_t s);
 hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
                              float4* qinfo, hipStream_t s);

@@ -59,30 +59,38 @@ __device__ __forceinline__ float up(double v) { return (float)(v * (1.0 + 0x1p-2
 // Row / query preparation
 // ---------------------------------------------------------------------------
 // Rows: fp32 row-major copy (exact rerank, DP wide), bf16 hi part of the centred row
-// (DPB wide, zero padded), |mu'|^2, |mu_lo|, |mu_hi|.  One wave per row.
+// (DPB wide, zero padded), |mu'|^2, |mu_lo|, |mu_hi|.  One wave per row.  Group-centred
+// rows (cwq_group.hip; grp[r] >= 0): centred at cent[g] instead of c, n2 = |M + d|^2
+// (d = cent[g] - c in fp64) and nm = |M|.
 __global__ void rows_prep_kernel(const float* __restrict__ mean, int D, const int64_t* __restrict__ nodes, int64_t n,
                                  const float* __restrict__ c, int DP, int DPB, int64_t ld, float* Mf, __bf16* Mb,
-                                 float* n2, float* nlo, float* nhi) {
+                                 float* n2, float* nlo, float* nhi, const float* __restrict__ cent,
+                                 const int* __restrict__ grp, float* nm) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
   if (r >= ld) return;
-  double s = 0.0, slo = 0.0, shi = 0.0;
+  const int g = (grp && r < n) ? grp[r] : -1;
+  const float* cc = g >= 0 ? cent + (int64_t)g * D : c;
+  double s = 0.0, slo = 0.0, shi = 0.0, sm = 0.0;
   const int W = DP > DPB ? DP : DPB;
   for (int d = lane; d < W; d += kWave) {
     const bool ok = r < n && d < D;
     const float v = ok ? mean[nodes[r] * (int64_t)D + d] : 0.f;
-    const float vc = ok ? v - c[d] : 0.f;
+    const float vc = ok ? v - cc[d] : 0.f;
     const __bf16 h = (__bf16)vc;
     const float hf = (float)h;
     const float lo = vc - hf;   // exact
     if (d < DP) Mf[r * DP + d] = v;
     if (d < DPB) Mb[r * DPB + d] = h;
-    s += (double)vc * (double)vc;
+    const double vs = g >= 0 && ok ? (double)vc + ((double)cc[d] - (double)c[d]) : (double)vc;
+    s += vs * vs;
+    sm += (double)vc * (double)vc;
     slo += (double)lo * (double)lo;
     shi += (double)hf * (double)hf;
   }
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off, 64);
+    sm += __shfl_xor(sm, off, 64);
     slo += __shfl_xor(slo, off, 64);
     shi += __shfl_xor(shi, off, 64);
   }
@@ -90,15 +98,16 @@ __global__ void rows_prep_kernel(const float* __restrict__ mean, int D, const in
     n2[r] = (float)s;
     nlo[r] = up(sqrt(slo));
     nhi[r] = up(sqrt(shi));
+    if (nm) nm[r] = up(sqrt(sm));
   }
 }
 
 hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c, int DP,
                             int DPB, int64_t ld, float* Mf, void* Mb, float* n2, float* nlo, float* nhi,
-                            hipStream_t s) {
+                            hipStream_t s, const float* cent, const int* grp, float* nm) {
   if (ld <= 0) return hipSuccess;
   hipLaunchKernelGGL(rows_prep_kernel, dim3((unsigned)((ld + 3) / 4)), dim3(256), 0, s, mean, D, nodes, n, c, DP, DPB,
-                     ld, Mf, (__bf16*)Mb, n2, nlo, nhi);
+                     ld, Mf, (__bf16*)Mb, n2, nlo, nhi, cent, grp, nm);
   return hipGetLastError();
 }
 
@@ -1107,7 +1116,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
             if (fb.par >= 0 && q < a.nq) pi = a.P[pidx(a.ldP, a.pT, q, fb.par)] * fb.invL;   // exact or lower bounds
             float u;
             fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, fb, pi, a.eps_n, a.slack, u, m);
-            if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, a.P[pidx(a.ldP, a.pT, q, fb.par)]);
+            if (a.cat && fb.par >= 0 && q < a.nq) m = fminf(m, (a.BFt ? a.BFt : a.P)[pidx(a.ldP, a.pT, q, fb.par)]);
           }
           a.lb[(size_t)q * a.ldlb + g] = m;
         }
@@ -1182,7 +1191,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
                 }
                 float u;
                 fg_bounds(d0, 0x1p-23f * fabsf(d0), qi, f, pi, a.eps_n, a.slack, u, lo);
-                if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, a.P[pidx(a.ldP, a.pT, q, f.par)]);
+                if (a.cat && f.par >= 0 && q < a.nq) lo = fminf(lo, (a.BFt ? a.BFt : a.P)[pidx(a.ldP, a.pT, q, f.par)]);
               }
               a.lb[(size_t)q * a.ldlb + r] = lo;
             } else if (usable && q < a.nq && (!uni || d0 >= 0.f)) {
@@ -1212,7 +1221,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
               float u, lo;
               fg_bounds2(d, ex, qi, f, pi, pl, a.eps_n, a.slack, u, lo);
               if (a.cat && f.par >= 0) {   // categorize key min(BF[parent], lp)
-                const float bp = a.P[pidx(a.ldP, a.pT, q, f.par)];
+                const float bp = (a.BFt ? a.BFt : a.P)[pidx(a.ldP, a.pT, q, f.par)];
                 u = fminf(u, bp);
                 lo = fminf(lo, bp);
               }

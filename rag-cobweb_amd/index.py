@@ -146,6 +146,14 @@ class CobwebIndex:
                 "device_bytes"]
         return dict(zip(keys, (int(v) for v in out)))
 
+    def filter_info(self):
+        """How the filters centre their rows (cwq_index_filter_info): group-centred rows on
+        clustered trees, the number of groups / group-centred rows, the int8 panel."""
+        out = np.zeros(4, np.int64)
+        check(self._L.cwq_index_filter_info(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"group_centred": bool(out[0]), "groups": int(out[1]), "group_rows": int(out[2]),
+                "int8_panel": bool(out[3])}
+
     def set_timing(self, enable=True):
         check(self._L.cwq_set_timing(self._h, int(bool(enable))))
 

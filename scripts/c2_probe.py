@@ -71,6 +71,7 @@ def main():
     ix = w._index
     inf = ix.info
     root_c = len(w.tree.root.children)
+    print(f"filter rows: {ix.filter_info()}", flush=True)
     print(f"C2 corpus {args.n}x{args.dim} ({args.clusters} clusters): device ifit {t_fit:.2f} s "
           f"({args.n / t_fit:.0f} inserts/s); tree {inf['n_nodes']} nodes, {inf['internal_nodes']} internal, "
           f"max depth {inf['max_depth']}, root children {root_c}; index build {t_ix:.2f} s "

@@ -1,0 +1,106 @@
+"""Group-centred filter rows (cwq_group.hip) against the exact fp32 scan.
+
+On a clustered corpus the filters store each isotropic row centred at its depth-1
+ancestor's mean and fold the per-(query, group) term into the parent-prefix tables
+(exact internal pass + outward-rounded shifts).  Results must not change: Fast top-k ids
+AND scores bit-identical to the exact scan (batch, and one / 8 / 64 queries per call), and
+Basic categorize's pop order, n_found and log_prob calls equal to the exact heap replay --
+with the mode chosen automatically on clustered two-level trees, and forced
+(CWQ_GROUP_CENTRE=1) on N(0,I) balanced / two-level trees where it would not be chosen.
+Reference semantics: CobwebWrapper.py:210-265 (Fast), CobwebTorchTree.py:235-289 (Basic)."""
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg
+
+
+def clustered(n, d, nc, seed):
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    C = 2.0 * torch.randn((nc, d), generator=g, device="cuda:0")
+    lab = torch.randint(0, nc, (n,), generator=g, device="cuda:0")
+    X = (C[lab] + 0.3 * torch.randn((n, d), generator=g, device="cuda:0")).contiguous()
+    Q = torch.cat([X[:256] + 0.05 * torch.randn((256, d), generator=g, device="cuda:0"),
+                   C[torch.randint(0, nc, (256,), generator=g, device="cuda:0")] +
+                   0.3 * torch.randn((256, d), generator=g, device="cuda:0")]).contiguous()
+    return X, lab, Q
+
+
+def make_index(gpu, t, mode, monkeypatch):
+    if mode is None:
+        monkeypatch.delenv("CWQ_GROUP_CENTRE", raising=False)
+    else:
+        monkeypatch.setenv("CWQ_GROUP_CENTRE", mode)
+    return gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+
+
+def check_fast(ix, Q, k=10):
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, k)
+    ix.set_filter(-1)
+    ids1, s1 = ix.score_topk(Q, k)
+    st = ix.last_stats()
+    assert st["filter_used"], st
+    assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
+    for nq in (1, 8, 64):
+        for a in range(0, 128, nq):
+            i2, s2 = ix.score_topk(Q[a:a + nq].contiguous(), k)
+            assert torch.equal(i2, ids0[a:a + nq]) and torch.equal(s2, s0[a:a + nq]), (nq, a)
+    return ids0, s0, st
+
+
+def check_basic(ix, Q, k=10, max_nodes=100000):
+    got = ix.categorize(Q, k, max_nodes)
+    ix.set_filter(0)
+    os.environ["CWQ_CAT_COUNT"] = "0"
+    try:
+        ref = ix.categorize(Q, k, max_nodes)
+    finally:
+        del os.environ["CWQ_CAT_COUNT"]
+        ix.set_filter(-1)
+    for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
+        assert torch.equal(a, b), name
+    return got
+
+
+def test_group_mode_clustered_two_level_auto(gpu, monkeypatch):
+    X, lab, Q = clustered(60_000, 128, 150, 41)
+    t = gpu.synth.two_level_synth(X, lab)
+    ix = make_index(gpu, t, None, monkeypatch)
+    fi = ix.filter_info()
+    assert fi["group_centred"] and fi["groups"] == 150 and fi["group_rows"] == 60_000, fi
+    ids, sc, st = check_fast(ix, Q)
+    basic = check_basic(ix, Q)
+    ix0 = make_index(gpu, t, "0", monkeypatch)
+    assert not ix0.filter_info()["group_centred"]
+    ids0, sc0, st0 = check_fast(ix0, Q)
+    assert torch.equal(ids, ids0) and torch.equal(sc, sc0)
+    assert all(torch.equal(a, b) for a, b in zip(basic, check_basic(ix0, Q)))
+    # the point of the centring: far fewer candidates reach the exact rerank
+    assert st["candidates"] * 3 <= st0["candidates"], (st, st0)
+
+
+@pytest.mark.parametrize("shape", ["balanced 4/6", "two-level 600"])
+def test_group_mode_forced_on_unclustered_trees(gpu, shape, monkeypatch):
+    X = gpu.synth.synthetic_corpus(40_000, 48, seed=43)
+    if shape.startswith("balanced"):
+        t = gpu.synth.balanced_synth(X, 4, 6)
+    else:
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(44)
+        t = gpu.synth.two_level_synth(X, torch.randint(0, 600, (X.shape[0],), generator=g, device="cuda:0"))
+    Q, _ = gpu.synth.synthetic_queries(X, 256, seed=45)
+    ix = make_index(gpu, t, "1", monkeypatch)
+    assert ix.filter_info()["group_centred"]
+    check_fast(ix, Q)
+    check_basic(ix, Q)
+    check_basic(ix, Q[:64], k=5, max_nodes=50)
