@@ -2201,7 +2201,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 3, 0, slabs))) {
       return rc;
     }
-    HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s));
+    HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s, true));
     SimArgs sa;
     memset(&sa, 0, sizeof(sa));
     sa.nq = nqc;
@@ -2256,6 +2256,117 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     for (int i = 0; i < nqc; ++i) {
       if (by_count && cst[i] == 0 && !fbad[i]) ++ix->stats[3];
       else if (!fbad[i]) ++ix->stats[4];
+    }
+    if (redo.empty()) continue;
+
+    // Two-level replay (simulate_two_kernel, §4.7) of the queries whose top-R list ended
+    // inside a tie: a second exact leaf scan keyed by the second-level bottleneck, then
+    // the replay on both lists; what it cannot certify goes to the DENSE re-run below.
+    const char* tle = getenv("CWQ_CAT_TWO");
+    if (ix->NI > 0 && !ix->any_int_sent && !complete && R == 64 && !(tle && *tle && atoi(tle) == 0)) {
+      std::vector<float> h1k((size_t)nqc * R), h1a((size_t)nqc * R);
+      std::vector<int> h1r((size_t)nqc * R);
+      HIPCHK(hipMemcpyAsync(h1k.data(), okey, h1k.size() * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(h1a.data(), oaux, h1a.size() * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(h1r.data(), orow, h1r.size() * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      std::vector<int> left;
+      const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
+      const size_t per_q2 = chunk_bytes(ix, kQPad) / kQPad + (size_t)std::max(ix->NI, 1) * 4 + (size_t)cap2 * 16 +
+                            (size_t)R * 12 * 2 + 64 + (size_t)k * 8 + (size_t)ix->D * 4 +
+                            (size_t)R * 12 * (pick_nslab(ix, ix->NL_iso, 1) + pick_nslab(ix, ix->NL_an, 1) + 2) *
+                                scan_lists_per_slab(kl);
+      const int64_t sub2 = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q2));
+      for (size_t r0 = 0; r0 < redo.size(); r0 += sub2) {
+        const int ns = (int)std::min<int64_t>(sub2, (int64_t)redo.size() - (int64_t)r0);
+        const int64_t ns_pad = round_up(ns, kQPad);
+        const int nqb2 = n_qblocks_for(ns, kl);
+        const int slabs2 = (pick_nslab(ix, ix->NL_iso, nqb2) + pick_nslab(ix, ix->NL_an, nqb2) + 2) *
+                           scan_lists_per_slab(kl);
+        const size_t ldI = (size_t)std::max(ix->NI, 1);
+        if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) +
+                              (size_t)ns_pad * (ldI * 4 + (size_t)slabs2 * R * 12 + (size_t)R * 24 + cap2 * 16 + 64 +
+                                                (size_t)k * 8) +
+                              (size_t)ns * ix->D * 4 + 24 * 256)))
+          return rc;
+        Bump b2(ix->ws, ix->ws_size);
+        Chunk c2;
+        carve_chunk(ix, b2, c2, ns);
+        float* qsub = b2.take<float>((size_t)ns * ix->D);
+        float* T2 = b2.take<float>((size_t)ns_pad * ldI);
+        float* pk2 = b2.take<float>((size_t)ns_pad * slabs2 * R);
+        float* pa2 = b2.take<float>((size_t)ns_pad * slabs2 * R);
+        int* pr2 = b2.take<int>((size_t)ns_pad * slabs2 * R);
+        float* l1k = b2.take<float>((size_t)ns_pad * R);
+        float* l1a = b2.take<float>((size_t)ns_pad * R);
+        int* l1r = b2.take<int>((size_t)ns_pad * R);
+        float* l2k = b2.take<float>((size_t)ns_pad * R);
+        float* l2a = b2.take<float>((size_t)ns_pad * R);
+        int* l2r = b2.take<int>((size_t)ns_pad * R);
+        HeapEnt* heap2 = b2.take<HeapEnt>((size_t)ns_pad * cap2);
+        int* status2 = b2.take<int>(ns_pad);
+        int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
+        int* found2 = b2.take<int>(ns_pad);
+        int64_t* calls2 = b2.take<int64_t>(ns_pad);
+        std::vector<int64_t> gq(ns);
+        std::vector<float> s1k((size_t)ns * R), s1a((size_t)ns * R);
+        std::vector<int> s1r((size_t)ns * R);
+        for (int i = 0; i < ns; ++i) {
+          const int li = redo[r0 + i];
+          gq[i] = q0 + li;
+          std::copy(h1k.begin() + (size_t)li * R, h1k.begin() + (size_t)(li + 1) * R, s1k.begin() + (size_t)i * R);
+          std::copy(h1a.begin() + (size_t)li * R, h1a.begin() + (size_t)(li + 1) * R, s1a.begin() + (size_t)i * R);
+          std::copy(h1r.begin() + (size_t)li * R, h1r.begin() + (size_t)(li + 1) * R, s1r.begin() + (size_t)i * R);
+        }
+        if ((rc = ix->reserve_fb((size_t)ns * 8))) return rc;
+        int64_t* d_gq = (int64_t*)ix->fb;
+        HIPCHK(hipMemcpyAsync(d_gq, gq.data(), (size_t)ns * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(l1k, s1k.data(), s1k.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(l1a, s1a.data(), s1a.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(l1r, s1r.data(), s1r.size() * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(launch_copy_rows(q, ix->D, d_gq, qsub, ix->D, nullptr, ns, ix->D, s));
+        HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
+        if ((rc = run_internal(ix, c2, s))) return rc;
+        HIPCHK(launch_cat_t2(c2.BF, c2.LPF, (int64_t)ldI, ix->NI, ns, ix->par_int, l1k, R, T2, s));
+        Chunk c2t = c2;
+        c2t.BF = T2;   // the leaf scan's categorize key reads min(T2[parent], lp)
+        int nst2 = 0;
+        if ((rc = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 3, 0,
+                                slabs2)))
+          return rc;
+        HIPCHK(launch_merge(pk2, pa2, pr2, ns, nst2 * R, R, l2k, l2a, l2r, s, true));
+        SimArgs st = sa;
+        st.nq = ns;
+        st.pre_status = 0;
+        st.LPF = c2.LPF;
+        st.BF = c2.BF;
+        st.lkey = l1k;
+        st.laux = l1a;
+        st.lrow = l1r;
+        st.lkey2 = l2k;
+        st.laux2 = l2a;
+        st.lrow2 = l2r;
+        st.T2 = T2;
+        st.heap = heap2;
+        st.heap_cap = cap2;
+        st.out_nodes = nodes2;
+        st.n_found = found2;
+        st.n_calls = calls2;
+        st.status = status2;
+        HIPCHK(launch_simulate_two(st, s));
+        // every result goes back; the uncertified ones are overwritten by the DENSE re-run
+        HIPCHK(launch_copy_rows(nodes2, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_gq, ns, 2 * (int64_t)k, s));
+        HIPCHK(launch_copy_rows(found2, 1, nullptr, n_found, 1, d_gq, ns, 1, s));
+        if (n_calls) HIPCHK(launch_copy_rows(calls2, 2, nullptr, n_calls, 2, d_gq, ns, 2, s));
+        std::vector<int> hs(ns);
+        HIPCHK(hipMemcpyAsync(hs.data(), status2, (size_t)ns * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));   // the pageable host sources must outlive their uploads
+        for (int i = 0; i < ns; ++i) {
+          if (hs[i]) left.push_back(redo[r0 + i]);
+          else ++ix->stats[5];
+        }
+      }
+      redo.swap(left);
     }
     ix->stats[1] += (int64_t)redo.size();
     if (redo.empty()) continue;

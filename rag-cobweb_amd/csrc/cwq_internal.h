@@ -83,6 +83,10 @@ struct SimArgs {
   int64_t* out_nodes; int* n_found; int64_t* n_calls; int* status;
   const int* par_int;  // parent internal id of every internal node (cat_count_kernel)
   int pre_status;      // simulate: skip the queries whose status the count pass already set to 0
+  // two-level replay (simulate_two_kernel, §4.7): the second-level table T2 [nq_pad][NI]
+  // (cat_t2_kernel) and the list by the second-level key [nq][R]
+  const float* T2;
+  const float* lkey2; const float* laux2; const int* lrow2;
 };
 
 // Node variances read by the index build.  Full: [n_nodes][D] rows (compute_var of every
@@ -147,8 +151,11 @@ hipError_t launch_int_small(const float* X, const float* A, const float* B, int6
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
                                float* LPF, hipStream_t s);
+hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
+                         const float* lkey, int R, float* T2, hipStream_t s);
+hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
-                        float* okey, float* oaux, int* orow, hipStream_t s);
+                        float* okey, float* oaux, int* orow, hipStream_t s, bool cat);
 hipError_t launch_merge_expand(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K, int k,
                                const int64_t* sent_ptr, const int64_t* sent_ids, int64_t* ids, float* scores,
                                hipStream_t s);

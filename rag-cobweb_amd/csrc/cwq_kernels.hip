@@ -52,14 +52,25 @@ __device__ __forceinline__ int shift_up<64>(int v) {
   return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
 }
 
-// Insert candidate (ck, ca, cr) into the sorted list held by lane group g.
-// Order: key descending, then row ascending.  The first K slots are the top-K.
-template <int KL>
+// List order of an entry (key k, aux a, row r) before (k2, a2, r2): key descending, then
+// row ascending; categorize lists (CAT) put the smaller aux (= the row's own lp) first
+// among equal keys, so that a list cut inside a tie at its last key G holds every row
+// whose own lp IS G (the rows that attain their path bottleneck; §4.7 two-level replay).
+template <bool CAT>
+__device__ __forceinline__ bool list_before(float k, float a, int r, float k2, float a2, int r2) {
+  if (k != k2) return k > k2;
+  if (CAT && a != a2) return a < a2;
+  return r < r2;
+}
+
+// Insert candidate (ck, ca, cr) into the sorted list held by lane group g (list_before
+// order).  The first K slots are the top-K.
+template <int KL, bool CAT = false>
 __device__ __forceinline__ void list_insert(float& lk, float& la, int& lr, int g, int lane, float ck, float ca,
                                             int cr, int K) {
   const bool ing = (KL == 64) || ((lane >> 4) == g);
   const int slot = lane & (KL - 1);
-  const bool prec = ing && (lk > ck || (lk == ck && lr < cr));
+  const bool prec = ing && list_before<CAT>(lk, la, lr, ck, ca, cr);
   const int pos = __popcll(__ballot(prec));
   if (pos < K) {
     const float sk = __int_as_float(shift_up<KL>(__float_as_int(lk)));
@@ -263,13 +274,14 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X, 
             const int g = qi % QPR;
             const int tl = g * KL + a.K - 1;
             const float tk = rl_f(lk[r], tl);
+            const float ta = rl_f(la[r], tl);
             const int tr = rl_i(lr[r], tl);
-            const bool c = key != -CWQ_INF && (key > tk || (key == tk && rid < tr));
+            const bool c = key != -CWQ_INF && list_before<CAT>(key, lp, rid, tk, ta, tr);
             uint64_t mask = __ballot(c);
             while (mask) {
               const int j = __builtin_ctzll(mask);
               mask &= mask - 1;
-              list_insert<KL>(lk[r], la[r], lr[r], g, lane, rl_f(key, j), rl_f(lp, j), rl_i(rid, j), a.K);
+              list_insert<KL, CAT>(lk[r], la[r], lr[r], g, lane, rl_f(key, j), rl_f(lp, j), rl_i(rid, j), a.K);
             }
           }
         }
@@ -645,6 +657,7 @@ hipError_t launch_scan_small(const float* X, const float* M, const ScanArgs& a0,
 // Merge the per-slab partial lists of one query into its global top-K (K <= 64).
 // One wave per query; the list lives in the wave's 64 lanes.
 // ---------------------------------------------------------------------------
+template <bool CAT>
 __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ pkey, const float* __restrict__ paux,
                                                     const int* __restrict__ prow, int nq, int nent, int K,
                                                     float* okey, float* oaux, int* orow) {
@@ -664,13 +677,14 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ pk
       er = prow[base + e];
     }
     const float tk = rl_f(lk, K - 1);
+    const float ta = rl_f(la, K - 1);
     const int tr = rl_i(lr, K - 1);
-    const bool c = ek != -CWQ_INF && (ek > tk || (ek == tk && er < tr));
+    const bool c = ek != -CWQ_INF && list_before<CAT>(ek, ea, er, tk, ta, tr);
     uint64_t mask = __ballot(c);
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= mask - 1;
-      list_insert<64>(lk, la, lr, 0, lane, rl_f(ek, j), rl_f(ea, j), rl_i(er, j), K);
+      list_insert<64, CAT>(lk, la, lr, 0, lane, rl_f(ek, j), rl_f(ea, j), rl_i(er, j), K);
     }
   }
   if (lane < K) {
@@ -681,9 +695,12 @@ __global__ __launch_bounds__(256) void merge_kernel(const float* __restrict__ pk
 }
 
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K, float* okey,
-                        float* oaux, int* orow, hipStream_t s) {
+                        float* oaux, int* orow, hipStream_t s, bool cat) {
   dim3 grid((unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG)), block(256);
-  hipLaunchKernelGGL(merge_kernel, grid, block, 0, s, pkey, paux, prow, nq, nent, K, okey, oaux, orow);
+  if (cat)
+    hipLaunchKernelGGL(merge_kernel<true>, grid, block, 0, s, pkey, paux, prow, nq, nent, K, okey, oaux, orow);
+  else
+    hipLaunchKernelGGL(merge_kernel<false>, grid, block, 0, s, pkey, paux, prow, nq, nent, K, okey, oaux, orow);
   return hipGetLastError();
 }
 
@@ -987,6 +1004,49 @@ hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int 
 }
 
 // ---------------------------------------------------------------------------
+// Second-level bottleneck table of the two-level categorize replay (§4.7).  For query q
+// with group value G (its top-R list's last key, the bottleneck of a tie), internal node
+// i in the group (BF == G) gets B2 = the min of lp over its path strictly below the
+// group's root a (the shallowest path node whose lp is G; +inf for a itself); every other
+// node gets -inf.  A leaf row under parent p then has the categorize key
+// min(T2[p], lp) = its second-level bottleneck when it belongs to the group, and a key
+// no larger than G when it does not.
+// ---------------------------------------------------------------------------
+__global__ void cat_t2_kernel(const float* __restrict__ BF, const float* __restrict__ LPF, int64_t ldI, int NI,
+                              int nq, const int* __restrict__ par_int, const float* __restrict__ lkey, int R,
+                              float* T2) {
+  const int64_t total = (int64_t)NI * nq;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / NI);
+    const int i = (int)(t % NI);
+    const float* bf = BF + (size_t)q * ldI;
+    const float g = lkey[(size_t)q * R + R - 1];   // the list's last key
+    float m = -CWQ_INF;
+    if (bf[i] == g) {
+      m = CWQ_INF;
+      int cur = i;
+      for (int guard = 0; guard < NI; ++guard) {
+        const int p = par_int[cur];
+        if (p < 0 || bf[p] > g) break;   // cur is the group's root
+        m = fminf(m, LPF[(size_t)q * ldI + cur]);
+        cur = p;
+      }
+    }
+    T2[(size_t)q * ldI + i] = m;
+  }
+}
+
+hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
+                         const float* lkey, int R, float* T2, hipStream_t s) {
+  const int64_t total = (int64_t)NI * nq;
+  if (total <= 0) return hipSuccess;
+  if (R <= 0) return hipErrorInvalidValue;
+  dim3 grid((unsigned)std::min<int64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(cat_t2_kernel, grid, dim3(256), 0, s, BF, LPF, ldI, NI, nq, par_int, lkey, R, T2);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Best-first categorize on precomputed scores (CobwebTorchTree.py:235-289).
 // One thread per query; binary heap in global scratch.  Pops come out in
 // non-increasing path-bottleneck order, so with the top-R leaf rows by
@@ -1273,6 +1333,114 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
     if (a.n_calls) a.n_calls[q] = calls;
     a.status[q] = status;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Two-level replay (§4.7).  A query whose top-R list (lkey, R = 64) ends inside a tie at
+// its last key G -- a group of more than R rows sharing the bottleneck G, e.g. the leaves
+// of the query's own cluster under the cluster node whose lp is the lowest on their paths
+// -- is replayed on two lists:
+//   list 1: its rows with key > G (every such row is in it) and its rows with key == G
+//           whose own lp is G (they attain the bottleneck themselves: the group's roots
+//           among the leaf rows; the categorize tie order (list_before<true>) puts them
+//           first inside the tie, so the list holds all of them when its last entry's own
+//           lp is above G -- checked here);
+//   list 2: the top R rows by the second-level key min(T2[parent], lp) (cat_t2_kernel):
+//           inside the group, the min of lp below the group's root.
+// Inside a group the pops come out in non-increasing second-level bottleneck b2 while
+// one root's subtree is searched (the same argument one level down: every other node
+// of the frontier has lp <= G < b2).  So the replay is exact while every popped group
+// node has b2 above list 2's last key (when list 2 is full; max'ed with G, so a deeper
+// node with lp == G ends it) and no second root of the group is popped; nodes below the
+// group (b < G) end it too.  Otherwise status = 1 and the host re-runs the query DENSE.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void simulate_two_kernel(const SimArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
+  int64_t hn = 0;
+  const float* BF = a.BF + (size_t)q * a.ldI;
+  const float* T2 = a.T2 + (size_t)q * a.ldI;
+  const int R = a.R;
+  const size_t lo = (size_t)q * R;
+  const float k1 = lane < R ? a.lkey[lo + lane] : -CWQ_INF;
+  const float x1 = lane < R ? a.laux[lo + lane] : 0.f;
+  const int w1 = lane < R ? a.lrow[lo + lane] : 0x7fffffff;
+  const float G = rl_f(k1, R - 1), xG = rl_f(x1, R - 1);
+  const int wG = rl_i(w1, R - 1);
+  const float k2 = lane < R ? a.lkey2[lo + lane] : -CWQ_INF;
+  const float x2 = lane < R ? a.laux2[lo + lane] : 0.f;
+  const int w2 = lane < R ? a.lrow2[lo + lane] : 0x7fffffff;
+  const bool e1 = lane < R && k1 != -CWQ_INF && w1 != 0x7fffffff;
+  const int pe1 = e1 ? a.row_par[w1] : -3;
+  // a row at the tie with own lp G under a parent of bottleneck G is a group member (list 2)
+  const bool v1 = e1 && (k1 > G || (k1 == G && x1 == G && (pe1 < 0 || BF[pe1] > G)));
+  const bool v2 = lane < R && k2 != -CWQ_INF && w2 != 0x7fffffff;
+  const bool full2 = __popcll(__ballot(v2)) == (uint64_t)R;
+  const float tau2 = fmaxf(rl_f(k2, R - 1), G);
+  const int p1 = v1 ? pe1 : -3, p2 = v2 ? a.row_par[w2] : -3;
+  int status = 0, found = 0, gpops = 0;
+  int64_t calls = 1, visited = 0;
+  // list 1 must be full, end inside the tie at G, and hold every group root among the rows
+  if (!(G > -CWQ_INF) || wG == 0x7fffffff || !(xG > G) || a.NI <= 0) status = 1;
+
+  if (!status) wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0}, lane);
+  while (hn > 0) {
+    const HeapEnt e = wheap_pop(h, hn, lane);
+    ++visited;
+    const bool is_int = e.node >= 0;
+    const int row = is_int ? -1 : -e.node - 1;
+    const int pr = is_int ? a.par_int[e.node] : a.row_par[row];
+    const float b = is_int ? BF[e.node] : (pr >= 0 ? fminf(BF[pr], e.score) : e.score);
+    if (!(b >= G)) {   // below the group (or NaN)
+      status = 1;
+      break;
+    }
+    if (b == G) {
+      const bool root = pr < 0 || BF[pr] > G;
+      const float b2 = is_int ? T2[e.node] : (pr >= 0 ? fminf(T2[pr], e.score) : CWQ_INF);
+      if (full2 && (root ? gpops > 0 : !(b2 > tau2))) {
+        status = 1;
+        break;
+      }
+      ++gpops;
+    }
+    if (visited >= a.max_nodes) break;
+    const bool has_sent = is_int ? a.int_has_sent[e.node] != 0 : (a.row_flags[row] & FLAG_HAS_SENT) != 0;
+    if (has_sent) {
+      if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+      ++found;
+    }
+    if (found == a.k) break;
+    if (is_int) {
+      const int u = e.node;
+      calls += a.int_nchild[u];
+      for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
+        wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c}, lane);
+      for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint)
+        uint64_t bm = __ballot(l == 0 ? p1 == u : p2 == u);
+        while (bm) {
+          const int j = __builtin_ctzll(bm);
+          bm &= bm - 1;
+          const int r = l == 0 ? rl_i(w1, j) : rl_i(w2, j);
+          const float sc = l == 0 ? rl_f(x1, j) : rl_f(x2, j);
+          wheap_push(h, hn, HeapEnt{sc, e.score, a.row_bfs[r], -(r + 1)}, lane);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    a.n_found[q] = found < a.k ? found : a.k;
+    if (a.n_calls) a.n_calls[q] = calls;
+    a.status[q] = status;
+  }
+}
+
+hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
+  if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(simulate_two_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -1848,7 +1848,8 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
         mask &= mask - 1;
         const float ck = rl_f2(key, b), ca = rl_f2(lp, b);
         const int cr = __builtin_amdgcn_readlane(rid, b);
-        const bool prec = lk > ck || (lk == ck && lr < cr);
+        // categorize lists: the smaller own lp first among equal keys (list_before<true>)
+        const bool prec = lk > ck || (lk == ck && (cat && la != ca ? la < ca : lr < cr));
         const int pos = __popcll(__ballot(prec));
         if (pos < K) {
           const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));

@@ -180,11 +180,12 @@ class CobwebIndex:
 
     def last_categorize_stats(self):
         """How the last categorize call resolved its queries (cwq_last_stats after
-        cwq_categorize): counting over the bottleneck order, heap replay, DENSE re-runs."""
+        cwq_categorize): counting over the bottleneck order, heap replay, the two-level
+        replay of lists that end inside a bottleneck tie, DENSE re-runs."""
         out = np.zeros(6, np.int64)
         check(self._L.cwq_last_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return {"queries": int(out[0]), "dense_reruns": int(out[1]), "filter_reruns": int(out[2]),
-                "by_count": int(out[3]), "by_replay": int(out[4])}
+                "by_count": int(out[3]), "by_replay": int(out[4]), "two_level": int(out[5])}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -126,3 +126,99 @@ def test_count_formulation_equals_heap_search(seed):
     # not certified: two retrievals sharing one bottleneck above G (frequent here: 6-d
     # clusters put many leaves above their parents); the kernel replays those queries
     assert checked > 2 * skipped, (checked, skipped)
+
+
+def _two_level_search(nodes, x, k, max_nodes, order, R):
+    """The two-level replay of simulate_two_kernel on the oracle's tree:
+    list 1 = the top-R leaves by (b desc, own lp asc, BFS asc), G = its last key; list 2 =
+    the top-R leaves by the second-level key min(T2[parent], lp); the replay pushes every
+    internal child and only the listed leaves, and certifies every pop.  None: not
+    certified (the kernel hands the query to the DENSE re-run)."""
+    lp = {id(n): float(O.log_prob(n, x)) for n in nodes}
+    b = {}
+    for n in nodes:
+        b[id(n)] = lp[id(n)] if n.parent is None else min(b[id(n.parent)], lp[id(n)])
+    leaves = [n for n in nodes if not n.children]
+    key1 = {id(n): min(b[id(n.parent)], lp[id(n)]) if n.parent is not None else lp[id(n)] for n in leaves}
+    l1 = sorted(leaves, key=lambda n: (-key1[id(n)], lp[id(n)], order[id(n)]))[:R]
+    if len(l1) < R:
+        return None
+    G = key1[id(l1[-1])]
+    if not lp[id(l1[-1])] > G or nodes[0].children == []:
+        return None
+    t2 = {}
+    for n in nodes:                                   # cat_t2_kernel
+        if not n.children:
+            continue
+        if b[id(n)] != G:
+            t2[id(n)] = -np.inf
+            continue
+        m, cur = np.inf, n
+        while cur.parent is not None and not b[id(cur.parent)] > G:
+            m = min(m, lp[id(cur)])
+            cur = cur.parent
+        t2[id(n)] = m
+    key2 = {id(n): min(t2[id(n.parent)], lp[id(n)]) for n in leaves if n.parent is not None}
+    l2 = [n for n in sorted((n for n in leaves if n.parent is not None and key2[id(n)] > -np.inf),
+                            key=lambda n: (-key2[id(n)], lp[id(n)], order[id(n)]))[:R]]
+    full2 = len(l2) == R
+    tau2 = max(key2[id(l2[-1])], G) if full2 else -np.inf
+    keep = {id(n) for n in l1 if key1[id(n)] > G or (lp[id(n)] == G and b[id(n.parent)] > G)}
+    assert not keep & {id(n) for n in l2}
+    keep |= {id(n) for n in l2}
+    calls, visited, gpops, ret = 1, 0, 0, []
+    heap = [(-lp[id(nodes[0])], 0.0, order[id(nodes[0])], nodes[0])]
+    while heap:
+        neg, _p, _t, cur = heapq.heappop(heap)
+        visited += 1
+        if not b[id(cur)] >= G:
+            return None
+        if b[id(cur)] == G:
+            root = cur.parent is None or b[id(cur.parent)] > G
+            b2 = t2[id(cur)] if cur.children else min(t2[id(cur.parent)], lp[id(cur)])
+            if full2 and (gpops > 0 if root else not b2 > tau2):
+                return None
+            gpops += 1
+        if visited >= max_nodes:
+            break
+        if cur.sentence_id:
+            ret.append(cur)
+        if len(ret) == k:
+            break
+        for c in cur.children:
+            calls += 1
+            if c.children or id(c) in keep:
+                heapq.heappush(heap, (-lp[id(c)], -neg, order[id(c)], c))
+    return ret, calls
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_two_level_replay_equals_heap_search(seed):
+    """Clustered trees where a query's whole cluster shares one bottleneck (the cluster
+    node's lp is the lowest on its leaves' paths): list 1 ends inside that tie, and the
+    two-level replay must equal the heap search whenever it certifies -- and certify most
+    of these queries (the DENSE re-run is the exception, not the rule)."""
+    rng = np.random.default_rng(seed)
+    D, N, NC = 16, 700, 4
+    C = rng.standard_normal((NC, D)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, NC, N)] + 0.3 * rng.standard_normal((N, D))).astype(np.float32)
+    X[100:103] = X[20]                                # duplicates: exact-match leaves
+    t = O.OTree(D, rng=random.Random(seed))
+    for i, x in enumerate(X):
+        t.ifit(x).sentence_id.append(i)
+    nodes = O.bfs_nodes(t.root)
+    order = {id(n): i for i, n in enumerate(nodes)}
+    queries = [X[i] + 0.05 * rng.standard_normal(D).astype(np.float32) for i in range(0, N, 70)] + \
+              [C[j] + 0.3 * rng.standard_normal(D).astype(np.float32) for j in range(NC)] + [X[20]]
+    checked = skipped = tie = 0
+    for x in queries:
+        for k, R, mx in ((10, 64, 100000), (10, 16, 100000), (3, 8, 100000), (40, 64, 100000), (10, 64, 30)):
+            want = _heap_search(t.root, x, k, mx, order)
+            got = _two_level_search(nodes, x, k, mx, order, R)
+            if got is None:
+                skipped += 1
+                continue
+            checked += 1
+            assert [order[id(n)] for n in got[0]] == [order[id(n)] for n in want[0]], (k, R, mx)
+            assert got[1] == want[1], (k, R, mx)
+    assert checked > 3 * skipped, (checked, skipped)

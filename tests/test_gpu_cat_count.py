@@ -9,7 +9,10 @@ nodes in pop order, n_found, log_prob call counts -- on two-level and deep trees
 max_nodes cutting before / inside / after the retrievals, k from 1 to 64, perturbed
 queries (a leaf closer than its parent: b ties along the path) and duplicated rows
 (retrievals sharing one b: left to the replay).  The G1/G2/G4/G5 reference goldens go
-through the counting path in tests/test_gpu_parity.py."""
+through the counting path in tests/test_gpu_parity.py.  Lists that end inside a
+bottleneck tie (a cluster of more than 64 leaves under one node) go through the two-level
+replay (simulate_two_kernel), checked here against the DENSE re-run on device-ifit trees
+of clustered data, where nearly every query's list ends in such a tie."""
 import os
 
 import numpy as np
@@ -26,23 +29,36 @@ def gpu(pkg):
     return pkg
 
 
-def _both(ix, Q, k, max_nodes):
-    os.environ["CWQ_CAT_COUNT"] = "0"
+def _run(ix, Q, k, max_nodes, **env):
+    old = {n: os.environ.get(n) for n in env}
+    os.environ.update(env)
     try:
-        ref = ix.categorize(Q, k, max_nodes)
+        out = ix.categorize(Q, k, max_nodes)
         torch.cuda.synchronize()
+        return out, ix.last_categorize_stats()
     finally:
-        del os.environ["CWQ_CAT_COUNT"]
-    got = ix.categorize(Q, k, max_nodes)
-    torch.cuda.synchronize()
-    st = ix.last_categorize_stats()
-    for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
-        if not torch.equal(a, b):
-            bad = (a != b).reshape(a.shape[0], -1).any(1).nonzero().flatten()[:4].tolist()
-            raise AssertionError(f"{name} differs (k={k}, max_nodes={max_nodes}, stats {st}) at queries {bad}: "
-                                 f"replay {[a[i].tolist() for i in bad]} count {[b[i].tolist() for i in bad]}; "
-                                 f"found {[int(ref[1][i]) for i in bad]}, calls {[int(ref[2][i]) for i in bad]} vs "
-                                 f"{[int(got[2][i]) for i in bad]}")
+        for n, v in old.items():
+            if v is None:
+                del os.environ[n]
+            else:
+                os.environ[n] = v
+
+
+def _both(ix, Q, k, max_nodes):
+    """Counting path (default) and heap replay (CWQ_CAT_COUNT=0), both with the
+    two-level replay of tied lists, against the replay whose every uncertified query
+    goes DENSE (CWQ_CAT_COUNT=0 CWQ_CAT_TWO=0)."""
+    ref, _ = _run(ix, Q, k, max_nodes, CWQ_CAT_COUNT="0", CWQ_CAT_TWO="0")
+    rep, _ = _run(ix, Q, k, max_nodes, CWQ_CAT_COUNT="0")
+    got, st = _run(ix, Q, k, max_nodes)
+    for leg, res in (("replay", rep), ("count", got)):
+        for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, res):
+            if not torch.equal(a, b):
+                bad = (a != b).reshape(a.shape[0], -1).any(1).nonzero().flatten()[:4].tolist()
+                raise AssertionError(f"{leg}: {name} differs (k={k}, max_nodes={max_nodes}, stats {st}) at queries "
+                                     f"{bad}: dense {[a[i].tolist() for i in bad]} {leg} {[b[i].tolist() for i in bad]}; "
+                                     f"found {[int(ref[1][i]) for i in bad]}, calls {[int(ref[2][i]) for i in bad]} vs "
+                                     f"{[int(res[2][i]) for i in bad]}")
     return st
 
 
@@ -97,3 +113,31 @@ def test_count_flat_tree_and_small(gpu):
         if k <= 64:
             _both(ix, Q[:50], k, mx)
     ix.close()
+
+
+@pytest.mark.parametrize("filt", [-1, 0])
+def test_two_level_replay_on_clustered_ifit_tree(gpu, filt):
+    """A device-ifit tree of 40 Gaussian clusters (C2's generator at 64 dims): the leaves of
+    the query's cluster share the cluster node's lp as their bottleneck, so the top-64 list
+    ends inside that tie for nearly every query.  Two-level replay == DENSE on every query
+    (pop order, n_found, calls), for the filter and the exact-scan lists, and it must
+    resolve most of them."""
+    import random
+    rng = np.random.default_rng(5)
+    n, d, nc = 20_000, 64, 40
+    C = rng.standard_normal((nc, d)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, nc, n)] + 0.3 * rng.standard_normal((n, d))).astype(np.float32)
+    random.seed(5)
+    w = gpu.CobwebWrapper(corpus=None, corpus_embeddings=X)
+    w.build_prediction_index()
+    ix = w._index
+    ix.set_filter(filt)
+    Qn = np.concatenate([X[:192] + 0.05 * rng.standard_normal((192, d)),
+                         C[rng.integers(0, nc, 64)] + 0.3 * rng.standard_normal((64, d))]).astype(np.float32)
+    Q = torch.from_numpy(Qn).cuda()
+    two = 0
+    for k, mx in [(10, 100000), (1, 100000), (40, 100000), (63, 100000), (64, 100000), (10, 40), (10, 3)]:
+        st = _both(ix, Q, k, mx)
+        if (k, mx) == (10, 100000):
+            two = st["two_level"]
+    assert two >= 0.5 * Q.shape[0], two
