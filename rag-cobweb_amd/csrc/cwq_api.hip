@@ -545,15 +545,38 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   const int sdiv = sd && atoi(sd) > 0 ? atoi(sd) : 128;
   int S = (int)std::min<int64_t>(32768, std::max<int64_t>(kFgTile, NLi / sdiv / kFgTile * kFgTile));
   const int stride = std::max(1, NLi / S);
-  std::vector<int> srow(round_up(S, kFgTile), -1);
-  int ns = 0;
+  std::vector<int> srow;
+  srow.reserve(S);
   for (int j = 0; j < S; ++j) {
     const int64_t r = (int64_t)j * stride;
-    if (r < NLi) {
-      srow[j] = (int)r;
-      ns = j + 1;
+    if (r < NLi) srow.push_back((int)r);
+  }
+  if (ix->grp_mode) {
+    // clustered trees: the query's own cluster decides its top-k, and a strided sample
+    // holds only ~1/sdiv of it, so T stayed at other clusters' keys and most of the
+    // cluster passed the filter (C2 ifit tree: ~1,100 candidates per query, overflowing
+    // the record buffers).  Add kPerGroup rows of every group, spread over its rows
+    // (distinct rows only: T must bound the K-th best key over distinct rows).
+    constexpr int kPerGroup = 64;
+    std::vector<std::vector<int>> gr(ix->G);
+    for (int64_t r = 0; r < NLi; ++r)
+      if (rgrp[r] >= 0) gr[rgrp[r]].push_back((int)r);
+    std::vector<char> in(NLi, 0);
+    for (int r : srow) in[r] = 1;
+    for (int g = 0; g < ix->G && (int64_t)srow.size() + kPerGroup <= 32768; ++g) {
+      const int n = (int)gr[g].size();
+      const int m = std::min(n, kPerGroup);
+      for (int j = 0; j < m; ++j) {
+        const int r = gr[g][(int64_t)j * n / m];
+        if (!in[r]) {
+          in[r] = 1;
+          srow.push_back(r);
+        }
+      }
     }
   }
+  const int ns = (int)srow.size();
+  srow.resize(round_up(ns, kFgTile), -1);
   ix->n_samp = ns;
   ix->ld_s = (int)srow.size();
   if ((rc = ix->upload(&ix->samp_rows, srow, s))) return rc;

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--clusters", type=int, default=0)
     ap.add_argument("--balanced", default=None, help="B,L: a depth-L tree of branching B (synth.balanced_synth)")
     ap.add_argument("--rank-queries", type=int, default=64)
+    ap.add_argument("--max-nodes", type=int, default=100_000,
+                    help="categorize max_nodes (the wrapper's max_init_search); raise it so found-k = 1")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     dev = torch.device("cuda", 0)
@@ -57,11 +59,11 @@ def main():
     torch.cuda.empty_cache()
     tree = (f"balanced {args.balanced}" if args.balanced else f"two-level G={args.clusters}" if args.clusters
             else "flat")
-    dt, (nodes, found, calls) = timed(lambda: ix.categorize(Q, args.k), args.reps)
+    dt, (nodes, found, calls) = timed(lambda: ix.categorize(Q, args.k, args.max_nodes), args.reps)
     ok = float((found == args.k).float().mean())
-    print(f"categorize ({tree}, {args.n}x{args.dim}, k={args.k}): {dt * 1e3:.2f} ms per {args.queries} queries  "
-          f"{args.queries / dt:.0f} q/s  found-k fraction {ok:.3f}  mean log_prob calls {float(calls.float().mean()):.0f}",
-          flush=True)
+    print(f"categorize ({tree}, {args.n}x{args.dim}, k={args.k}, max_nodes={args.max_nodes}): {dt * 1e3:.2f} ms per "
+          f"{args.queries} queries  {args.queries / dt:.0f} q/s  found-k fraction {ok:.3f}  mean log_prob calls "
+          f"{float(calls.float().mean()):.0f}  resolved {ix.last_categorize_stats()}", flush=True)
     Qr = Q[:args.rank_queries]
     dt, out = timed(lambda: ix.rank_scores(Qr), args.reps)
     print(f"rank_scores ({tree}): {dt * 1e3:.2f} ms per {Qr.shape[0]} queries  {Qr.shape[0] / dt:.0f} q/s  "
