@@ -1331,6 +1331,11 @@ constexpr int kFiltMinRows = 16384;   // automatic mode: below this the exact sc
 constexpr int kFiltMaxK = 64;         // the filter serves the list-based top-k path (k <= 64)
 constexpr int kFgRecPerQ = 512;       // candidate-record slots per query (append buffer)
 constexpr int kFgDirPerQ = 256;       // direct-record slots per query (tiles past kFgCap)
+// Clustered (group-centred) trees: a query's whole cluster can pass -- categorize keys tie at
+// the cluster node's lp for every row of the cluster (~1,000 rows at C2) -- so the record
+// buffers hold 4x as many per query (48 KB instead of 12 KB per query).
+inline int rec_per_q(const cwq_index* ix) { return ix->grp_mode ? 4 * kFgRecPerQ : kFgRecPerQ; }
+inline int dir_per_q(const cwq_index* ix) { return ix->grp_mode ? 4 * kFgDirPerQ : kFgDirPerQ; }
 
 // min_rows: the automatic mode's threshold (the batch filter: kFiltMinRows; the per-call
 // stream path pays no batch pipeline and wins from a few hundred rows on -- the exact
@@ -1707,7 +1712,7 @@ struct IsoFilter {
 
 size_t iso_filter_bytes_per_query(const cwq_index* ix, int n_rt) {
   return (size_t)ix->DPB * 2 + 16 + (size_t)ix->ld_s * 4 + 64 * 8 + (size_t)kFgCapQ * 12 + 32 +
-         (size_t)(kFgRecPerQ + kFgDirPerQ) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
+         (size_t)(rec_per_q(ix) + dir_per_q(ix)) * 16 + 64 + ((size_t)2 * ix->cus * kFgChunk * 16) / 256 +
          (ix->n_multi_tiles ? (size_t)n_rt * 8 : 0) + 4 + 64 * 4;
 }
 
@@ -1737,11 +1742,11 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   float* cu = b.take<float>((size_t)nqf * kFgCapQ);
   float* cl = b.take<float>((size_t)nqf * kFgCapQ);
   // every workgroup holds one partly filled chunk at a time: keep room for two per workgroup
-  const int64_t rec_cap = round_up(std::max<int64_t>((int64_t)nqf * kFgRecPerQ, (int64_t)2 * ix->cus * kFgChunk),
+  const int64_t rec_cap = round_up(std::max<int64_t>((int64_t)nqf * rec_per_q(ix), (int64_t)2 * ix->cus * kFgChunk),
                                    kFgChunk);
   int4* rec = b.take<int4>((size_t)rec_cap);
   int* chunk_fill = b.take<int>((size_t)(rec_cap / kFgChunk));
-  const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * kFgDirPerQ, INT32_MAX / 2);
+  const int dir_cap = (int)std::min<int64_t>((int64_t)nqf * dir_per_q(ix), INT32_MAX / 2);
   int4* rec_dir = b.take<int4>((size_t)dir_cap);
   float2* pmm = (!cat && ix->n_multi_tiles) ? b.take<float2>((size_t)n_rt * nqf) : nullptr;
   HIPCHK(launch_query_prep(qsrc, nqc, ix->D, ix->iso_c, ix->DPB, nqf, Xb, qinfo, s));
