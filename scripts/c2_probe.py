@@ -93,7 +93,8 @@ def main():
     top1 = float((ids1[:len(pick), 0].cpu().numpy() == pick).mean())
     print(f"Fast batch nq={args.nq}: filter {t_f * 1e3:.3f} ms = {args.nq / t_f:.0f} q/s (exact scan "
           f"{t_scan * 1e3:.3f} ms = {args.nq / t_scan:.0f} q/s); ids/scores == exact scan: {same}; "
-          f"candidates/query {st['candidates']}, exact reranks {st['exact_reranks']}; "
+          f"candidates/query {st['candidates']}, exact reranks {st['exact_reranks']}, "
+          f"fallback queries {st['fallback_queries']}; "
           f"perturbed passage ranked first {top1:.3f}", flush=True)
     print(f"  last call phases (HIP events, ms): " + ", ".join(f"{a} {b:.3f}" for a, b in tm.items()), flush=True)
     # one query per call
@@ -111,6 +112,15 @@ def main():
         print(f"Fast per call nq={nq} (score_topk, device tensor): median {ts[len(ts) // 2] * 1e6:.1f} us, "
               f"p10 {ts[len(ts) // 10] * 1e6:.1f} us; path {st['path']} int8 {st['int8_pass']}; "
               f"== exact {ok}", flush=True)
+    # one query per call: phase times from HIP events (median over 30 calls)
+    ix.set_timing(True)
+    ph = []
+    for i in range(30):
+        ix.score_topk(Q[i:i + 1].contiguous(), k)
+        ph.append(ix.last_timing())
+    ix.set_timing(False)
+    print("  per-call phases (HIP events, median ms): " +
+          ", ".join(f"{n} {sorted(p[n] for p in ph)[15]:.4f}" for n in ph[0] if n.endswith("_ms")), flush=True)
     ts = []
     for i in range(args.calls):
         t0 = time.perf_counter()
