@@ -1514,11 +1514,12 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float4* qinfo8 = i8 ? b.take<float4>(nq16) : nullptr;
   int* Tb = b.take<int>((size_t)(K + 1) * nqc);   // [K][nq] blocks + [nq] live threshold
   float* T = b.take<float>(nqc);
-  int* qcnt = b.take<int>((size_t)5 * nqc);   // [qcnt | ok | n_exact | qover | done]
+  int* qcnt = b.take<int>((size_t)5 * nqc + 1);   // [qcnt | ok | n_exact | qover | done | select counter]
   int* okf = qcnt + nqc;
   int* nex = qcnt + 2 * nqc;
   int* qover = qcnt + 3 * nqc;
   int* done = qcnt + 4 * nqc;
+  int* sel_ctr = qcnt + 5 * nqc;
   int* crow = b.take<int>((size_t)nqc * capq);
   float* cu = b.take<float>((size_t)nqc * capq);
   float* cl = b.take<float>((size_t)nqc * capq);
@@ -1580,7 +1581,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
     HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
     if (i8) HIPCHK(launch_query_prep_i8(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xq, qinfo8, s));
-    HIPCHK(hipMemsetAsync(qcnt, 0, (size_t)5 * nqc * 4, s));
+    HIPCHK(hipMemsetAsync(qcnt, 0, ((size_t)5 * nqc + 1) * 4, s));
   }
   if ((rc = group_tables(ix, c, q, false, s))) return rc;
   const FiltConsts fc = filt_consts(ix->DPB);
@@ -1635,8 +1636,17 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.T0 = tl;
   a.ldT0 = 64;
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
+  // the select runs in the probe launch's last workgroup (one launch less per call);
+  // CWQ_SELECT_UNFUSED=1 keeps select_kernel (same thresholds: both run select_wave)
+  const bool fsel = !getenv("CWQ_SELECT_UNFUSED");
+  if (fsel) {
+    a.sel_ctr = sel_ctr;
+    a.sel_lk = tl;
+    a.sel_lr = tr;
+  }
   HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
-  HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
+  a.sel_ctr = nullptr;
+  if (!fsel) HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
   if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)
     StreamArgs a8 = a;

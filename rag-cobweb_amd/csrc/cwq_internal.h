@@ -534,6 +534,12 @@ struct StreamArgs {
   int* crow;                   // [nq][capq]
   float* cu;
   float* cl;
+  // probe with the select fused (sel_ctr set, zero at launch): the last workgroup to finish
+  // runs select_wave over lb and writes the top-K lists [nq][64] (sel_lk, sel_lr), as
+  // select_kernel does, then clears sel_ctr
+  int* sel_ctr;
+  float* sel_lk;
+  int* sel_lr;
 };
 hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s);   // 0 filter, 1 probe, 2 path dots
 hipError_t launch_stream_init(int* Tb, int n, hipStream_t s);

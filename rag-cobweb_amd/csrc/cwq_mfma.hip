@@ -305,6 +305,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
   }
   if (!valid) return;
   if (tid < 5) a.qcnt[(size_t)tid * a.nq + r] = 0;
+  if (r == 0 && tid == 5) a.qcnt[(size_t)5 * a.nq] = 0;   // the probe's fused-select counter
   if (a.NI == 0) return;
   // internal nodes: partials of (node n, slice v), straight from the caller's query
   float* part = s_sb + 2 * DQ;

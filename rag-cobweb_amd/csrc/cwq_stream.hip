@@ -335,6 +335,32 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   if (!idle)
     while (step(bA, bB) && step(bB, bA)) {
     }
+  if (MODE == 1 && a.sel_ctr) {
+    // fused select: the workgroup that finishes last (cross-workgroup protocol: every lb store
+    // of the workgroup complete, barrier, agent-scope release, then the counter) reads all of
+    // lb after an agent-scope acquire and writes the thresholds select_kernel would
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int prev = atomicAdd(a.sel_ctr, 1);
+      s_last = prev == (int)gridDim.x - 1;
+      if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (s_last) {
+      for (int q = wave; q < a.nq; q += SK_WAVES) {
+        float lk;
+        int lr;
+        select_wave(a.lb + (size_t)q * a.ldlb, (int)a.n_probe, a.K, lane, lk, lr);
+        a.sel_lk[(size_t)q * 64 + lane] = lk;
+        a.sel_lr[(size_t)q * 64 + lane] = lr;
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(a.sel_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (MODE != 0 || !SLB) return;
   // ---- flush the workgroup's candidate buffer: one global atomic per query ----
   __syncthreads();
