@@ -1480,6 +1480,14 @@ bool ensure_i8(cwq_index* ix, hipStream_t s) {
   return true;
 }
 
+// Workgroups of the per-call filter pass: one per CU (8 waves); CWQ_STREAM_WGS = m runs m
+// per CU (more loads in flight on short passes -- an A/B knob).
+int stream_wgs(const cwq_index* ix) {
+  const char* e = getenv("CWQ_STREAM_WGS");   // read per call: in-process A/Bs switch it
+  const int m = e && atoi(e) > 0 ? std::min(4, atoi(e)) : 1;
+  return ix->cus * m;
+}
+
 int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                      hipStream_t s) {
   const int K = k, kl = k <= 16 ? 16 : 64;
@@ -1655,9 +1663,9 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     a8.qinfo = qinfo8;
     a8.Mb = reinterpret_cast<const uint16_t*>(ix->iso_Mq);
     a8.rf = ix->iso_rf8;
-    HIPCHK(launch_stream(a8, 0, ix->cus, s));
+    HIPCHK(launch_stream(a8, 0, stream_wgs(ix), s));
   } else {
-    HIPCHK(launch_stream(a, 0, ix->cus, s));
+    HIPCHK(launch_stream(a, 0, stream_wgs(ix), s));
   }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
   int nst = 0;
