@@ -82,6 +82,7 @@ struct cwq_index {
   int max_depth = 0;
   int cus = 256;
   std::vector<std::pair<int, int>> levels;   // internal-node ranges, one per depth
+  int* d_lv = nullptr;                       // device copy: level starts + end [levels + 1]
   std::vector<void*> allocs;
   size_t bytes = 0;
   // row data
@@ -723,6 +724,9 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   }
   std::vector<int> node_src(n_nodes);
   for (int64_t nd = 0; nd < n_nodes; ++nd) node_src[nd] = int_id[nd] >= 0 ? int_id[nd] : -(row_of_node[nd] + 1);
+  std::vector<int> lv_starts;
+  for (auto& lv : ix->levels) lv_starts.push_back(lv.first);
+  lv_starts.push_back(ix->NI);
 
   // ---- device arrays ----
   const int DP = ix->DP;
@@ -782,6 +786,7 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   if ((rc = ix->upload(&ix->sent_ids, sids, s))) return rc;
   if ((rc = ix->upload(&ix->row_of_sent, row_of_sent, s))) return rc;
   if ((rc = ix->upload(&ix->node_src, node_src, s))) return rc;
+  if ((rc = ix->upload(&ix->d_lv, lv_starts, s))) return rc;
   if (ix->NL_iso > 0 && ix->NI >= 2 && ix->max_depth <= kMaxChain) {
     // internal-node bound operands: K = [x'^2, x'] -> DPB2 = fgemm width of 2*DP
     ix->DPB2 = fgemm_dpb(2 * ix->DP);
@@ -967,12 +972,14 @@ struct Chunk {
   // [Pg_lo, Pg_hi] and categorize [Pc_lo, Pc_hi] -- and the per-(query, group) shifts
   float *Pg_lo = nullptr, *Pg_hi = nullptr, *Pc_lo = nullptr, *Pc_hi = nullptr;
   double* gsh = nullptr;
+  int grp_done = -1;   // the group tables run_internal's fused pass wrote: -1 none, 0 Fast, 1 + categorize
 };
 
 // The group-centred rows' prefix tables of a chunk (after the exact internal pass wrote
 // c.P): q = the chunk's [nq][D] queries.  No-op without grp_mode.
 int group_tables(cwq_index* ix, Chunk& c, const float* q, bool cat, hipStream_t s) {
   if (!ix->grp_mode || ix->NI == 0) return CWQ_OK;
+  if (c.grp_done >= (cat ? 1 : 0)) return CWQ_OK;   // written by run_internal's fused pass
   HIPCHK(launch_group_prefixes(q, c.nq, ix->D, ix->iso_c, ix->grp_c, ix->G, c.P, c.ldP, ix->NI, ix->grp_par, ix->grp_F,
                                ix->grp_Fc, c.gsh, c.Pg_lo, c.Pg_hi, cat ? c.Pc_lo : nullptr, cat ? c.Pc_hi : nullptr,
                                s));
@@ -1033,17 +1040,66 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
 // Internal nodes: raw sums -> P (path prefix), BF (bottleneck), LPF (full lp).
 // bf_lpf: also the path bottleneck BF and full lp LPF (categorize / log_prob); the fast
 // keys need only P.
-int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true) {
+// The raw sums -> prefixes step of run_internal: one prefix_level_kernel launch per level,
+// or (several levels, up to kFinishMaxQ queries) one internal_finish_kernel launch -- a
+// workgroup per query walks the levels -- which also writes the group-centred rows'
+// prefix tables when q (the caller's queries) is given: grp_cat 0 Fast, 1 + categorize.
+constexpr int kFinishMaxQ = 2048;
+int internal_prefixes(cwq_index* ix, Chunk& c, hipStream_t s, float* BF, float* LPF, float dfull, const float* q,
+                      int grp_cat) {
+  const char* fe = getenv("CWQ_INT_FINISH");
+  const bool fin = ix->levels.size() > 1 && c.nq <= kFinishMaxQ && ix->d_lv && !(fe && *fe && atoi(fe) == 0);
+  if (!fin) {
+    for (auto& lv : ix->levels)
+      HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
+                                 dfull, c.P, BF, LPF, s));
+    return CWQ_OK;
+  }
+  IntFinishArgs f;
+  memset(&f, 0, sizeof(f));
+  f.S = c.S_int;
+  f.ldS = ix->NI;
+  f.nq = c.nq;
+  f.NI = ix->NI;
+  f.lv0 = ix->d_lv;
+  f.nlev = (int)ix->levels.size();
+  f.par_int = ix->par_int;
+  f.w_int = ix->w_int;
+  f.logdet_int = ix->logdet_int;
+  f.dfull = dfull;
+  f.P = c.P;
+  f.BF = BF;
+  f.LPF = LPF;
+  const bool grp = q && grp_cat >= 0 && ix->grp_mode && c.Pg_lo && ix->G > 0;
+  if (grp) {
+    f.q = q;
+    f.D = ix->D;
+    f.c0 = ix->iso_c;
+    f.cent = ix->grp_c;
+    f.G = ix->G;
+    f.grp = ix->grp_par;
+    f.F = ix->grp_F;
+    f.Fc = ix->grp_Fc;
+    f.sh = c.gsh;
+    f.Plo = c.Pg_lo;
+    f.Phi = c.Pg_hi;
+    f.Pclo = grp_cat ? c.Pc_lo : nullptr;
+    f.Pchi = grp_cat ? c.Pc_hi : nullptr;
+  }
+  HIPCHK(launch_internal_finish(f, s));
+  if (grp) c.grp_done = grp_cat;
+  return CWQ_OK;
+}
+
+int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true, const float* q = nullptr,
+                 int grp_cat = -1) {
   float* BF = bf_lpf ? c.BF : nullptr;
   float* LPF = bf_lpf ? c.LPF : nullptr;
   if (ix->NI == 0) return CWQ_OK;
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
   if (ix->NI <= kWave && (size_t)ix->DP * 8 <= 65536) {   // a few internal nodes: lane = query, same arithmetic
     HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, ix->NI, ix->DP, c.nq, c.S_int, ix->NI, s));
-    for (auto& lv : ix->levels)
-      HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
-                                 dfull, c.P, BF, LPF, s));
-    return CWQ_OK;
+    return internal_prefixes(ix, c, s, BF, LPF, dfull, q, grp_cat);
   }
   ScanArgs a = base_args(ix, c);
   // raw sums need no top-k list: the hot (list width 16, two rows per lane) configuration
@@ -1058,10 +1114,7 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true) {
   a.out = c.S_int;
   a.ldo = ix->NI;
   HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
-  for (auto& lv : ix->levels)
-    HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,
-                               dfull, c.P, BF, LPF, s));
-  return CWQ_OK;
+  return internal_prefixes(ix, c, s, BF, LPF, dfull, q, grp_cat);
 }
 
 int fg_order();
@@ -1583,7 +1636,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
-    } else if ((rc = run_internal(ix, c, s, false))) {
+    } else if ((rc = run_internal(ix, c, s, false, q, 0))) {
       return rc;
     }
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
@@ -1927,7 +1980,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q + q0 * ix->D, nqf, b, s))) return rc;
-    } else if ((rc = run_internal(ix, c, s, false))) {
+    } else if ((rc = run_internal(ix, c, s, false, q + q0 * ix->D, filt ? 0 : -1))) {
       return rc;
     }
     if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, false, s))) return rc;
@@ -2221,7 +2274,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HeapEnt* heap = b.take<HeapEnt>((size_t)nq_pad * cap_list);
     int* status = b.take<int>((size_t)nq_pad);
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s))) return rc;
+    if ((rc = run_internal(ix, c, s, true, q + q0 * ix->D, filt ? 1 : -1))) return rc;
     if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, true, s))) return rc;
     int nst = 0;
     std::vector<char> fbad(nqc, 0);

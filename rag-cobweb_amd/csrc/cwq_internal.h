@@ -151,6 +151,19 @@ hipError_t launch_int_small(const float* X, const float* A, const float* B, int6
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
                                float* LPF, hipStream_t s);
+// Internal nodes' raw sums -> prefixes in one launch (internal_finish_kernel, cwq_group.hip):
+// one workgroup per query walks the levels with prefix_level_kernel's arithmetic, then
+// (G > 0) the group-centred prefix tables with group_shift_kernel / group_pprime_kernel's.
+struct IntFinishArgs {
+  const float* S; int64_t ldS; int nq; int NI;
+  const int* lv0; int nlev;                      // level starts, lv0[nlev] = NI
+  const int* par_int; const float* w_int; const float* logdet_int; float dfull;
+  float* P; float* BF; float* LPF;               // [nq][ldS]; BF / LPF optional
+  const float* q; int D; const float* c0; const float* cent; int G;   // groups (G > 0)
+  const int* grp; const double* F; const double* Fc; double* sh;
+  float* Plo; float* Phi; float* Pclo; float* Pchi;
+};
+hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s);
 hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
                          const float* lkey, int R, float* T2, hipStream_t s);
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
