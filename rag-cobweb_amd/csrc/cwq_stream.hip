@@ -339,7 +339,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     // fused select: the workgroup that finishes last (cross-workgroup protocol: every lb store
     // of the workgroup complete, barrier, agent-scope release, then the counter) reads all of
     // lb after an agent-scope acquire and writes the thresholds select_kernel would
-    __shared__ int s_last;
+    // the flag lives in the query image's first word: every wave is past its last LDS read
+    // of it at the barrier below (a static __shared__ word would push the kernel past the
+    // dynamic-LDS maximum launch_one requests)
+    int& s_last = *reinterpret_cast<int*>(sq);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
