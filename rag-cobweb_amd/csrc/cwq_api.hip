@@ -83,6 +83,8 @@ struct cwq_index {
   int cus = 256;
   std::vector<std::pair<int, int>> levels;   // internal-node ranges, one per depth
   int* d_lv = nullptr;                       // device copy: level starts + end [levels + 1]
+  int* sel_ctr = nullptr;                    // per-call path: fused select counter (probe with fused prep)
+  float root_w0 = 0.f, root_logdet0 = 0.f;   // the root's w and logdet (host copies)
   std::vector<void*> allocs;
   size_t bytes = 0;
   // row data
@@ -787,6 +789,11 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
   if ((rc = ix->upload(&ix->row_of_sent, row_of_sent, s))) return rc;
   if ((rc = ix->upload(&ix->node_src, node_src, s))) return rc;
   if ((rc = ix->upload(&ix->d_lv, lv_starts, s))) return rc;
+  if (ix->NI > 0) {   // the root's terms (the per-call probe's fused prep forms its prefix)
+    ix->root_w0 = w_int[0];
+    HIPCHK(hipMemcpyAsync(&ix->root_logdet0, ix->logdet_int, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
   if (ix->NL_iso > 0 && ix->NI >= 2 && ix->max_depth <= kMaxChain) {
     // internal-node bound operands: K = [x'^2, x'] -> DPB2 = fgemm width of 2*DP
     ix->DPB2 = fgemm_dpb(2 * ix->DP);
@@ -1629,7 +1636,18 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (sp.nlev > 0) sp.lv0[sp.nlev] = ix->levels.back().second;
     if (ix->NI > 0 && (!c.P || sp.nlev == 0 || sp.lv0[0] != 0 || sp.lv0[sp.nlev] != ix->NI)) fused = false;
   }
-  if (fused) {
+  // flat trees, up to 16 queries, bf16 pass: the prep runs inside the probe launch
+  // (stream_kernel<1> with fprep) -- one launch less per call; CWQ_PROBE_PREP=0 keeps sb_prep
+  const char* fpe = getenv("CWQ_PROBE_PREP");
+  const bool fprep = fused && ix->NI == 1 && nqb == 1 && !i8 && ix->DP <= 1024 && !getenv("CWQ_SELECT_UNFUSED") &&
+                     !(fpe && *fpe && atoi(fpe) == 0);
+  if (fprep && !ix->sel_ctr) {   // the fused select's counter: zeroed once, reset by its last workgroup
+    if ((rc = ix->alloc(&ix->sel_ctr, 1))) return rc;
+    HIPCHK(hipMemsetAsync(ix->sel_ctr, 0, 4, s));
+  }
+  if (fprep) {
+    if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
+  } else if (fused) {
     HIPCHK(launch_sb_prep(sp, s));
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
   } else {
@@ -1701,12 +1719,30 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   // CWQ_SELECT_UNFUSED=1 keeps select_kernel (same thresholds: both run select_wave)
   const bool fsel = !getenv("CWQ_SELECT_UNFUSED");
   if (fsel) {
-    a.sel_ctr = sel_ctr;
+    a.sel_ctr = fprep ? ix->sel_ctr : sel_ctr;
     a.sel_lk = tl;
     a.sel_lr = tr;
   }
+  if (fprep) {
+    a.fprep = 1;
+    a.fq = q;
+    a.fc = ix->iso_c;
+    a.fD = ix->D;
+    a.fDP = ix->DP;
+    a.f_nq_pad = c.nq_pad;
+    a.fX = c.X;
+    a.fA = ix->int_A;
+    a.fB = ix->int_B;
+    a.fld = ix->ld_int;
+    a.fw0 = ix->root_w0;
+    a.flogdet0 = ix->root_logdet0;
+    a.fP = c.P;
+    a.fldP = std::max(ix->NI, 1);
+    a.fqcnt = qcnt;
+  }
   HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
   a.sel_ctr = nullptr;
+  a.fprep = 0;
   if (!fsel) HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
   if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)

@@ -553,6 +553,22 @@ struct StreamArgs {
   int* sel_ctr;
   float* sel_lk;
   int* sel_lr;
+  // probe with the query prep fused (flat trees, nq <= 16, bf16; fprep set): every workgroup
+  // forms the bf16 query fragments, the {|x'|^2, |x_hi|, |x_lo|} terms and the root's exact
+  // prefix itself (sb_prep_kernel's arithmetic), and workgroup 0 also writes them to Xb /
+  // qinfo / P with the scan-layout X and the cleared counters for the launches after it
+  int fprep;
+  const float* fq;             // [nq][D] caller queries
+  const float* fc;             // centre
+  int fD, fDP;
+  int64_t f_nq_pad;
+  float* fX;                   // scan layout, f_nq_pad rows
+  const float *fA, *fB;        // root row of the internal arrays, dim-major [DP][fld]
+  int64_t fld;
+  float fw0, flogdet0;         // root w and logdet
+  float* fP;                   // [nq][fldP] root prefix (column 0)
+  int64_t fldP;
+  int* fqcnt;                  // [5][nq] counters to clear
 };
 hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s);   // 0 filter, 1 probe, 2 path dots
 hipError_t launch_stream_init(int* Tb, int n, hipStream_t s);

@@ -97,24 +97,107 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   float* s_cl = s_cu + nqb * 16 * SLB;
   if (SLB)
     for (int i = threadIdx.x; i < nqb * 16; i += blockDim.x) s_cnt[i] = 0;
+  // fused prep (MODE 1, fprep): per-query terms and the root prefix, after the image
+  const bool fprep = MODE == 1 && a.fprep;
+  float4* s_qi = reinterpret_cast<float4*>(sq + (size_t)nqb * nkp * 1024);
+  float* s_pr = reinterpret_cast<float*>(s_qi + 16);
+  float* s_part = s_pr + 16;
   // ---- stage the queries' fragments (B operand: 16 B at k = (16/ES)*(l>>4).., query = l&15) ----
   for (int f = threadIdx.x; f < nqb * nkp * 64; f += blockDim.x) {
     const int l = f & 63, ks = (f >> 6) % nkp, qb = (f >> 6) / nkp;
     const int q = qb * 16 + (l & 15);
-    const uint4 v = ks < nk ? *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.Xb) +
-                                                              ((size_t)q * a.DPB * ES + ks * 64 + 16 * (l >> 4)))
-                            : make_uint4(0u, 0u, 0u, 0u);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (fprep) {
+      // sb_prep_kernel's bf16 hi parts of x - c, 8 dims per fragment
+      if (ks < nk && q < a.nq) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        const int d0 = ks * 32 + 8 * (l >> 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int d = d0 + j;
+          const float x = d < a.fD ? a.fq[(size_t)q * a.fD + d] - a.fc[d] : 0.f;
+          const __bf16 h = (__bf16)x;
+          w[j >> 1] |= (uint32_t)__builtin_bit_cast(uint16_t, h) << (16 * (j & 1));
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      if (blockIdx.x == 0 && ks < nk)   // the filter pass reads Xb (rows < 16 incl. zero padding)
+        *reinterpret_cast<uint4*>(const_cast<char*>(reinterpret_cast<const char*>(a.Xb)) +
+                                  ((size_t)q * a.DPB * ES + ks * 64 + 16 * (l >> 4))) = v;
+    } else if (ks < nk) {
+      v = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.Xb) +
+                                          ((size_t)q * a.DPB * ES + ks * 64 + 16 * (l >> 4)));
+    }
     *reinterpret_cast<uint4*>(sq + (size_t)f * 16) = v;
+  }
+  if (fprep) {
+    // {|x'|^2, |x_hi|, |x_lo|} per query row (sb_prep_kernel's loop and reduction; rows
+    // past nq are zero), one wave per row
+    for (int r = wave; r < 16; r += SK_WAVES) {
+      double sv = 0.0, slo = 0.0, shi = 0.0;
+      for (int d = lane; d < a.DPB; d += 64) {
+        const float x = (r < a.nq && d < a.fD) ? a.fq[(size_t)r * a.fD + d] - a.fc[d] : 0.f;
+        const __bf16 h = (__bf16)x;
+        const float hf = (float)h;
+        const float lo = x - hf;
+        sv += (double)x * (double)x;
+        slo += (double)lo * (double)lo;
+        shi += (double)hf * (double)hf;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        sv += __shfl_xor(sv, off, 64);
+        slo += __shfl_xor(slo, off, 64);
+        shi += __shfl_xor(shi, off, 64);
+      }
+      if (lane == 0) {
+        const float4 v4 = make_float4((float)sv, (float)(sqrt(shi) * (1.0 + 0x1p-20)), (float)(sqrt(slo) * (1.0 + 0x1p-20)),
+                                      0.f);
+        s_qi[r] = v4;
+        if (blockIdx.x == 0) const_cast<float4*>(a.qinfo)[r] = v4;
+      }
+    }
+    // the root's exact prefix: 16-dim fma partials in dimension order, summed in slice order
+    const int NV16 = a.fDP / 16;
+    for (int t = threadIdx.x; t < a.nq * NV16; t += blockDim.x) {
+      const int q = t / NV16, vv = t - q * NV16;
+      float pp = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int d = vv * 16 + j;
+        const float x = d < a.fD ? a.fq[(size_t)q * a.fD + d] : 0.f;
+        const float tt = fmaf(x, a.fA[(size_t)d * a.fld], -a.fB[(size_t)d * a.fld]);
+        pp = (j == 0) ? tt * tt : fmaf(tt, tt, pp);
+      }
+      s_part[t] = pp;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < a.nq) {
+      float acc = 0.f;
+      for (int vv = 0; vv < NV16; ++vv) acc += s_part[threadIdx.x * NV16 + vv];
+      const float P = a.fw0 * (-0.5f * (a.flogdet0 + acc));
+      s_pr[threadIdx.x] = P;
+      if (blockIdx.x == 0) a.fP[(size_t)threadIdx.x * a.fldP] = P;
+    }
+    if (blockIdx.x == 0) {
+      // the scan layout X [r/kXQ][v][r%kXQ][16] of the first query group, and the counters
+      for (int e = threadIdx.x; e < 16 * a.fDP; e += blockDim.x) {
+        const int r = e / a.fDP, d = e - r * a.fDP;
+        const size_t o = ((size_t)(d / 16) * kXQ + r) * 16 + (d % 16);
+        a.fX[o] = (r < a.nq && d < a.fD) ? a.fq[(size_t)r * a.fD + d] : 0.f;
+      }
+      for (int e = threadIdx.x; e < 5 * a.nq; e += blockDim.x) a.fqcnt[e] = 0;
+    }
   }
   // per-lane query terms for the lane's column (query qb*16 + (lane & 15))
   float4 qi[MQB];
   float Tq[MQB];
   bool qok[MQB];
+  if (fprep) __syncthreads();   // s_qi, s_pr written
 #pragma unroll
   for (int qb = 0; qb < MQB; ++qb) {
     const int q = qb * 16 + (lane & 15);
     qok[qb] = qb < nqb && q < a.nq;
-    qi[qb] = qok[qb] ? a.qinfo[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    qi[qb] = qok[qb] ? (fprep ? s_qi[q] : a.qinfo[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
     Tq[qb] = CWQ_INF;
     if (MODE == 0 && qok[qb]) {
       Tq[qb] = a.T0[(size_t)q * a.ldT0 + (a.K - 1)];
@@ -259,7 +342,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         for (int qb = 0; qb < MQB; ++qb) {
           cP[qb] = cPh[qb] = 0.f;
           if (!qok[qb] || cpar < 0) continue;
-          if (a.pb.dot) {
+          if (fprep) {   // flat tree: the root is every row's parent
+            cP[qb] = cPh[qb] = s_pr[qb * 16 + r16];
+          } else if (a.pb.dot) {
             pathb_bounds(a.pb, qb * 16 + r16, cpar, cP[qb], cPh[qb]);
           } else {
             const size_t o = pidx(a.ldP, a.pT, qb * 16 + r16, cpar);
@@ -415,7 +500,10 @@ hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s)
   b.slots = mode == 0 && stream_lds_bytes(a.nqb, a.DPB, i8, true) <= (size_t)kStreamMaxLds && !getenv("CWQ_STREAM_NOBUF")
                 ? kStreamSlots
                 : 0;
-  const size_t lds = stream_lds_bytes(a.nqb, a.DPB, i8, b.slots > 0);
+  const size_t lds = stream_lds_bytes(a.nqb, a.DPB, i8, b.slots > 0) +
+                     (mode == 1 && a.fprep ? (size_t)(16 + 16 + 16 * (a.fDP / 16)) * 16 : 0);
+  if (mode == 1 && a.fprep && (a.nqb != 1 || a.nq > 16 || a.fDP % 16 || a.fDP > 1024 || !a.fq || !a.fX || !a.fP))
+    return hipErrorInvalidValue;
   if (a.nq <= 0 || a.nqb * 16 < a.nq || a.nqb > SK_MAXQB || a.DPB % (i8 ? 64 : 32) || a.K < 1 || a.K > 64 ||
       lds > (size_t)kStreamMaxLds || n_wg < 1 || (mode == 1 ? a.n_probe : a.nrows) < 1)
     return hipErrorInvalidValue;
