@@ -1540,6 +1540,12 @@ bool ensure_i8(cwq_index* ix, hipStream_t s) {
   return true;
 }
 
+// CWQ_SELECT_UNFUSED=1: the per-call path keeps select_kernel (and sb_prep) -- A/B only
+bool sel_unfused() {
+  const char* e = getenv("CWQ_SELECT_UNFUSED");
+  return e && *e && atoi(e) != 0;
+}
+
 // Workgroups of the per-call filter pass: one per CU (8 waves); CWQ_STREAM_WGS = m runs m
 // per CU (more loads in flight on short passes -- an A/B knob).
 int stream_wgs(const cwq_index* ix) {
@@ -1639,7 +1645,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   // flat trees, up to 16 queries, bf16 pass: the prep runs inside the probe launch
   // (stream_kernel<1> with fprep) -- one launch less per call; CWQ_PROBE_PREP=0 keeps sb_prep
   const char* fpe = getenv("CWQ_PROBE_PREP");
-  const bool fprep = fused && ix->NI == 1 && nqb == 1 && !i8 && ix->DP <= 1024 && !getenv("CWQ_SELECT_UNFUSED") &&
+  const bool fprep = fused && ix->NI == 1 && nqb == 1 && !i8 && ix->DP <= 1024 && !sel_unfused() &&
                      !(fpe && *fpe && atoi(fpe) == 0);
   if (fprep && !ix->sel_ctr) {   // the fused select's counter: zeroed once, reset by its last workgroup
     if ((rc = ix->alloc(&ix->sel_ctr, 1))) return rc;
@@ -1717,7 +1723,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
   // the select runs in the probe launch's last workgroup (one launch less per call);
   // CWQ_SELECT_UNFUSED=1 keeps select_kernel (same thresholds: both run select_wave)
-  const bool fsel = !getenv("CWQ_SELECT_UNFUSED");
+  const bool fsel = !sel_unfused();
   if (fsel) {
     a.sel_ctr = fprep ? ix->sel_ctr : sel_ctr;
     a.sel_lk = tl;
