@@ -160,6 +160,7 @@ int cwq_prefix_bounds(cwq_index* idx, const float* q, int64_t nq, float* lo, flo
  * / _cobweb_categorize with retrieve_k=k (CobwebTorchTree.py:235-310) as called by
  * CobwebWrapper.cobweb_predict (CobwebWrapper.py:435-461).
  *   nodes     device [nq*k] int64: BFS indices of the retrieved nodes in pop order
+ *             (-1 past n_found)
  *   n_found   device [nq] int32: number retrieved (< k where the reference raises
  *             IndexError: too few leaves, or max_nodes reached, :264-289)
  *   n_calls   device [nq] int64: log_prob evaluations the reference would make
@@ -202,7 +203,8 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  * After cwq_categorize, cwq_last_stats reports instead: [queries, queries re-run with
  * every leaf row materialised (DENSE), queries re-run after a filter list overflow,
  * queries resolved by counting over the bottleneck order, queries resolved by the heap
- * replay, 0].
+ * replay, queries the two-level replay resolved after their list ended inside a
+ * bottleneck tie].
  */
 int cwq_set_filter(cwq_index* idx, int mode);
 int cwq_last_stats(cwq_index* idx, int64_t* out6);

@@ -2619,7 +2619,9 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   if (wu.rc) return wu.rc;
   const int rc = categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
   ix->stats[0] = nq;
-  return rc;
+  if (rc) return rc;
+  HIPCHK(launch_clear_tail(nodes, n_found, nq, k, s));
+  return CWQ_OK;
 }
 
 extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order,

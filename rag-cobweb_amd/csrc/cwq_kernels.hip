@@ -1437,6 +1437,20 @@ __global__ __launch_bounds__(256) void simulate_two_kernel(const SimArgs a) {
   }
 }
 
+// nodes[q][i] = -1 for i >= n_found[q]: the entries past a query's retrievals are defined
+// whichever path (count, replay, two-level, DENSE) resolved it.
+__global__ void clear_tail_kernel(int64_t* nodes, const int* n_found, int64_t nq, int k) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= nq * k) return;
+  if ((int)(t % k) >= n_found[t / k]) nodes[t] = -1;
+}
+
+hipError_t launch_clear_tail(int64_t* nodes, const int* n_found, int64_t nq, int k, hipStream_t s) {
+  if (nq <= 0 || k <= 0) return hipSuccess;
+  hipLaunchKernelGGL(clear_tail_kernel, dim3((unsigned)((nq * k + 255) / 256)), dim3(256), 0, s, nodes, n_found, nq, k);
+  return hipGetLastError();
+}
+
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
   if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
   hipLaunchKernelGGL(simulate_two_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a);
