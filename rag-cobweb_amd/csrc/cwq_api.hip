@@ -1048,14 +1048,15 @@ ScanArgs base_args(const cwq_index* ix, const Chunk& c) {
 // bf_lpf: also the path bottleneck BF and full lp LPF (categorize / log_prob); the fast
 // keys need only P.
 // The raw sums -> prefixes step of run_internal: one prefix_level_kernel launch per level,
-// or (several levels, up to kFinishMaxQ queries) one internal_finish_kernel launch -- a
-// workgroup per query walks the levels -- which also writes the group-centred rows'
+// or (several levels, a few queries, shallow trees) internal_chain_kernel -- one thread per
+// (query, node) down its path, same values -- which also writes the group-centred rows'
 // prefix tables when q (the caller's queries) is given: grp_cat 0 Fast, 1 + categorize.
-constexpr int kFinishMaxQ = 2048;
+constexpr int kChainMaxQ = 64, kChainMaxDepth = 16;
 int internal_prefixes(cwq_index* ix, Chunk& c, hipStream_t s, float* BF, float* LPF, float dfull, const float* q,
                       int grp_cat) {
   const char* fe = getenv("CWQ_INT_FINISH");
-  const bool fin = ix->levels.size() > 1 && c.nq <= kFinishMaxQ && ix->d_lv && !(fe && *fe && atoi(fe) == 0);
+  const bool fin = ix->levels.size() > 1 && c.nq <= kChainMaxQ && ix->max_depth <= kChainMaxDepth &&
+                   !(fe && *fe && atoi(fe) == 0);
   if (!fin) {
     for (auto& lv : ix->levels)
       HIPCHK(launch_prefix_level(c.S_int, ix->NI, c.nq, lv.first, lv.second, ix->par_int, ix->w_int, ix->logdet_int,

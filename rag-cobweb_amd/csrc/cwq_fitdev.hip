@@ -140,6 +140,7 @@ struct FitDev {
   int fork_min;                 // fork a level's KL pass when it has >= fork_min children
   uint64_t spin_ticks;          // bound of every spin (100 MHz steady counter ticks)
   int* dbg;                     // [16] progress words (read back by the host on FD_HANG)
+  int prof;                     // CWQ_FIT_PROFILE: forked levels' phase ticks into dbg[8..13], count dbg[14]
 };
 
 constexpr int kFdThreads = 1024;
@@ -809,6 +810,15 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         break;
       }
       // ---- internal node: the CU terms of every operation ----
+      const bool prof = f.prof && f.dbg && f.job != nullptr && b >= f.fork_min;
+      uint64_t tprev = prof ? (uint64_t)wall_clock64() : 0;
+      auto stamp = [&](int k) {   // thread 0: ticks since the previous stamp into dbg[8 + k]
+        if (prof && tid == 0) {
+          const uint64_t t = (uint64_t)wall_clock64();
+          atomicAdd(&f.dbg[8 + k], (int)(t - tprev));
+          tprev = t;
+        }
+      };
       const float cP = f.count[cur];
       for (int d = tid; d < D; d += kFdThreads) {   // P + x (mean_var_insert of the parent)
         float m, v;
@@ -846,6 +856,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         }
       }
       __syncthreads();
+      stamp(0);   // the KL pass (fork / join)
       // fp32 terms per child (parallel; numpy's elementwise float32 ops of fit.py)
       const float nP1 = cP + 1.0f;
       for (int j = tid; j < b; j += kFdThreads) {
@@ -860,6 +871,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         f.ncv[j] = nc;
       }
       __syncthreads();
+      stamp(1);   // the per-child terms
       // two_best_children: one random() per child, in list order
       int i1 = -1, i2 = -1;
       if (forked) {
@@ -894,6 +906,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           __syncthreads();
         }
       }
+      stamp(2);   // two_best_children
       // pu sums (sequential float32 in list order -- Python's `score += ...`): chunks of
       // the terms staged in LDS, the three sums run side by side by thread 0
       float q_all = 0.f, q_ins = 0.f, q_keep = 0.f;
@@ -922,6 +935,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           __syncthreads();
         }
       }
+      stamp(3);   // the pu sums
       // the operation choice: thread 0
       if (tid == 0) {
         const float knew = f.kres[2 * b];
@@ -1007,6 +1021,31 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         }
       }
       __syncthreads();
+      if (do_split) {
+        // the split's partition-utility sum, sequential float32 in list order (Python's
+        // `score += ...`): the terms formed by all threads into LDS chunks (their KL results
+        // and counts are global loads -- one at a time in thread 0 they were a serial chain
+        // of uncached loads, milliseconds at fan-out 16k), thread 0 adds them in order
+        float ssum = 0.f;
+        bool sfirst = true;
+        for (int c0 = 0; c0 < n_split; c0 += kFdChunk) {
+          const int m = n_split - c0 < kFdChunk ? n_split - c0 : kFdChunk;
+          for (int j = tid; j < m; j += kFdThreads) {
+            const int jj = c0 + j;
+            const float ks = split_forked ? ld_agent_f(&f.kres[2 * b + 1 + jj]) : f.kres[2 * b + 1 + jj];
+            sh.cg[j] = (f.count[f.jobs[jj]] / cP) * ks;
+          }
+          __syncthreads();
+          if (tid == 0)
+            for (int j = 0; j < m; ++j) {
+              ssum = sfirst ? sh.cg[j] : ssum + sh.cg[j];
+              sfirst = false;
+            }
+          __syncthreads();
+        }
+        if (tid == 0) sh.cf[4] = ssum;
+        __syncthreads();
+      }
       if (tid == 0) {
         // get_best_operation: max of (pu, random(), name); names "best" < "merge" < "new" < "split"
         float bp = pu_best;
@@ -1029,15 +1068,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           offer(pu_merge, r, 1);
         }
         if (do_split) {
-          float s = 0.f;
-          bool first = true;
-          for (int j = 0; j < n_split; ++j) {
-            const float ks = split_forked ? ld_agent_f(&f.kres[2 * b + 1 + j]) : f.kres[2 * b + 1 + j];
-            const float t = (f.count[f.jobs[j]] / cP) * ks;
-            s = first ? t : s + t;
-            first = false;
-          }
-          const float pu_split = s / (float)(b - 1 + f.ccnt[b1]);
+          const float pu_split = sh.cf[4] / (float)(b - 1 + f.ccnt[b1]);
           const double r = mt_random(sh.mt, mt_idx);
           drawn += 1;
           offer(pu_split, r, 3);
@@ -1045,6 +1076,8 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         sh.ci[7] = bn;
       }
       __syncthreads();
+      stamp(4);   // merge / split terms and the choice
+      if (prof && tid == 0) atomicAdd(&f.dbg[14], 1);
       const int op = sh.ci[7];
       __syncthreads();
       if (op == 0) {          // best: into b1
@@ -1252,6 +1285,7 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   if (const char* e = getenv("CWQ_FIT_FORK_MIN")) f.fork_min = atoi(e) < 2 ? 2 : atoi(e);
   f.spin_ticks = kFdSpinTicks;
   if (const char* e = getenv("CWQ_FIT_SPIN_MS")) f.spin_ticks = (uint64_t)(atoll(e) > 0 ? atoll(e) : 1) * 100000ull;
+  f.prof = getenv("CWQ_FIT_PROFILE") ? 1 : 0;
   if (helpers == 0) f.job = nullptr;
   else if (hipMemsetAsync(f.job, 0, sizeof(FdJob), s) != hipSuccess || hipMemsetAsync(f.dbg, 0, 64, s) != hipSuccess)
     return fit_fail(CWQ_ERR_HIP, "job reset failed");
@@ -1283,6 +1317,13 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   info[1] = c64[2];
   info[2] = ctrl[3];
   info[3] = ctrl[0];
+  if (f.prof && f.dbg && f.job) {   // diagnostics: where a forked level's time goes (100 MHz ticks)
+    int dbg[16];
+    if (hipMemcpy(dbg, f.dbg, 64, hipMemcpyDeviceToHost) == hipSuccess && dbg[14] > 0)
+      fprintf(stderr, "[fit profile] %d forked levels, us per level: KL pass %.1f, child terms %.1f, top-2 %.1f, "
+                      "pu sums %.1f, merge/split + choice %.1f\n", dbg[14], dbg[8] * 0.01 / dbg[14],
+              dbg[9] * 0.01 / dbg[14], dbg[10] * 0.01 / dbg[14], dbg[11] * 0.01 / dbg[14], dbg[12] * 0.01 / dbg[14]);
+  }
   if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");
   if (ctrl[3] == FD_HANG) {
     int dbg[16];

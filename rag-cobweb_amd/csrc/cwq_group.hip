@@ -153,83 +153,78 @@ hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0,
   return hipGetLastError();
 }
 
-// One workgroup per query: the internal nodes' prefixes level by level (P = fmaf(w, lp',
-// P[parent]), BF = min(BF[parent], lp), LPF = lp -- prefix_level_kernel's arithmetic; the
-// workgroup barrier between levels orders a parent's store before its children's loads),
-// then the group shifts (group_shift_kernel's loop and reduction, one wave per group) and
-// the outward-rounded prefix tables (group_pprime_kernel).  Replaces one launch per tree
-// level plus two: at one query per call on C2's depth-9 ifit tree that is 11 launches.
-__global__ __launch_bounds__(512) void internal_finish_kernel(const IntFinishArgs f) {
-  const int qi = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+// Internal prefixes for a few queries in one launch: one thread per (query, node) forms
+// the node's P, BF, LPF from the root down its path -- the ancestor t levels above found
+// by walking parents (depth^2 parent loads, no local array) -- with prefix_level_kernel's
+// arithmetic in the same order (P = fmaf(w, lp', P) per level, BF = fminf chain), so the
+// values are the per-level launches' bit for bit; then (G > 0) the group-centred prefix
+// tables from the shifts group_shift_kernel wrote.  At one query per call on C2's
+// depth-9 ifit tree this replaces one launch per level plus one (a workgroup per query
+// walking the levels measured 293 us: each level a chain of dependent loads).
+__global__ void internal_chain_kernel(const IntFinishArgs f) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)f.nq * f.NI) return;
+  const int qi = (int)(t / f.NI);
+  const int i = (int)(t % f.NI);
   const size_t ro = (size_t)qi * f.ldS;
-  for (int lv = 0; lv < f.nlev; ++lv) {
-    const int i1 = f.lv0[lv + 1];
-    for (int i = f.lv0[lv] + tid; i < i1; i += blockDim.x) {
-      const size_t o = ro + i;
-      const float sv = f.S[o];
-      const float ld = f.logdet_int[i];
-      const float lp = -0.5f * (ld + sv);
-      const float lpf = -0.5f * (ld + f.dfull + sv);
-      const int p = f.par_int[i];
-      if (p >= 0) {
-        const size_t op = ro + p;
-        f.P[o] = fmaf(f.w_int[i], lp, f.P[op]);
-        if (f.BF) f.BF[o] = fminf(f.BF[op], lpf);
-      } else {
-        f.P[o] = f.w_int[i] * lp;
-        if (f.BF) f.BF[o] = lpf;
-      }
-      if (f.LPF) f.LPF[o] = lpf;
+  int d = 0;
+  for (int a = i; f.par_int[a] >= 0; a = f.par_int[a]) ++d;
+  float P = 0.f, B = 0.f, lpf = 0.f;
+  for (int l = d; l >= 0; --l) {   // the ancestor l levels above i, root first
+    int a = i;
+    for (int u = 0; u < l; ++u) a = f.par_int[a];
+    const float sv = f.S[ro + a];
+    const float ld = f.logdet_int[a];
+    const float lp = -0.5f * (ld + sv);
+    lpf = -0.5f * (ld + f.dfull + sv);
+    if (l == d) {
+      P = f.w_int[a] * lp;
+      B = lpf;
+    } else {
+      P = fmaf(f.w_int[a], lp, P);
+      B = fminf(B, lpf);
     }
-    __syncthreads();
   }
+  const size_t o = ro + i;
+  f.P[o] = P;
+  if (f.BF) f.BF[o] = B;
+  if (f.LPF) f.LPF[o] = lpf;
   if (f.G <= 0) return;
-  for (int g = wave; g < f.G; g += nw) {
-    double a = 0.0;
-    for (int d = lane; d < f.D; d += 64) {
-      const float xc = f.q[(size_t)qi * f.D + d] - f.c0[d];
-      const double dd = (double)f.cent[(size_t)g * f.D + d] - (double)f.c0[d];
-      a += (double)xc * dd;
-    }
-    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
-    if (lane == 0) f.sh[(size_t)qi * f.G + g] = -2.0 * a;
-  }
-  __syncthreads();
-  for (int p = tid; p < f.NI; p += blockDim.x) {
-    const int g = f.grp[p];
-    const size_t o = ro + p;
-    const float pv = f.P[o];
-    if (g < 0) {
-      f.Plo[o] = pv;
-      f.Phi[o] = pv;
-      if (f.Pclo) {
-        f.Pclo[o] = 0.f;
-        f.Pchi[o] = 0.f;
-      }
-      continue;
-    }
-    const double sv = f.sh[(size_t)qi * f.G + g];
-    const double a = f.F[p] * sv;
-    const double t = (double)pv + a;
-    float lo, hi;
-    out_round(t, (fabs((double)pv) + fabs(a)) * 0x1p-50, lo, hi);
-    f.Plo[o] = lo;
-    f.Phi[o] = hi;
+  const int g = f.grp[i];
+  if (g < 0) {
+    f.Plo[o] = P;
+    f.Phi[o] = P;
     if (f.Pclo) {
-      const double c = f.Fc[p] * sv;
-      out_round(c, fabs(c) * 0x1p-50, lo, hi);
-      f.Pclo[o] = lo;
-      f.Pchi[o] = hi;
+      f.Pclo[o] = 0.f;
+      f.Pchi[o] = 0.f;
     }
+    return;
+  }
+  const double sv = f.sh[(size_t)qi * f.G + g];
+  const double a = f.F[i] * sv;
+  const double tt = (double)P + a;
+  float lo, hi;
+  out_round(tt, (fabs((double)P) + fabs(a)) * 0x1p-50, lo, hi);
+  f.Plo[o] = lo;
+  f.Phi[o] = hi;
+  if (f.Pclo) {
+    const double c = f.Fc[i] * sv;
+    out_round(c, fabs(c) * 0x1p-50, lo, hi);
+    f.Pclo[o] = lo;
+    f.Pchi[o] = hi;
   }
 }
 
 hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s) {
   if (f.nq <= 0 || f.NI <= 0) return hipSuccess;
-  if (!f.lv0 || f.nlev <= 0 || f.ldS < f.NI || (f.G > 0 && (!f.q || !f.sh || !f.Plo || !f.Phi)))
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(internal_finish_kernel, dim3((unsigned)f.nq), dim3(512), 0, s, f);
+  if (f.ldS < f.NI || (f.G > 0 && (!f.q || !f.sh || !f.Plo || !f.Phi))) return hipErrorInvalidValue;
+  if (f.G > 0) {   // the shifts first (one wave per (query, group))
+    const int64_t nw = (int64_t)f.nq * f.G;
+    hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, f.q, (int64_t)f.nq, f.D,
+                       f.c0, f.cent, f.G, f.sh);
+  }
+  const int64_t n = (int64_t)f.nq * f.NI;
+  hipLaunchKernelGGL(internal_chain_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f);
   return hipGetLastError();
 }
 

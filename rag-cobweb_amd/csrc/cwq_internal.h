@@ -151,9 +151,10 @@ hipError_t launch_int_small(const float* X, const float* A, const float* B, int6
 hipError_t launch_prefix_level(const float* S, int64_t ldS, int nq, int i0, int i1, const int* par_int,
                                const float* w_int, const float* logdet_int, float dfull, float* P, float* BF,
                                float* LPF, hipStream_t s);
-// Internal nodes' raw sums -> prefixes in one launch (internal_finish_kernel, cwq_group.hip):
-// one workgroup per query walks the levels with prefix_level_kernel's arithmetic, then
-// (G > 0) the group-centred prefix tables with group_shift_kernel / group_pprime_kernel's.
+// Internal nodes' raw sums -> prefixes for a few queries (internal_chain_kernel,
+// cwq_group.hip): one thread per (query, node) down the node's path with
+// prefix_level_kernel's arithmetic, then (G > 0) the group-centred prefix tables with
+// group_shift_kernel / group_pprime_kernel's.
 struct IntFinishArgs {
   const float* S; int64_t ldS; int nq; int NI;
   const int* lv0; int nlev;                      // level starts, lv0[nlev] = NI
