@@ -1643,11 +1643,13 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (sp.nlev > 0) sp.lv0[sp.nlev] = ix->levels.back().second;
     if (ix->NI > 0 && (!c.P || sp.nlev == 0 || sp.lv0[0] != 0 || sp.lv0[sp.nlev] != ix->NI)) fused = false;
   }
-  // flat trees, up to 16 queries, bf16 pass: the prep runs inside the probe launch
-  // (stream_kernel<1> with fprep) -- one launch less per call; CWQ_PROBE_PREP=0 keeps sb_prep
+  // flat trees, up to 16 queries, bf16 pass: the prep inside the probe launch (stream_kernel<1>
+  // with fprep) -- one launch less, but measured slower (C2 one query per call 101.5 ->
+  // 104.9 us: the probe's workgroups all wait for the prep, profiles/r04_percall_ab_c2_v1.log),
+  // so opt-in: CWQ_PROBE_PREP=1
   const char* fpe = getenv("CWQ_PROBE_PREP");
   const bool fprep = fused && ix->NI == 1 && nqb == 1 && !i8 && ix->DP <= 1024 && !sel_unfused() &&
-                     !(fpe && *fpe && atoi(fpe) == 0);
+                     (fpe && *fpe && atoi(fpe) == 1);
   if (fprep && !ix->sel_ctr) {   // the fused select's counter: zeroed once, reset by its last workgroup
     if ((rc = ix->alloc(&ix->sel_ctr, 1))) return rc;
     HIPCHK(hipMemsetAsync(ix->sel_ctr, 0, 4, s));

@@ -22,6 +22,7 @@
 // (lane stride 64) then a butterfly, rounded once -- exactly cwq_fit_kl's arithmetic,
 // so this and the host-driven fitter (fit.py TreeFitter.ifit) build identical trees.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -188,7 +189,8 @@ struct FdShared {
   float muP[kFdMaxD], vP[kFdMaxD], lvP[kFdMaxD];
   uint32_t mt[kMtN];
   uint32_t mtn[kMtN];   // the parallel twist's new words
-  float cg[kFdChunk], cn[kFdChunk];
+  alignas(16) float cg[kFdChunk];
+  float cn[kFdChunk];
   int ci[8];
   float cf[8];
   double cr[2];   // random() of "best" and "new"
@@ -908,32 +910,66 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       }
       stamp(2);   // two_best_children
       // pu sums (sequential float32 in list order -- Python's `score += ...`): chunks of
-      // the terms staged in LDS, the three sums run side by side by thread 0
+      // the terms staged in LDS by all threads; the three sums are three dependent chains,
+      // so each runs in its own wave (lane 0; waves 0-2 sit on different SIMDs) with its
+      // values read 8 at a time (two ds_read_b128 ahead of the adds).  One thread running
+      // all three with a read per value was 1.3 ms per level at fan-out 19k -- 90% of a
+      // chip-wide insert (profiles/r04_fit_flat20k_profile_v1.log).
       float q_all = 0.f, q_ins = 0.f, q_keep = 0.f;
       {
-        bool first_all = true, first_ins = true, first_keep = true;
+        float acc = 0.f;
+        bool fst = true;
+        const float tins1 = (wave == 1 && lane == 0 && i1 >= 0) ? f.tins[i1] : 0.f;
+        // chain W over this chunk (W: 0 all, 1 ins, 2 keep), a loop per chain so that no
+        // branch on the chain sits inside it
+        auto chain = [&](auto wtag, int c0, int m) {
+          constexpr int W = decltype(wtag)::value;
+          auto step = [&](int j, float ta) {
+            if constexpr (W == 0) {
+              acc = fst ? ta : acc + ta;
+              fst = false;
+            } else if constexpr (W == 1) {
+              const float ti = j == i1 ? tins1 : ta;
+              acc = fst ? ti : acc + ti;
+              fst = false;
+            } else {
+              if (j != i1 && j != i2) {
+                acc = fst ? ta : acc + ta;
+                fst = false;
+              }
+            }
+          };
+          int jj = 0;
+          for (; jj + 8 <= m; jj += 8) {
+            float4 v4[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) v4[u] = *reinterpret_cast<const float4*>(&sh.cg[jj + 4 * u]);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              step(c0 + jj + 4 * u, v4[u].x);
+              step(c0 + jj + 4 * u + 1, v4[u].y);
+              step(c0 + jj + 4 * u + 2, v4[u].z);
+              step(c0 + jj + 4 * u + 3, v4[u].w);
+            }
+          }
+          for (; jj < m; ++jj) step(c0 + jj, sh.cg[jj]);
+        };
         for (int c0 = 0; c0 < b; c0 += kFdChunk) {
           const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
           for (int j = tid; j < m; j += kFdThreads) sh.cg[j] = f.tall[c0 + j];
           __syncthreads();
-          if (tid == 0) {
-            const float tins1 = (i1 >= c0 && i1 < c0 + m) ? f.tins[i1] : 0.f;
-            for (int jj = 0; jj < m; ++jj) {
-              const int j = c0 + jj;
-              const float ta = sh.cg[jj];
-              const float ti = j == i1 ? tins1 : ta;
-              q_all = first_all ? ta : q_all + ta;
-              first_all = false;
-              q_ins = first_ins ? ti : q_ins + ti;
-              first_ins = false;
-              if (j != i1 && j != i2) {
-                q_keep = first_keep ? ta : q_keep + ta;
-                first_keep = false;
-              }
-            }
+          if (lane == 0) {
+            if (wave == 0) chain(std::integral_constant<int, 0>{}, c0, m);
+            else if (wave == 1) chain(std::integral_constant<int, 1>{}, c0, m);
+            else if (wave == 2) chain(std::integral_constant<int, 2>{}, c0, m);
           }
           __syncthreads();
         }
+        if (lane == 0 && (wave == 1 || wave == 2)) sh.cf[4 + wave] = acc;   // cf[5] ins, cf[6] keep
+        if (wave == 0) q_all = acc;
+        __syncthreads();
+        q_ins = sh.cf[5];
+        q_keep = sh.cf[6];
       }
       stamp(3);   // the pu sums
       // the operation choice: thread 0
@@ -1036,11 +1072,27 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
             sh.cg[j] = (f.count[f.jobs[jj]] / cP) * ks;
           }
           __syncthreads();
-          if (tid == 0)
-            for (int j = 0; j < m; ++j) {
+          if (tid == 0) {
+            int j = 0;
+            for (; j + 16 <= m; j += 16) {   // 16 values read ahead of their adds
+              float4 v4[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) v4[u] = *reinterpret_cast<const float4*>(&sh.cg[j + 4 * u]);
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const float t4[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  ssum = sfirst ? t4[e] : ssum + t4[e];
+                  sfirst = false;
+                }
+              }
+            }
+            for (; j < m; ++j) {
               ssum = sfirst ? sh.cg[j] : ssum + sh.cg[j];
               sfirst = false;
             }
+          }
           __syncthreads();
         }
         if (tid == 0) sh.cf[4] = ssum;
