@@ -191,7 +191,7 @@ struct FdShared {
   uint32_t mtn[kMtN];   // the parallel twist's new words
   alignas(16) float cg[kFdChunk];
   float cn[kFdChunk];
-  int ci[8];
+  int ci[10];
   float cf[8];
   double cr[2];   // random() of "best" and "new"
   int flag;
@@ -908,6 +908,15 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           __syncthreads();
         }
       }
+      // every thread needs the two best (the pu sums' chains run in three waves); the
+      // sequential form above leaves them in thread 0
+      if (tid == 0) {
+        sh.ci[8] = i1;
+        sh.ci[9] = i2;
+      }
+      __syncthreads();
+      i1 = sh.ci[8];
+      i2 = sh.ci[9];
       stamp(2);   // two_best_children
       // pu sums (sequential float32 in list order -- Python's `score += ...`): chunks of
       // the terms staged in LDS by all threads; the three sums are three dependent chains,
