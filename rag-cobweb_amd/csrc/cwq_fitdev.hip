@@ -190,7 +190,7 @@ struct FdShared {
   uint32_t mt[kMtN];
   uint32_t mtn[kMtN];   // the parallel twist's new words
   alignas(16) float cg[kFdChunk];
-  float cn[kFdChunk];
+  alignas(16) float cn[kFdChunk];
   int ci[10];
   float cf[8];
   double cr[2];   // random() of "best" and "new"
@@ -695,6 +695,39 @@ __device__ __forceinline__ bool fd_fork(const FitDev& f, FdShared& sh, int64_t r
   return ok;
 }
 
+// acc += v[a], v[a+1], ..., v[e-1] in order (sequential float32, Python's `score += ...`);
+// the first term is taken as is while `fst` (the reference's first `+=` onto 0 keeps its
+// sign of zero only this way).  One lane: 16 values read ahead of their adds (four
+// ds_read_b128 in flight while the previous adds run), so the chain runs at the VALU's
+// dependent-add rate instead of one LDS round trip per value.
+__device__ __forceinline__ void fd_add_run(float& acc, bool& fst, const float* v, int a, int e) {
+  if (a < e && fst) {
+    acc = v[a++];
+    fst = false;
+  }
+  while (a < e && (a & 3)) acc = acc + v[a++];
+  for (; a + 16 <= e; a += 16) {
+    float4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const float4*>(v + a + 4 * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc = acc + w[u].x;
+      acc = acc + w[u].y;
+      acc = acc + w[u].z;
+      acc = acc + w[u].w;
+    }
+  }
+  for (; a + 4 <= e; a += 4) {
+    const float4 w = *reinterpret_cast<const float4*>(v + a);
+    acc = acc + w.x;
+    acc = acc + w.y;
+    acc = acc + w.z;
+    acc = acc + w.w;
+  }
+  while (a < e) acc = acc + v[a++];
+}
+
 // top-2 lists of (gain, count, random, index), best first; index -1 = empty
 struct FdTop2 {
   float g1, n1, g2, n2;
@@ -918,61 +951,59 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       i1 = sh.ci[8];
       i2 = sh.ci[9];
       stamp(2);   // two_best_children
-      // pu sums (sequential float32 in list order -- Python's `score += ...`): chunks of
-      // the terms staged in LDS by all threads; the three sums are three dependent chains,
-      // so each runs in its own wave (lane 0; waves 0-2 sit on different SIMDs) with its
-      // values read 8 at a time (two ds_read_b128 ahead of the adds).  One thread running
-      // all three with a read per value was 1.3 ms per level at fan-out 19k -- 90% of a
-      // chip-wide insert (profiles/r04_fit_flat20k_profile_v1.log).
+      // pu sums (sequential float32 in list order -- Python's `score += ...`): the three sums
+      // are three dependent chains, so each runs in its own wave (lane 0; waves 0-2 sit on
+      // different SIMDs) as runs of plain adds over LDS chunks (fd_add_run).  One thread
+      // running all three with a read and a first-term select per value was 1.3 ms per level
+      // at fan-out 19k -- 90% of a chip-wide insert (profiles/r04_fit_flat20k_profile_v1.log).
       float q_all = 0.f, q_ins = 0.f, q_keep = 0.f;
       {
+        // chain 0: all terms; chain 1: term i1 replaced by tins[i1]; chain 2: i1, i2 skipped.
+        // Each chain is runs of plain adds between its special indices (s0 <= s1).  The
+        // chunks are double-buffered: waves 3.. stage chunk c+1 while waves 0-2 add chunk c.
         float acc = 0.f;
         bool fst = true;
         const float tins1 = (wave == 1 && lane == 0 && i1 >= 0) ? f.tins[i1] : 0.f;
-        // chain W over this chunk (W: 0 all, 1 ins, 2 keep), a loop per chain so that no
-        // branch on the chain sits inside it
-        auto chain = [&](auto wtag, int c0, int m) {
-          constexpr int W = decltype(wtag)::value;
-          auto step = [&](int j, float ta) {
-            if constexpr (W == 0) {
-              acc = fst ? ta : acc + ta;
-              fst = false;
-            } else if constexpr (W == 1) {
-              const float ti = j == i1 ? tins1 : ta;
-              acc = fst ? ti : acc + ti;
-              fst = false;
-            } else {
-              if (j != i1 && j != i2) {
-                acc = fst ? ta : acc + ta;
-                fst = false;
-              }
-            }
-          };
-          int jj = 0;
-          for (; jj + 8 <= m; jj += 8) {
-            float4 v4[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) v4[u] = *reinterpret_cast<const float4*>(&sh.cg[jj + 4 * u]);
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              step(c0 + jj + 4 * u, v4[u].x);
-              step(c0 + jj + 4 * u + 1, v4[u].y);
-              step(c0 + jj + 4 * u + 2, v4[u].z);
-              step(c0 + jj + 4 * u + 3, v4[u].w);
-            }
-          }
-          for (; jj < m; ++jj) step(c0 + jj, sh.cg[jj]);
-        };
+        int s0 = 0x7fffffff, s1 = 0x7fffffff;
+        if (wave == 1 && i1 >= 0) s0 = i1;
+        if (wave == 2) {
+          const int a0 = i1 >= 0 ? i1 : 0x7fffffff, a1 = i2 >= 0 ? i2 : 0x7fffffff;
+          s0 = a0 < a1 ? a0 : a1;
+          s1 = a0 < a1 ? a1 : a0;
+        }
+        {
+          const int m = b < kFdChunk ? b : kFdChunk;
+          for (int j = tid; j < m; j += kFdThreads) sh.cg[j] = f.tall[j];
+        }
+        __syncthreads();
+        int cur = 0;
         for (int c0 = 0; c0 < b; c0 += kFdChunk) {
           const int m = b - c0 < kFdChunk ? b - c0 : kFdChunk;
-          for (int j = tid; j < m; j += kFdThreads) sh.cg[j] = f.tall[c0 + j];
-          __syncthreads();
-          if (lane == 0) {
-            if (wave == 0) chain(std::integral_constant<int, 0>{}, c0, m);
-            else if (wave == 1) chain(std::integral_constant<int, 1>{}, c0, m);
-            else if (wave == 2) chain(std::integral_constant<int, 2>{}, c0, m);
+          float* cb = cur ? sh.cn : sh.cg;
+          float* nb = cur ? sh.cg : sh.cn;
+          if (wave >= 3) {
+            const int n0 = c0 + kFdChunk;
+            const int nm = b - n0 < kFdChunk ? b - n0 : kFdChunk;
+            for (int j = tid - 192; j < nm; j += kFdThreads - 192) nb[j] = f.tall[n0 + j];
+          } else if (lane == 0) {
+            int lo = c0;
+            const int hi = c0 + m;
+            while (lo < hi) {
+              const int sp = s0 >= lo ? s0 : (s1 >= lo ? s1 : 0x7fffffff);
+              const int end = sp < hi ? sp : hi;
+              fd_add_run(acc, fst, cb, lo - c0, end - c0);
+              lo = end;
+              if (lo < hi) {   // lo == sp: chain 1 takes tins[i1] there, chain 2 skips it
+                if (wave == 1) {
+                  acc = fst ? tins1 : acc + tins1;
+                  fst = false;
+                }
+                ++lo;
+              }
+            }
           }
           __syncthreads();
+          cur ^= 1;
         }
         if (lane == 0 && (wave == 1 || wave == 2)) sh.cf[4 + wave] = acc;   // cf[5] ins, cf[6] keep
         if (wave == 0) q_all = acc;
@@ -1081,27 +1112,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
             sh.cg[j] = (f.count[f.jobs[jj]] / cP) * ks;
           }
           __syncthreads();
-          if (tid == 0) {
-            int j = 0;
-            for (; j + 16 <= m; j += 16) {   // 16 values read ahead of their adds
-              float4 v4[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) v4[u] = *reinterpret_cast<const float4*>(&sh.cg[j + 4 * u]);
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const float t4[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  ssum = sfirst ? t4[e] : ssum + t4[e];
-                  sfirst = false;
-                }
-              }
-            }
-            for (; j < m; ++j) {
-              ssum = sfirst ? sh.cg[j] : ssum + sh.cg[j];
-              sfirst = false;
-            }
-          }
+          if (tid == 0) fd_add_run(ssum, sfirst, sh.cg, 0, m);
           __syncthreads();
         }
         if (tid == 0) sh.cf[4] = ssum;

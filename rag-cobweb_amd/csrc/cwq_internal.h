@@ -168,6 +168,7 @@ hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s);
 hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
                          const float* lkey, int R, float* T2, hipStream_t s);
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
+hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hipStream_t s);
 hipError_t launch_clear_tail(int64_t* nodes, const int* n_found, int64_t nq, int k, hipStream_t s);
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
                         float* okey, float* oaux, int* orow, hipStream_t s, bool cat);

@@ -1090,6 +1090,7 @@ __device__ HeapEnt heap_pop(HeapEnt* h, int64_t& n) {
 __global__ void simulate_kernel(const SimArgs a) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nq) return;
+  if (a.pre_status && a.status[q] == 0) return;   // resolved already (count pass) or skipped
   HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
   int64_t hn = 0;
   const bool dense = a.R == 0;
@@ -1448,6 +1449,21 @@ __global__ void clear_tail_kernel(int64_t* nodes, const int* n_found, int64_t nq
 hipError_t launch_clear_tail(int64_t* nodes, const int* n_found, int64_t nq, int k, hipStream_t s) {
   if (nq <= 0 || k <= 0) return hipSuccess;
   hipLaunchKernelGGL(clear_tail_kernel, dim3((unsigned)((nq * k + 255) / 256)), dim3(256), 0, s, nodes, n_found, nq, k);
+  return hipGetLastError();
+}
+
+// status[q] for the replay's pre_status gate: 0 (skip) where the filter could not certify
+// the query's list; init: also 1 (replay) everywhere else.
+__global__ void skip_failed_kernel(int* status, const int* okf, int nq, int init) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  if (init) status[q] = okf[q] ? 1 : 0;
+  else if (!okf[q]) status[q] = 0;
+}
+
+hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(skip_failed_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, status, okf, nq, init);
   return hipGetLastError();
 }
 
