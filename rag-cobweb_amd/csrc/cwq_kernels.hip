@@ -347,10 +347,17 @@ static int hot_cfg() {
   return v < 0 ? 0 : v;
 }
 
+// List width 64 (categorize, k > 16): one configuration, with the shared-query form for
+// small calls too (one query per call used one wave of four per workgroup: C2's Basic
+// one-query list scan ran 1.2 ms at ~1 wave per CU)
+static bool shq64() { return hot_cfg() == 3; }
 int scan_tq(int kl) { return kl == 16 ? kHotCfgs[hot_cfg()].tq : 16; }
-int scan_queries_per_block(int kl) { return kl == 16 && kHotCfgs[hot_cfg()].shq ? scan_tq(kl) : 4 * scan_tq(kl); }
+int scan_queries_per_block(int kl) {
+  const bool shq = kl == 16 ? kHotCfgs[hot_cfg()].shq != 0 : shq64();
+  return shq ? scan_tq(kl) : 4 * scan_tq(kl);
+}
 int scan_rows_per_tile(int kl) {
-  if (kl != 16) return kWave;
+  if (kl != 16) return kWave * (shq64() ? kWavesPerWG : 1);
   const ScanCfg& c = kHotCfgs[hot_cfg()];
   return kWave * c.lpl * (c.shq ? kWavesPerWG : 1);
 }
@@ -359,7 +366,9 @@ int scan_xcd_map() {
   const char* e = getenv("CWQ_XCD_MAP");
   return e ? atoi(e) != 0 : 1;
 }
-int scan_lists_per_slab(int kl) { return kl == 16 && kHotCfgs[hot_cfg()].shq ? kWavesPerWG : 1; }
+int scan_lists_per_slab(int kl) {
+  return (kl == 16 ? kHotCfgs[hot_cfg()].shq != 0 : shq64()) ? kWavesPerWG : 1;
+}
 
 #define CWQ_LAUNCH(TQ_, KL_, LPL_, DCH_, SHQ_) \
   hipLaunchKernelGGL((scan_kernel<ISO, EPI, TQ_, KL_, CAT, LPL_, DCH_, SHQ_>), grid, block, 0, s, X, A, B, a.out, \
@@ -378,6 +387,8 @@ static hipError_t launch_scan_t(int kl, const float* X, const float* A, const fl
       case 2: CWQ_LAUNCH(16, 16, 4, 16, false); break;
       default: CWQ_LAUNCH(16, 16, 2, 16, true); break;
     }
+  } else if (shq64()) {
+    CWQ_LAUNCH(16, 64, 1, 16, true);
   } else {
     CWQ_LAUNCH(16, 64, 1, 16, false);
   }
@@ -388,11 +399,13 @@ static hipError_t launch_scan_t(int kl, const float* X, const float* A, const fl
 // Resident workgroups per CU of the fast leaf scan (ISO, TOPK, list width 16).
 int scan_wgs_per_cu(int kl) {
   static int cache[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int cfg = kl == 16 ? hot_cfg() : 7;
+  const int cfg = kl == 16 ? hot_cfg() : (shq64() ? 6 : 7);
   if (cache[cfg]) return cache[cfg];
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
-  if (kl != 16)
+  if (kl != 16 && cfg == 6)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<true, EPI_TOPK, 16, 64, false, 1, 16, true>, 256, 0);
+  else if (kl != 16)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<true, EPI_TOPK, 16, 64, false, 1, 16, false>, 256, 0);
   else if (cfg == 0)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<true, EPI_TOPK, 16, 16, false, 2, 16, false>, 256, 0);
