@@ -986,6 +986,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
             const int nm = b - n0 < kFdChunk ? b - n0 : kFdChunk;
             for (int j = tid - 192; j < nm; j += kFdThreads - 192) nb[j] = f.tall[n0 + j];
           } else if (lane == 0) {
+            __builtin_amdgcn_s_setprio(3);   // the chains are the critical path; staging waits
             int lo = c0;
             const int hi = c0 + m;
             while (lo < hi) {
@@ -1001,6 +1002,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
                 ++lo;
               }
             }
+            __builtin_amdgcn_s_setprio(0);
           }
           __syncthreads();
           cur ^= 1;

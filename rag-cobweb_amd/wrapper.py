@@ -104,7 +104,9 @@ class CobwebWrapper:
         # fitter (per level one KL launch) -- both build the same tree
         use_dev = os.environ.get("CWQ_FIT_DEVICE", "1") != "0" and self.tree.dim <= _MAX_DEVICE_DIM
         if use_dev:
-            leaves = DeviceTreeFitter(self.tree, device=self.device).fit_batch(X[:n])
+            fitter = DeviceTreeFitter(self.tree, device=self.device)
+            leaves = fitter.fit_batch(X[:n])
+            self.last_fit_stats = dict(fitter.stats)   # rows, kernel seconds, draws, ... (diagnostics)
         else:
             fitter = TreeFitter(self.tree, device=self.device)
             leaves = [fitter.ifit(X[i]) for i in range(n)]

@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="rows per add_sentences call (0: one call)")
     ap.add_argument("--compare-every", type=int, default=0,
                     help="every this many rows, also time --compare-rows rows with one workgroup")
-    ap.add_argument("--compare-rows", type=int, default=100)
+    ap.add_argument("--compare-rows", type=int, default=200)
     ap.add_argument("--host", action="store_true", help="the host-driven fitter (CWQ_FIT_DEVICE=0)")
     args = ap.parse_args()
     if args.host:
@@ -105,9 +105,14 @@ def main():
             same = random.getstate() == st1 and all(
                 (np.array_equal(a, b) if isinstance(a, np.ndarray) else a == b)
                 for a, b in zip(arrays(w.tree.root), arrays(w1.tree.root)))
+            # the insert kernel's own time (cwq_fit_insert; the call also loads the tree into
+            # the device pool and exports it back -- a fixed cost per add_sentences call)
+            k1 = getattr(w1, "last_fit_stats", {}).get("kernel_s", float("nan"))
+            k2 = getattr(w, "last_fit_stats", {}).get("kernel_s", float("nan"))
             print(f"  at {done} rows (root fan-out {fan}): {len(rows)} inserts -- one workgroup "
                   f"{1e3 * t1 / len(rows):.3f} ms/insert, chip-wide {1e3 * t2 / len(rows):.3f} ms/insert "
-                  f"= {t1 / t2:.1f}x; trees and random() state identical: {same}", flush=True)
+                  f"= {t1 / t2:.1f}x per call; insert kernel {1e3 * k1 / len(rows):.3f} vs {1e3 * k2 / len(rows):.3f} "
+                  f"ms/insert = {k1 / k2:.1f}x; trees and random() state identical: {same}", flush=True)
             done += len(rows)
             t_all += t2
             next_cmp += args.compare_every
