@@ -13,6 +13,7 @@ step() {   # name, limit, command...
   tail -6 gpurun_out/$name.log
   if [ $rc -ne 0 ]; then echo "stopping at $name (rc=$rc)"; exit $rc; fi
 }
+CWQ_FIT_PROFILE=1 step r4e_fitflat 300 python -u scripts/fit_probe.py --n 20000 --dim 768 --clusters 0 --chunk 2000 --compare-every 5000
 step r4e_pytest_gpu 900 python -u -m pytest -p no:cacheprovider -v --timeout 400 --timeout-method thread -m gpu tests/
 step r4e_smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()"
 step r4e_cat_b4 240 python -u scripts/basic_probe.py --balanced 4,9 --queries 500 --reps 2 --max-nodes 1000000000 --rank-queries 8
