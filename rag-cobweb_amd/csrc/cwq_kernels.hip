@@ -1368,11 +1368,18 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // node with lp == G ends it) and no second root of the group is popped; nodes below the
 // group (b < G) end it too.  Otherwise status = 1 and the host re-runs the query DENSE.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void simulate_two_kernel(const SimArgs a) {
+// The heap lives in LDS (kTwoHeapLds entries, one wave per workgroup): a two-level replay
+// pushes ~1.5k entries on C2's tree, and its pops / pushes are dependent round trips --
+// ~100 cycles in LDS instead of ~1-2 us in global memory.  A heap that outgrows it
+// ends the replay uncertified (the query goes DENSE).
+constexpr int kTwoHeapLds = 4096;
+__global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
+  extern __shared__ HeapEnt s_heap[];
   const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = blockIdx.x;
   if (q >= a.nq) return;
-  HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
+  HeapEnt* h = s_heap;
+  const int64_t hcap = kTwoHeapLds;
   int64_t hn = 0;
   const float* BF = a.BF + (size_t)q * a.ldI;
   const float* T2 = a.T2 + (size_t)q * a.ldI;
@@ -1430,6 +1437,11 @@ __global__ __launch_bounds__(256) void simulate_two_kernel(const SimArgs a) {
     if (is_int) {
       const int u = e.node;
       calls += a.int_nchild[u];
+      // room for every push of this pop (internal children + at most 2R list rows)
+      if (hn + (a.int_child_end[u] - a.int_child_begin[u]) + 2 * R > hcap) {
+        status = 1;
+        break;
+      }
       for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
         wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c}, lane);
       for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint)
@@ -1482,7 +1494,7 @@ hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hip
 
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
   if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(simulate_two_kernel, dim3((a.nq + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(simulate_two_kernel, dim3((unsigned)a.nq), dim3(64), kTwoHeapLds * sizeof(HeapEnt), s, a);
   return hipGetLastError();
 }
 
