@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "../../include/cobweb_query.h"
+#include "cwq_refmath.h"
 
 namespace cwq {
 
@@ -48,8 +49,9 @@ __global__ void fit_kl_kernel(Stats st, int D, const float* __restrict__ x, floa
   const float cP = st.count[p_slot];
   const float c1 = n1 >= 0 ? st.count[n1] : 0.f;
   const float c2 = n2 >= 0 ? st.count[n2] : 0.f;
-  double sa = 0.0, sb = 0.0;
-  for (int d = lane; d < D; d += 64) {
+  float sa, sb;
+  torch_sum2(D, lane, [&](int d, float& a, float& b) {
+#pragma clang fp contract(off)
     const float xd = x[d];
     // reference P or P+x
     float mu2, v2;
@@ -83,19 +85,13 @@ __global__ void fit_kl_kernel(Stats st, int D, const float* __restrict__ x, floa
       mu1 = m;
       v1 = m2 / cnt + pv;
     }
-    const float a = logf(v2) - logf(v1);
+    a = ref_logf(v2) - ref_logf(v1);
     const float df = mu1 - mu2;
-    const float b = (v1 + df * df) / v2;
-    sa += (double)a;
-    sb += (double)b;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    sa += __shfl_xor(sa, off, 64);
-    sb += __shfl_xor(sb, off, 64);
-  }
+    b = (v1 + df * df) / v2;
+  }, sa, sb);
   if (lane == 0) {
-    float score = (float)sa;
-    score = score + (float)sb;
+    float score = sa;
+    score = score + sb;
     score = score - (float)D;
     score = score / 2.0f;
     out[job] = score;

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "../../include/cobweb_query.h"
+#include "cwq_refmath.h"
 
 namespace cwq {
 
@@ -411,19 +412,7 @@ __device__ __forceinline__ void fd_remove(const FitDev& f, FdShared& sh, int p, 
 
 // KL(cand || ref) of one wave: per-lane fp64 sums over d = lane, lane + 64, ..., then the
 // butterfly, then (sa + sb - D) / 2 in fp32 -- cwq_fit_kl's arithmetic
-__device__ __forceinline__ float fd_kl_finish(double sa, double sb, int D) {
-#pragma clang fp contract(off)
-  for (int off = 32; off > 0; off >>= 1) {
-    sa += __shfl_xor(sa, off, 64);
-    sb += __shfl_xor(sb, off, 64);
-  }
-  float score = (float)sa;
-  score = score + (float)sb;
-  score = score - (float)D;
-  score = score / 2.0f;
-  return score;
-}
-
+// mean_var_insert (CobwebTorchNode.py:214-222) of one element, float32 op order
 __device__ __forceinline__ void fd_insert_mv(float c, float m, float m2, float x, float pv, float& mo, float& vo) {
 #pragma clang fp contract(off)
   const float cnt = c + 1.0f;
@@ -434,71 +423,68 @@ __device__ __forceinline__ void fd_insert_mv(float c, float m, float m2, float x
   vo = mm2 / cnt + pv;
 }
 
-// U = KL(c + x || P + x), T = KL(c || P + x) of child slot c: ONE wave (all lanes return
-// them); reference P + x = (sh.mu2, sh.v2, sh.lv2), x = sh.x
+// KL(cand || ref) of one wave from its two sums: (Sa + Sb - D) / 2 in float32 --
+// compute_score's op order (CobwebTorchTree.py:344-356)
+__device__ __forceinline__ float fd_kl_score(float sa, float sb, int D) {
+#pragma clang fp contract(off)
+  float score = sa;
+  score = score + sb;
+  score = score - (float)D;
+  score = score / 2.0f;
+  return score;
+}
+// The per-child KL terms of one wave, summed in torch's order (torch_sum2): U = KL(c + x ||
+// P + x) and T = KL(c || P + x) for child c (two sums each)
 __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, int c, int lane, float& U, float& T) {
 #pragma clang fp contract(off)
   const int D = f.D;
   const float pv = f.pv;
-  double sU = 0.0, tU = 0.0, sT = 0.0, tT = 0.0;
   const float cc = f.count[c];
-  for (int d = lane; d < D; d += 64) {
-    const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
-    const float mu2 = sh.mu2[d], v2 = sh.v2[d], lv2 = sh.lv2[d];
+  float sa, sb;
+  torch_sum2(D, lane, [&](int d, float& a, float& b) {
     float mu1, v1;
-    fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
-    {
-      const float a = lv2 - logf(v1);
-      const float df = mu1 - mu2;
-      const float bb = (v1 + df * df) / v2;
-      sU += (double)a;
-      tU += (double)bb;
-    }
-    mu1 = m;
-    v1 = m2 / cc + pv;
-    {
-      const float a = lv2 - logf(v1);
-      const float df = mu1 - mu2;
-      const float bb = (v1 + df * df) / v2;
-      sT += (double)a;
-      tT += (double)bb;
-    }
-  }
-  U = fd_kl_finish(sU, tU, D);
-  T = fd_kl_finish(sT, tT, D);
+    fd_insert_mv(cc, f.mean[(size_t)c * D + d], f.meanSq[(size_t)c * D + d], sh.x[d], pv, mu1, v1);
+    a = sh.lv2[d] - ref_logf(v1);
+    const float df = mu1 - sh.mu2[d];
+    b = (v1 + df * df) / sh.v2[d];
+  }, sa, sb);
+  U = fd_kl_score(sa, sb, D);
+  torch_sum2(D, lane, [&](int d, float& a, float& b) {
+    const float mu1 = f.mean[(size_t)c * D + d];
+    const float v1 = f.meanSq[(size_t)c * D + d] / cc + pv;
+    a = sh.lv2[d] - ref_logf(v1);
+    const float df = mu1 - sh.mu2[d];
+    b = (v1 + df * df) / sh.v2[d];
+  }, sa, sb);
+  T = fd_kl_score(sa, sb, D);
 }
-
-// KL(c || ref) of node slot c, ref = (mu, v, lv) in LDS: ONE wave
+// KL(c || ref) with the reference vectors (mu, v, log v) given
 __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, const float* v, const float* lv, int c,
                                            int lane) {
 #pragma clang fp contract(off)
   const int D = f.D;
   const float cc = f.count[c];
-  double sa = 0.0, sb = 0.0;
-  for (int d = lane; d < D; d += 64) {
+  float sa, sb;
+  torch_sum2(D, lane, [&](int d, float& a, float& b) {
     const float mu1 = f.mean[(size_t)c * D + d], v1 = f.meanSq[(size_t)c * D + d] / cc + f.pv;
-    const float a = lv[d] - logf(v1);
+    a = lv[d] - ref_logf(v1);
     const float df = mu1 - mu[d];
-    const float bb = (v1 + df * df) / v[d];
-    sa += (double)a;
-    sb += (double)bb;
-  }
-  return fd_kl_finish(sa, sb, D);
+    b = (v1 + df * df) / v[d];
+  }, sa, sb);
+  return fd_kl_score(sa, sb, D);
 }
-
-// KL(new || P + x) of the would-be new leaf N(x, pv): ONE wave
+// KL(new leaf || P + x)
 __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, int lane) {
 #pragma clang fp contract(off)
-  double sU = 0.0, tU = 0.0;
-  for (int d = lane; d < f.D; d += 64) {
-    const float mu1 = sh.x[d], v1 = 0.f + f.pv;
-    const float a = sh.lv2[d] - logf(v1);
-    const float df = mu1 - sh.mu2[d];
-    const float bb = (v1 + df * df) / sh.v2[d];
-    sU += (double)a;
-    tU += (double)bb;
-  }
-  return fd_kl_finish(sU, tU, f.D);
+  float sa, sb;
+  const float v1 = 0.f + f.pv;
+  const float lv1 = ref_logf(v1);
+  torch_sum2(f.D, lane, [&](int d, float& a, float& b) {
+    a = sh.lv2[d] - lv1;
+    const float df = sh.x[d] - sh.mu2[d];
+    b = (v1 + df * df) / sh.v2[d];
+  }, sa, sb);
+  return fd_kl_score(sa, sb, f.D);
 }
 
 // one child of a job (ONE wave): its KL terms to kres by write-through stores
@@ -860,7 +846,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         fd_insert_mv(cP, f.mean[(size_t)cur * D + d], f.meanSq[(size_t)cur * D + d], sh.x[d], pv, m, v);
         sh.mu2[d] = m;
         sh.v2[d] = v;
-        sh.lv2[d] = logf(v);
+        sh.lv2[d] = ref_logf(v);
       }
       __syncthreads();
       const int64_t cbase = f.coff[cur];
@@ -1046,7 +1032,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float m = f.mean[(size_t)cur * D + d], v = f.meanSq[(size_t)cur * D + d] / cP + pv;
           sh.muP[d] = m;
           sh.vP[d] = v;
-          sh.lvP[d] = logf(v);
+          sh.lvP[d] = ref_logf(v);
         }
         // the split's nodes: cur's children except b1, then b1's children (list order)
         const int nb1 = f.ccnt[b1];
@@ -1061,8 +1047,9 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       __syncthreads();
       if (do_merge && wave == kFdWaves - 1) {   // mean_var_merge(b1, b2) with x vs P + x
         const float c1 = f.count[b1], c2 = f.count[b2];
-        double sa = 0.0, sb = 0.0;
-        for (int d = lane; d < D; d += 64) {
+        float sa, sb;
+        torch_sum2(D, lane, [&](int d, float& a, float& bb) {
+#pragma clang fp contract(off)
           const float ma = f.mean[(size_t)b1 * D + d], mb = f.mean[(size_t)b2 * D + d];
           const float sa2 = f.meanSq[(size_t)b1 * D + d], sb2 = f.meanSq[(size_t)b2 * D + d];
           const float delta = mb - ma;
@@ -1075,13 +1062,11 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           m = m + dl / cnt;
           m2 = m2 + dl * (xd - m);
           const float v1 = m2 / cnt + pv;
-          const float a = sh.lv2[d] - logf(v1);
+          a = sh.lv2[d] - ref_logf(v1);
           const float df = m - sh.mu2[d];
-          const float bb = (v1 + df * df) / sh.v2[d];
-          sa += (double)a;
-          sb += (double)bb;
-        }
-        const float K = fd_kl_finish(sa, sb, D);
+          bb = (v1 + df * df) / sh.v2[d];
+        }, sa, sb);
+        const float K = fd_kl_score(sa, sb, D);
         if (lane == 0) sh.cf[3] = K;
       }
       const bool split_forked = do_split && f.job != nullptr && n_split >= f.fork_min;
