@@ -145,7 +145,9 @@ struct FitDev {
   int prof;                     // CWQ_FIT_PROFILE: forked levels' phase ticks into dbg[8..13], count dbg[14]
 };
 
-constexpr int kFdThreads = 1024;
+// 512 threads (8 waves): up to 256 VGPRs per lane -- the torch-order KL sums
+// (cwq_refmath.h) spilled at 1024 threads' 128 (the kernel takes ~170, so one workgroup per CU)
+constexpr int kFdThreads = 512;
 constexpr int kFdWaves = kFdThreads / 64;
 constexpr int kFdMaxD = 1024;   // 7 D-vectors + the MT state stay within 64 KiB of LDS
 constexpr int kFdChunk = 1024;
@@ -202,6 +204,8 @@ struct FdShared {
   double tr[kFdWaves][2];
   int ti[kFdWaves][2];
 };
+static_assert(sizeof(FdShared) <= 160 * 1024, "the fit workgroup's LDS");
+
 
 __device__ __forceinline__ int ld_agent(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -441,22 +445,21 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
   const float pv = f.pv;
   const float cc = f.count[c];
   float sa, sb;
-  torch_sum2(D, lane, [&](int d, float& a, float& b) {
+  // U on lanes 0-31, T on lanes 32-63 (the same instructions: only (mu1, v1) differ)
+  torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
+    const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
     float mu1, v1;
-    fd_insert_mv(cc, f.mean[(size_t)c * D + d], f.meanSq[(size_t)c * D + d], sh.x[d], pv, mu1, v1);
+    fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
+    const float vT = m2 / cc + pv;
+    mu1 = h ? m : mu1;
+    v1 = h ? vT : v1;
     a = sh.lv2[d] - ref_logf(v1);
     const float df = mu1 - sh.mu2[d];
     b = (v1 + df * df) / sh.v2[d];
   }, sa, sb);
-  U = fd_kl_score(sa, sb, D);
-  torch_sum2(D, lane, [&](int d, float& a, float& b) {
-    const float mu1 = f.mean[(size_t)c * D + d];
-    const float v1 = f.meanSq[(size_t)c * D + d] / cc + pv;
-    a = sh.lv2[d] - ref_logf(v1);
-    const float df = mu1 - sh.mu2[d];
-    b = (v1 + df * df) / sh.v2[d];
-  }, sa, sb);
-  T = fd_kl_score(sa, sb, D);
+  const float k = fd_kl_score(sa, sb, D);
+  U = __shfl(k, 0, 64);
+  T = __shfl(k, 32, 64);
 }
 // KL(c || ref) with the reference vectors (mu, v, log v) given
 __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, const float* v, const float* lv, int c,
