@@ -142,7 +142,7 @@ struct FitDev {
   int fork_min;                 // fork a level's KL pass when it has >= fork_min children
   uint64_t spin_ticks;          // bound of every spin (100 MHz steady counter ticks)
   int* dbg;                     // [16] progress words (read back by the host on FD_HANG)
-  int prof;                     // CWQ_FIT_PROFILE: forked levels' phase ticks into dbg[8..13], count dbg[14]
+  int prof;                     // CWQ_FIT_PROFILE: forked levels' phase ticks into dbg[8..13], count dbg[14] ("all": every level)
 };
 
 // 512 threads (8 waves): up to 256 VGPRs per lane -- the torch-order KL sums
@@ -475,6 +475,24 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, con
     b = (v1 + df * df) / v[d];
   }, sa, sb);
   return fd_kl_score(sa, sb, D);
+}
+// KL(c0 || ref) and KL(c1 || ref) in one wave (c0 on lanes 0-31, c1 on lanes 32-63)
+__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const float* mu, const float* v, const float* lv, int c0,
+                                           int c1, int lane, float& K0, float& K1) {
+#pragma clang fp contract(off)
+  const int D = f.D;
+  const float cc0 = f.count[c0], cc1 = f.count[c1];
+  float sa, sb;
+  torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
+    const size_t o = (size_t)(h ? c1 : c0) * D + d;
+    const float mu1 = f.mean[o], v1 = f.meanSq[o] / (h ? cc1 : cc0) + f.pv;
+    a = lv[d] - ref_logf(v1);
+    const float df = mu1 - mu[d];
+    b = (v1 + df * df) / v[d];
+  }, sa, sb);
+  const float k = fd_kl_score(sa, sb, D);
+  K0 = __shfl(k, 0, 64);
+  K1 = __shfl(k, 32, 64);
 }
 // KL(new leaf || P + x)
 __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, int lane) {
@@ -834,7 +852,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         break;
       }
       // ---- internal node: the CU terms of every operation ----
-      const bool prof = f.prof && f.dbg && f.job != nullptr && b >= f.fork_min;
+      const bool prof = f.prof && f.dbg && f.job != nullptr && (b >= f.fork_min || f.prof == 2);
       uint64_t tprev = prof ? (uint64_t)wall_clock64() : 0;
       auto stamp = [&](int k) {   // thread 0: ticks since the previous stamp into dbg[8 + k]
         if (prof && tid == 0) {
@@ -1080,9 +1098,14 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
             break;
           }
         } else {
-          for (int j = wave; j < n_split; j += kFdWaves) {
-            const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
-            if (lane == 0) f.kres[2 * b + 1 + j] = K;
+          for (int j = 2 * wave; j < n_split; j += 2 * kFdWaves) {   // two nodes per wave
+            const int j1 = j + 1 < n_split ? j + 1 : j;
+            float K0, K1;
+            fd_kl_ref2(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
+            if (lane == 0) {
+              f.kres[2 * b + 1 + j] = K0;
+              f.kres[2 * b + 1 + j1] = K1;
+            }
           }
         }
       }
@@ -1347,7 +1370,7 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   if (const char* e = getenv("CWQ_FIT_FORK_MIN")) f.fork_min = atoi(e) < 2 ? 2 : atoi(e);
   f.spin_ticks = kFdSpinTicks;
   if (const char* e = getenv("CWQ_FIT_SPIN_MS")) f.spin_ticks = (uint64_t)(atoll(e) > 0 ? atoll(e) : 1) * 100000ull;
-  f.prof = getenv("CWQ_FIT_PROFILE") ? 1 : 0;
+  f.prof = getenv("CWQ_FIT_PROFILE") ? (strcmp(getenv("CWQ_FIT_PROFILE"), "all") == 0 ? 2 : 1) : 0;
   if (helpers == 0) f.job = nullptr;
   else if (hipMemsetAsync(f.job, 0, sizeof(FdJob), s) != hipSuccess || hipMemsetAsync(f.dbg, 0, 64, s) != hipSuccess)
     return fit_fail(CWQ_ERR_HIP, "job reset failed");
@@ -1382,8 +1405,8 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   if (f.prof && f.dbg && f.job) {   // diagnostics: where a forked level's time goes (100 MHz ticks)
     int dbg[16];
     if (hipMemcpy(dbg, f.dbg, 64, hipMemcpyDeviceToHost) == hipSuccess && dbg[14] > 0)
-      fprintf(stderr, "[fit profile] %d forked levels, us per level: KL pass %.1f, child terms %.1f, top-2 %.1f, "
-                      "pu sums %.1f, merge/split + choice %.1f\n", dbg[14], dbg[8] * 0.01 / dbg[14],
+      fprintf(stderr, "[fit profile] %d %s levels, us per level: KL pass %.1f, child terms %.1f, top-2 %.1f, "
+                      "pu sums %.1f, merge/split + choice %.1f\n", dbg[14], f.prof == 2 ? "internal" : "forked", dbg[8] * 0.01 / dbg[14],
               dbg[9] * 0.01 / dbg[14], dbg[10] * 0.01 / dbg[14], dbg[11] * 0.01 / dbg[14], dbg[12] * 0.01 / dbg[14]);
   }
   if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");

@@ -86,13 +86,15 @@ def _tree_arrays(root):
 
 
 @pytest.mark.parametrize("D,n,clusters,fork_min", [(48, 1500, 12, None), (384, 600, 6, None), (768, 400, 0, None),
-                                                   (64, 1200, 10, "2"), (96, 1500, 0, "64"), (768, 700, 0, "2")])
+                                                   (64, 1200, 10, "2"), (96, 1500, 0, "64"), (768, 700, 0, "2"),
+                                                   (5, 600, 4, None), (6, 500, 0, "2")])
 def test_device_fit_equals_host_fit(pkg, D, n, clusters, fork_min, monkeypatch):
     """Device-resident ifit == host-driven ifit: structure, sentence placement, statistics
     bit for bit, and the random() stream position afterwards; with a batch split in two
     add_sentences calls (state carried over).  The device loop forks levels of >= 256
     children over every CU (flat N(0,I) rows: the root); fork_min forces forks at smaller
-    levels -- every level, split passes included, at "2"."""
+    levels -- every level, split passes included, at "2".  D = 5, 6: torch's scalar sum path
+    (fewer than 8 elements) in the per-half sums as well."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if fork_min:
