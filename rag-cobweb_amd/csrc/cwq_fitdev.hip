@@ -446,13 +446,17 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
   const float cc = f.count[c];
   float sa, sb;
   // U on lanes 0-31, T on lanes 32-63 (the same instructions: only (mu1, v1) differ)
+  const float cnt = cc + 1.0f;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
+    // U: c + x (fd_insert_mv's ops); T: c as is (m2 / cc + pv) -- one variance division per
+    // lane, the operands selected per half
     const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
-    float mu1, v1;
-    fd_insert_mv(cc, m, m2, sh.x[d], pv, mu1, v1);
-    const float vT = m2 / cc + pv;
-    mu1 = h ? m : mu1;
-    v1 = h ? vT : v1;
+    const float xd = sh.x[d];
+    const float delta = xd - m;
+    const float mm = m + delta / cnt;
+    const float mu1 = h ? m : mm;
+    const float num = h ? m2 : m2 + delta * (xd - mm);
+    const float v1 = num / (h ? cc : cnt) + pv;
     a = sh.lv2[d] - ref_logf(v1);
     const float df = mu1 - sh.mu2[d];
     b = (v1 + df * df) / sh.v2[d];
@@ -1098,7 +1102,9 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
             break;
           }
         } else {
-          for (int j = 2 * wave; j < n_split; j += 2 * kFdWaves) {   // two nodes per wave
+          // two nodes per wave; the merge's wave (the last) sits this out when there is one
+          const int nsw = do_merge ? kFdWaves - 1 : kFdWaves;
+          for (int j = 2 * wave; wave < nsw && j < n_split; j += 2 * nsw) {
             const int j1 = j + 1 < n_split ? j + 1 : j;
             float K0, K1;
             fd_kl_ref2(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
