@@ -91,7 +91,7 @@ def _tree_arrays(root):
 def test_device_fit_equals_host_fit(pkg, D, n, clusters, fork_min, monkeypatch):
     """Device-resident ifit == host-driven ifit: structure, sentence placement, statistics
     bit for bit, and the random() stream position afterwards; with a batch split in two
-    add_sentences calls (state carried over).  The device loop forks levels of >= 256
+    add_sentences calls (state carried over).  The device loop forks levels of >= 64
     children over every CU (flat N(0,I) rows: the root); fork_min forces forks at smaller
     levels -- every level, split passes included, at "2".  D = 5, 6: torch's scalar sum path
     (fewer than 8 elements) in the per-half sums as well."""
