@@ -149,7 +149,7 @@ __device__ __forceinline__ void torch_sum2(int D, int lane, Term term, float& Sa
   int i = 0;
   if (size_ilp <= 32) {   // D < 1056: kSumPf rows' terms first, their loads in flight together
 #pragma unroll
-    for (int c = 0; c < 32 / kSumPf; ++c) {
+    for (int c = 0; c < (32 + kSumPf - 1) / kSumPf; ++c) {
       float ta[kSumPf], tb[kSumPf];
 #pragma unroll
       for (int r = 0; r < kSumPf; ++r) {
@@ -158,17 +158,18 @@ __device__ __forceinline__ void torch_sum2(int D, int lane, Term term, float& Sa
         if (kSumPf * c + r < size_ilp && act) term((kSumPf * c + r) * 32 + lane, ta[r], tb[r]);
       }
 #pragma unroll
-      for (int r = 0; r < kSumPf; ++r)
-        if (kSumPf * c + r < size_ilp) {
+      for (int r = 0; r < kSumPf; ++r) {
+        const int row = kSumPf * c + r;
+        if (row < size_ilp) {
           a0 = a0 + ta[r];
           b0 = b0 + tb[r];
         }
-      const int done = kSumPf * (c + 1);
-      if ((done & 15) == 0 && done <= (size_ilp & ~15)) {   // a whole step: level 1 takes level 0 (never a carry further)
-        a1 = a1 + a0;
-        a0 = 0.f;
-        b1 = b1 + b0;
-        b0 = 0.f;
+        if (((row + 1) & 15) == 0 && row + 1 <= (size_ilp & ~15)) {   // a whole step: level 1 takes level 0 (never a carry further)
+          a1 = a1 + a0;
+          a0 = 0.f;
+          b1 = b1 + b0;
+          b0 = 0.f;
+        }
       }
     }
     i = size_ilp;
@@ -263,7 +264,7 @@ __device__ __forceinline__ void torch_sum2_halves(int D, int lane, Term term, fl
   int i = 0;
   if (size_ilp <= 32) {   // D < 1056: kSumPf rows' terms first, their loads in flight together
 #pragma unroll
-    for (int c = 0; c < 32 / kSumPf; ++c) {
+    for (int c = 0; c < (32 + kSumPf - 1) / kSumPf; ++c) {
       float ta[kSumPf], tb[kSumPf];
 #pragma unroll
       for (int r = 0; r < kSumPf; ++r) {
@@ -272,17 +273,18 @@ __device__ __forceinline__ void torch_sum2_halves(int D, int lane, Term term, fl
         if (kSumPf * c + r < size_ilp) term((kSumPf * c + r) * 32 + hl, h, ta[r], tb[r]);
       }
 #pragma unroll
-      for (int r = 0; r < kSumPf; ++r)
-        if (kSumPf * c + r < size_ilp) {
+      for (int r = 0; r < kSumPf; ++r) {
+        const int row = kSumPf * c + r;
+        if (row < size_ilp) {
           a0 = a0 + ta[r];
           b0 = b0 + tb[r];
         }
-      const int done = kSumPf * (c + 1);
-      if ((done & 15) == 0 && done <= (size_ilp & ~15)) {   // a whole step: level 1 takes level 0 (never a carry further)
-        a1 = a1 + a0;
-        a0 = 0.f;
-        b1 = b1 + b0;
-        b0 = 0.f;
+        if (((row + 1) & 15) == 0 && row + 1 <= (size_ilp & ~15)) {   // a whole step: level 1 takes level 0 (never a carry further)
+          a1 = a1 + a0;
+          a0 = 0.f;
+          b1 = b1 + b0;
+          b0 = 0.f;
+        }
       }
     }
     i = size_ilp;
