@@ -154,6 +154,7 @@ constexpr int kFdChunk = 1024;
 constexpr int kFdRing = 64;     // per-job claim / completion counters, by epoch
 constexpr int kFdWaveClaim = 4; // children per claim of a master wave
 constexpr int kFdHelperPer = 2; // children per helper wave per workgroup claim
+constexpr int kFdParTop = 8;    // unforked levels of >= this many children: parallel draws + top-2
 constexpr int kFdForkMin = 64;  // default fork threshold (children of a level; 64 measured best of 32-256 on clustered 768-d data)
 enum { FD_OK = 0, FD_ROOM = 1, FD_FULL = 2, FD_HANG = 3 };
 // bounded spins (the steady counter runs at 100 MHz): a helper with no new job for
@@ -236,7 +237,7 @@ __device__ __forceinline__ void wave_sync() {
 // calls would, writing the tempered outputs to out[0..n).  Every lane passes the same idx.
 // A twist is 227 chains over the 64 lanes (mt_chain_*), the new words into tmp (LDS) while
 // mt still holds the old ones, then copied back with word 623.
-__device__ __forceinline__ void mt_gen_wave(uint32_t* mt, uint32_t* tmp, int& idx, int64_t n, uint32_t* out, int lane) {
+__device__ __attribute__((noinline)) void mt_gen_wave(uint32_t* mt, uint32_t* tmp, int& idx, int64_t n, uint32_t* out, int lane) {
   int64_t done = 0;
   while (done < n) {
     if (idx >= kMtN) {
@@ -887,6 +888,12 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         }
         if (tid == 0) drawn += b;
       } else {
+        if (b >= kFdParTop && wave == 0) {   // the level's sort draws, as a fork makes them
+          int idx = __builtin_amdgcn_readlane(mt_idx, 0);
+          mt_gen_wave(sh.mt, sh.mtn, idx, 2 * (int64_t)b, f.rnd, lane);
+          if (lane == 0) mt_idx = idx;
+        }
+        if (b >= kFdParTop && tid == 0) drawn += b;
         for (int j = wave; j <= b; j += kFdWaves) {
           if (j < b) {
             float U, T;
@@ -920,7 +927,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       stamp(1);   // the per-child terms
       // two_best_children: one random() per child, in list order
       int i1 = -1, i2 = -1;
-      if (forked) {
+      if (forked || b >= kFdParTop) {
         fd_top2_parallel(f, sh, b);   // the draws are in f.rnd already
         i1 = sh.ci[2];
         i2 = sh.ci[3];
