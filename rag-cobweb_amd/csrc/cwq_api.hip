@@ -1152,7 +1152,6 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
   int* tctr = b.take<int>(64);
   HIPCHK(launch_query_prep2(q, c.nq, ix->D, ix->iso_c, ix->DP, ix->DPB2, nqf, Xb2, qinfo2, s));
   HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, c.nq, Sroot, 1, s));   // root, exact
-  HIPCHK(hipMemsetAsync(tctr, 0, 64 * 4, s));
   FgArgs g;
   memset(&g, 0, sizeof(g));
   g.DPB = ix->DPB2;
@@ -1211,6 +1210,7 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
     sa.ldpout = g.ldlb;
     HIPCHK(launch_stream(sa, 2, ix->cus, s));
   } else {
+    HIPCHK(hipMemsetAsync(tctr, 0, 64 * 4, s));   // the tile claim counters (the stream pass has none)
     HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
   }
   if (!ix->int_path)
@@ -1667,9 +1667,9 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
       return rc;
     }
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
-    HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s));
+    // the counters (qcnt, qover, done, ..., the fused select's) zeroed by the prep's block 0
+    HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s, qcnt, (int)(5 * nqc + 1)));
     if (i8) HIPCHK(launch_query_prep_i8(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xq, qinfo8, s));
-    HIPCHK(hipMemsetAsync(qcnt, 0, ((size_t)5 * nqc + 1) * 4, s));
   }
   if ((rc = group_tables(ix, c, q, false, s))) return rc;
   const FiltConsts fc = filt_consts(ix->DPB);

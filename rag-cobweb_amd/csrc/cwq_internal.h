@@ -589,7 +589,7 @@ hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0,
                                  double* sh, float* Plo, float* Phi, float* Pclo, float* Pchi, hipStream_t s);
 hipError_t launch_gather_bf16_rows(const void* Mb, int DPB, const int* srow, int64_t n, void* Sb, hipStream_t s);
 hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
-                             float4* qinfo, hipStream_t s);
+                             float4* qinfo, hipStream_t s, int* zero = nullptr, int nzero = 0);
 hipError_t launch_fgemm(const void* Xb, const void* Mb, const FgArgs& a, int n_wg, hipStream_t s);
 int fgemm_dpb(int D);   // padded bf16 operand width the fgemm build needs
 hipError_t launch_select(const float* u, int64_t ldu, int nq, int nrows, int Kp, float* cu, int* crow, hipStream_t s);

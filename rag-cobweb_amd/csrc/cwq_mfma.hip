@@ -218,9 +218,11 @@ hipError_t launch_query_prep_i8(const float* q, int64_t nq, int D, const float* 
 
 // Queries: bf16 hi part of the centred query, and {|x'|^2, |x_hi|, |x_lo|}.
 __global__ void query_prep_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c,
-                                  int DPB, int64_t nq_pad, __bf16* Xb, float4* qinfo) {
+                                  int DPB, int64_t nq_pad, __bf16* Xb, float4* qinfo, int* zero, int nzero) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kWavesPerWG + (threadIdx.x >> 6);
+  if (blockIdx.x == 0)   // the call's counters (a memset launch less per call)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
   if (r >= nq_pad) return;
   double s = 0.0, slo = 0.0, shi = 0.0;
   for (int d = lane; d < DPB; d += kWave) {
@@ -242,9 +244,10 @@ __global__ void query_prep_kernel(const float* __restrict__ q, int64_t nq, int D
 }
 
 hipError_t launch_query_prep(const float* q, int64_t nq, int D, const float* c, int DPB, int64_t nq_pad, void* Xb,
-                             float4* qinfo, hipStream_t s) {
+                             float4* qinfo, hipStream_t s, int* zero, int nzero) {
+  if (nzero < 0 || (nzero > 0 && !zero)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(query_prep_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, nq, D, c, DPB, nq_pad,
-                     (__bf16*)Xb, qinfo);
+                     (__bf16*)Xb, qinfo, zero, nzero);
   return hipGetLastError();
 }
 

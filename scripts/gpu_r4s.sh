@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, call S: parallel draws + top-2 on unforked levels of >= 8 children -- the whole
-# -m gpu suite, the clustered fit profile, the C2 probe.
+# -m gpu suite, the clustered fit profile, the C2 probe; the per-call counters zeroed by the
+# query prep (no memset launch) on the b4/d9 and b10/d5 one-query calls.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
@@ -16,4 +17,6 @@ step() {   # name, limit, command...
 step r4s_pytest_gpu 900 python -u -m pytest -p no:cacheprovider -v --timeout 400 --timeout-method thread -m gpu tests
 CWQ_FIT_PROFILE=all step r4s_fitclu 300 python -u scripts/fit_probe.py --n 20000 --dim 768 --clusters 100 --chunk 5000
 step r4s_c2 400 python -u scripts/c2_probe.py --calls 100
+step r4s_pc_b4 300 python -u scripts/percall_probe.py --balanced 4,9 --nq 1,8,64 --modes -1 --reps 50
+step r4s_pc_b10 300 python -u scripts/percall_probe.py --balanced 10,5 --nq 1,8,64 --modes -1 --reps 50
 echo done
