@@ -875,6 +875,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         sh.lv2[d] = ref_logf(v);
       }
       __syncthreads();
+      stamp(5);   // P + x (into dbg[13])
       const int64_t cbase = f.coff[cur];
       // per child: U = KL(c + x || P + x), T = KL(c || P + x); the new leaf's KL(new || P + x).
       // A level of >= fork_min children goes over the whole chip (fd_fork), the level's b
@@ -1123,6 +1124,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         }
       }
       __syncthreads();
+      stamp(7);   // the merge and split KL terms (into dbg[15])
       if (do_split) {
         // the split's partition-utility sum, sequential float32 in list order (Python's
         // `score += ...`): the terms formed by all threads into LDS chunks (their KL results
@@ -1418,9 +1420,10 @@ extern "C" int cwq_fit_insert(cwq_fit* h, const float* X, int64_t n, int32_t* le
   if (f.prof && f.dbg && f.job) {   // diagnostics: where a forked level's time goes (100 MHz ticks)
     int dbg[16];
     if (hipMemcpy(dbg, f.dbg, 64, hipMemcpyDeviceToHost) == hipSuccess && dbg[14] > 0)
-      fprintf(stderr, "[fit profile] %d %s levels, us per level: KL pass %.1f, child terms %.1f, top-2 %.1f, "
-                      "pu sums %.1f, merge/split + choice %.1f\n", dbg[14], f.prof == 2 ? "internal" : "forked", dbg[8] * 0.01 / dbg[14],
-              dbg[9] * 0.01 / dbg[14], dbg[10] * 0.01 / dbg[14], dbg[11] * 0.01 / dbg[14], dbg[12] * 0.01 / dbg[14]);
+      fprintf(stderr, "[fit profile] %d %s levels, us per level: P+x %.1f, KL pass %.1f, child terms %.1f, top-2 %.1f, "
+                      "pu sums %.1f, merge/split KL %.1f, split sum + choice %.1f\n", dbg[14], f.prof == 2 ? "internal" : "forked",
+              dbg[13] * 0.01 / dbg[14], dbg[8] * 0.01 / dbg[14], dbg[9] * 0.01 / dbg[14], dbg[10] * 0.01 / dbg[14],
+              dbg[11] * 0.01 / dbg[14], dbg[15] * 0.01 / dbg[14], dbg[12] * 0.01 / dbg[14]);
   }
   if (ctrl[3] == FD_FULL) return fit_fail(CWQ_ERR_OOM, "cwq_fit_insert: node pool or child arena exhausted mid-insert");
   if (ctrl[3] == FD_HANG) {
