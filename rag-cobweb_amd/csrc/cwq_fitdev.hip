@@ -5,10 +5,9 @@
 // The tree lives in device memory: a pool of node statistics (count, mean, meanSq =
 // Welford M2, CobwebTorchNode.py:31-68), parent links and per-node child lists in list
 // order (slabs of an arena; append at the end, remove with the tail shifted left, as
-// Python's list.append / list.remove).  One 512-thread master workgroup runs the inserts in
-// order; per tree level it computes every child's KL terms (all threads forming terms into
-// LDS, half-waves summing them in torch's order; levels of >= fork_min children over every
-// CU), then one thread makes the reference's scalar decisions in its float32 op order:
+// Python's list.append / list.remove).  One 1024-thread workgroup runs the inserts in
+// order; per tree level it computes every child's KL terms (one wave per child), then
+// one thread makes the reference's scalar decisions in its float32 op order:
 //   two_best_children (CobwebTorchNode.py:374-420): gain = p1*KL(c+x || P+x) -
 //     p2*KL(c || P+x), sorted by (gain, count, random()) descending;
 //   pu_for_insert / pu_for_new_child / pu_for_merge / pu_for_split (:422-650), each a
