@@ -195,10 +195,6 @@ struct FdShared {
   uint32_t mtn[kMtN];   // the parallel twist's new words
   alignas(16) float cg[kFdChunk];
   alignas(16) float cn[kFdChunk];
-  // staged KL terms (fd_kl_staged): sequence s's terms a at kt[2s*D..], b at kt[(2s+1)*D..]
-  alignas(16) float kt[2 * 8 * kFdMaxD];
-  int sn[8];      // the staged sequences' nodes
-  float sc[8];    // and counts
   int ci[10];
   float cf[8];
   double cr[2];   // random() of "best" and "new"
@@ -485,6 +481,24 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, con
   }, sa, sb);
   return fd_kl_score(sa, sb, D);
 }
+// KL(c0 || ref) and KL(c1 || ref) in one wave (c0 on lanes 0-31, c1 on lanes 32-63)
+__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const float* mu, const float* v, const float* lv, int c0,
+                                           int c1, int lane, float& K0, float& K1) {
+#pragma clang fp contract(off)
+  const int D = f.D;
+  const float cc0 = f.count[c0], cc1 = f.count[c1];
+  float sa, sb;
+  torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
+    const size_t o = (size_t)(h ? c1 : c0) * D + d;
+    const float mu1 = f.mean[o], v1 = f.meanSq[o] / (h ? cc1 : cc0) + f.pv;
+    a = lv[d] - ref_logf(v1);
+    const float df = mu1 - mu[d];
+    b = (v1 + df * df) / v[d];
+  }, sa, sb);
+  const float k = fd_kl_score(sa, sb, D);
+  K0 = __shfl(k, 0, 64);
+  K1 = __shfl(k, 32, 64);
+}
 // KL(new leaf || P + x)
 __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, int lane) {
 #pragma clang fp contract(off)
@@ -512,73 +526,6 @@ __device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh
   } else {
     const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
     st_agent_f(&f.kres[kofs + j], K);
-  }
-}
-
-// The KL scores of nseq sequences inside the master workgroup, kFdSeq at a time: meta(t,
-// node, count) names sequence t's node (threads < ns), every thread then loads its elements'
-// two stats words (load(node, d), all of a thread's loads in flight together) and forms their
-// terms (form(t, node, count, d, raw, a, b)) into sh.kt; waves 0-3 sum two staged sequences
-// each in torch's order (torch_sum2_halves) and out(t, K) stores the score.  A level's terms
-// are spread over all 512 threads this way: one wave per child (24 dependent rows per lane at
-// D = 768) was ~30 us per round of 8 children on clustered trees.
-constexpr int kFdSeq = 8;
-constexpr int kFdStE = kFdSeq * kFdMaxD / kFdThreads;   // elements per thread per batch (<= 16)
-constexpr int kFdStG = 8;                                // of which formed per group
-template <typename Meta, typename Load, typename Form, typename Out>
-__device__ __forceinline__ void fd_kl_staged(const FitDev& f, FdShared& sh, int nseq, Meta meta, Load load, Form form,
-                                             Out out) {
-#pragma clang fp contract(off)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, D = f.D;
-  for (int t0 = 0; t0 < nseq; t0 += kFdSeq) {
-    const int ns = nseq - t0 < kFdSeq ? nseq - t0 : kFdSeq;
-    if (tid < ns) {
-      int nd;
-      float cn;
-      meta(t0 + tid, nd, cn);
-      sh.sn[tid] = nd;
-      sh.sc[tid] = cn;
-    }
-    __syncthreads();
-    const int ne = ns * D;
-#pragma unroll 1
-    for (int g0 = 0; g0 < kFdStE; g0 += kFdStG) {   // kFdStG elements' loads in flight, then their terms
-      if (tid + g0 * kFdThreads >= ne) break;
-      float2 raw[kFdStG];
-#pragma unroll
-      for (int e = 0; e < kFdStG; ++e) {
-        const int i = tid + (g0 + e) * kFdThreads;
-        raw[e] = make_float2(0.f, 0.f);
-        if (i < ne) {
-          const int sq = i / D;
-          raw[e] = load(sh.sn[sq], i - sq * D);
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < kFdStG; ++e) {
-        const int i = tid + (g0 + e) * kFdThreads;
-        if (i < ne) {
-          const int sq = i / D, d = i - sq * D;
-          float a, b;
-          form(t0 + sq, sh.sn[sq], sh.sc[sq], d, raw[e], a, b);
-          sh.kt[(2 * sq) * D + d] = a;
-          sh.kt[(2 * sq + 1) * D + d] = b;
-        }
-      }
-    }
-    __syncthreads();
-    if (2 * wave < ns) {
-      float sa, sb;
-      torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
-        const int sq = 2 * wave + h < ns ? 2 * wave + h : ns - 1;   // a missing second: the first again, unused
-        a = sh.kt[(2 * sq) * D + d];
-        b = sh.kt[(2 * sq + 1) * D + d];
-      }, sa, sb);
-      const float k = fd_kl_score(sa, sb, D);
-      if (lane == 0) out(t0 + 2 * wave, k);
-      if (lane == 32 && 2 * wave + 1 < ns) out(t0 + 2 * wave + 1, k);
-    }
-    __syncthreads();
   }
 }
 
@@ -948,39 +895,19 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           if (lane == 0) mt_idx = idx;
         }
         if (b >= kFdParTop && tid == 0) drawn += b;
-        // sequence t < 2b: child t/2's U (t even) or T (t odd) -- fd_kl_UT's terms; t = 2b: the
-        // new leaf's (fd_kl_new's); scores to kres[t]
-        fd_kl_staged(f, sh, 2 * b + 1,
-            [&](int t, int& nd, float& cn) {
-              nd = t < 2 * b ? f.arena[cbase + (t >> 1)] : -1;
-              cn = nd >= 0 ? f.count[nd] : 0.f;
-            },
-            [&](int nd, int d) {
-              return nd >= 0 ? make_float2(f.mean[(size_t)nd * D + d], f.meanSq[(size_t)nd * D + d])
-                             : make_float2(0.f, 0.f);
-            },
-            [&](int t, int nd, float cc, int d, float2 r, float& a, float& bb) {
-#pragma clang fp contract(off)
-              if (nd < 0) {
-                const float v1 = 0.f + pv;
-                a = sh.lv2[d] - ref_logf(v1);
-                const float df = sh.x[d] - sh.mu2[d];
-                bb = (v1 + df * df) / sh.v2[d];
-                return;
-              }
-              const bool h = (t & 1) != 0;
-              const float m = r.x, m2 = r.y, cnt = cc + 1.0f;
-              const float xd = sh.x[d];
-              const float delta = xd - m;
-              const float mm = m + delta / cnt;
-              const float mu1 = h ? m : mm;
-              const float num = h ? m2 : m2 + delta * (xd - mm);
-              const float v1 = num / (h ? cc : cnt) + pv;
-              a = sh.lv2[d] - ref_logf(v1);
-              const float df = mu1 - sh.mu2[d];
-              bb = (v1 + df * df) / sh.v2[d];
-            },
-            [&](int t, float k) { f.kres[t] = k; });
+        for (int j = wave; j <= b; j += kFdWaves) {
+          if (j < b) {
+            float U, T;
+            fd_kl_UT(f, sh, f.arena[cbase + j], lane, U, T);
+            if (lane == 0) {
+              f.kres[2 * j] = U;
+              f.kres[2 * j + 1] = T;
+            }
+          } else {
+            const float K = fd_kl_new(f, sh, lane);
+            if (lane == 0) f.kres[2 * b] = K;
+          }
+        }
       }
       __syncthreads();
       stamp(0);   // the KL pass (fork / join)
@@ -1151,53 +1078,49 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         for (int j = tid; j < nb1; j += kFdThreads) f.jobs[b - 1 + j] = f.arena[b1base + j];
       }
       __syncthreads();
-      // mean_var_merge(b1, b2) with x vs P + x (sequence 0 when merging), and KL(c || P) of the
-      // split's nodes (unless the split is forked), staged over the whole workgroup
-      const bool split_forked = do_split && f.job != nullptr && n_split >= f.fork_min;
-      {
-        const int nm = do_merge ? 1 : 0;
-        const int nsp = do_split && !split_forked ? n_split : 0;
-        const float c1 = do_merge ? f.count[b1] : 0.f, c2 = do_merge ? f.count[b2] : 0.f;
-        fd_kl_staged(f, sh, nm + nsp,
-            [&](int t, int& nd, float& cn) {
-              nd = t < nm ? b1 : f.jobs[t - nm];
-              cn = t < nm ? c1 : f.count[nd];
-            },
-            [&](int nd, int d) { return make_float2(f.mean[(size_t)nd * D + d], f.meanSq[(size_t)nd * D + d]); },
-            [&](int t, int nd, float cc, int d, float2 r, float& a, float& bb) {
+      if (do_merge && wave == kFdWaves - 1) {   // mean_var_merge(b1, b2) with x vs P + x
+        const float c1 = f.count[b1], c2 = f.count[b2];
+        float sa, sb;
+        torch_sum2(D, lane, [&](int d, float& a, float& bb) {
 #pragma clang fp contract(off)
-              if (t < nm) {
-                const float ma = r.x, sa2 = r.y;
-                const float mb = f.mean[(size_t)b2 * D + d], sb2 = f.meanSq[(size_t)b2 * D + d];
-                const float delta = mb - ma;
-                const float tot = c1 + c2;
-                float m2 = (sa2 + sb2) + (delta * delta) * ((c1 * c2) / tot);
-                float m = (c1 * ma + c2 * mb) / tot;
-                const float cnt = tot + 1.0f;
-                const float xd = sh.x[d];
-                const float dl = xd - m;
-                m = m + dl / cnt;
-                m2 = m2 + dl * (xd - m);
-                const float v1 = m2 / cnt + pv;
-                a = sh.lv2[d] - ref_logf(v1);
-                const float df = m - sh.mu2[d];
-                bb = (v1 + df * df) / sh.v2[d];
-                return;
-              }
-              const float v1 = r.y / cc + pv;
-              a = sh.lvP[d] - ref_logf(v1);
-              const float df = r.x - sh.muP[d];
-              bb = (v1 + df * df) / sh.vP[d];
-            },
-            [&](int t, float k) {
-              if (t < nm) sh.cf[3] = k;
-              else f.kres[2 * b + 1 + (t - nm)] = k;
-            });
+          const float ma = f.mean[(size_t)b1 * D + d], mb = f.mean[(size_t)b2 * D + d];
+          const float sa2 = f.meanSq[(size_t)b1 * D + d], sb2 = f.meanSq[(size_t)b2 * D + d];
+          const float delta = mb - ma;
+          const float tot = c1 + c2;
+          float m2 = (sa2 + sb2) + (delta * delta) * ((c1 * c2) / tot);
+          float m = (c1 * ma + c2 * mb) / tot;
+          const float cnt = tot + 1.0f;
+          const float xd = sh.x[d];
+          const float dl = xd - m;
+          m = m + dl / cnt;
+          m2 = m2 + dl * (xd - m);
+          const float v1 = m2 / cnt + pv;
+          a = sh.lv2[d] - ref_logf(v1);
+          const float df = m - sh.mu2[d];
+          bb = (v1 + df * df) / sh.v2[d];
+        }, sa, sb);
+        const float K = fd_kl_score(sa, sb, D);
+        if (lane == 0) sh.cf[3] = K;
       }
-      if (split_forked) {   // KL(c || P) of the split's nodes over the chip
-        if (!fd_fork(f, sh, row, 1, n_split, 0, 2 * b + 1, 0, mt_idx)) {
-          if (tid == 0) f.ctrl[3] = FD_HANG;
-          break;
+      const bool split_forked = do_split && f.job != nullptr && n_split >= f.fork_min;
+      if (do_split) {   // KL(c || P) of the split's nodes
+        if (split_forked) {
+          if (!fd_fork(f, sh, row, 1, n_split, 0, 2 * b + 1, 0, mt_idx)) {
+            if (tid == 0) f.ctrl[3] = FD_HANG;
+            break;
+          }
+        } else {
+          // two nodes per wave; the merge's wave (the last) sits this out when there is one
+          const int nsw = do_merge ? kFdWaves - 1 : kFdWaves;
+          for (int j = 2 * wave; wave < nsw && j < n_split; j += 2 * nsw) {
+            const int j1 = j + 1 < n_split ? j + 1 : j;
+            float K0, K1;
+            fd_kl_ref2(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
+            if (lane == 0) {
+              f.kres[2 * b + 1 + j] = K0;
+              f.kres[2 * b + 1 + j1] = K1;
+            }
+          }
         }
       }
       __syncthreads();
