@@ -197,6 +197,17 @@ def per_call(index, Q, k, nqs=(1, 8, 64), reps=20):
     return out
 
 
+def pmc_candidates(explicit):
+    """The PMC file to read: the one given, else profiles/pmc_rNN_fgemm.json newest round first
+    (the first whose workload and kernel match the run is used)."""
+    if explicit:
+        return [explicit]
+    import glob
+    import re
+    fs = glob.glob(os.path.join(ROOT, "profiles", "pmc_r*_fgemm.json"))
+    return sorted(fs, key=lambda f: int(re.search(r"pmc_r(\d+)_", f).group(1)), reverse=True)
+
+
 class _Names:
     """Sentence strings "s<i>" of the synthetic corpus, made on demand (no 1M-10M list)."""
 
@@ -248,7 +259,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-call", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03_fgemm.json"))
+    ap.add_argument("--pmc-file", default=None,
+                    help="PMC summary (scripts/pmc_summary.py) of the filter kernel; default: the newest "
+                         "profiles/pmc_rNN_fgemm.json whose workload matches this run")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="rehearsal only: gloo lets several ranks share one GPU (RCCL refuses that)")
     args = ap.parse_args()
@@ -372,16 +385,19 @@ def main():
         launches = 1
     achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
     bytes_q = 8.0 * (N + 1) * D + 8.0 * 2 * N + 4.0 * D + 12.0 * k   # SURVEY §8(d) bytes per query
-    traffic = clk = None
-    if os.path.exists(args.pmc_file):
+    traffic = clk = pmc_used = None
+    for pf in pmc_candidates(args.pmc_file):
         try:
-            pm = json.load(open(args.pmc_file))
-            if pm.get("workload") == [N, D, nql, k] and pm.get("kernel") == kname.split(" ")[0]:
-                # per step (the launches of one call), like `achieved`
-                traffic = pm.get("hbm_bytes_per_launch")
-                clk = pm.get("effective_clock_ghz")   # GRBM_GUI_ACTIVE / kernel time, same PMC run
-        except Exception:
-            traffic = clk = None
+            pm = json.load(open(pf))
+        except (OSError, ValueError):
+            continue
+        if pm.get("workload") == [N, D, nql, k] and pm.get("kernel") == kname.split(" ")[0]:
+            # per step (the filter launches of one call), like `achieved`; files before round 5
+            # stored the per-call figure under the key hbm_bytes_per_launch
+            traffic = pm.get("hbm_bytes_per_call", pm.get("hbm_bytes_per_launch"))
+            clk = pm.get("effective_clock_ghz")   # GRBM_GUI_ACTIVE / kernel time, same PMC run
+            pmc_used = os.path.relpath(pf, ROOT)
+            break
 
     torch.cuda.empty_cache()
     used_steady = dev_used()              # + the handle's workspace after the timed calls
@@ -431,7 +447,8 @@ def main():
                        else "single GPU"},
             "roofline": {"bound": "mfma", "pipe": pipe,
                          "achieved": round(achieved_tf, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved_tf / peak, 4), "traffic": traffic,
+                         "frac": round(achieved_tf / peak, 4), "traffic": traffic, "traffic_unit": "bytes per step",
+                         "pmc_file": pmc_used,
                          "kernel": kname, "kernel_ms": round(kern_ms, 3), "launches_per_step": launches,
                          "avg_launch_ms": round(kern_ms / launches, 3),
                          "call_ms": round(call_ms, 3), "flops_per_step": flops_launch, "phases_ms": phases,

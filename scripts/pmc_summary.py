@@ -62,10 +62,12 @@ if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_AC
 if "TCC_HIT_sum" in c:
     res["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
 if "FETCH_SIZE" in c:
-    res["fetch_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024        # gfx950 16-B-lane correction
-    res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"]       # upper bound: MALL hits counted
+    # summed over the PHASES filter launches of one call (one bench step), not one launch
+    res["fetch_bytes_per_call"] = 2 * c["FETCH_SIZE"] * 1024          # gfx950 16-B-lane correction
+    res["hbm_bytes_per_call"] = res["fetch_bytes_per_call"]           # upper bound: MALL hits counted
+    res["hbm_bytes_per_launch"] = res["fetch_bytes_per_call"] / PHASES
 if "WRITE_SIZE" in c:
-    res["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+    res["write_bytes_per_call"] = c["WRITE_SIZE"] * 1024
 res["workload"] = [1000000, 768, 10000, 10]   # filter_probe defaults the passes ran
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
