@@ -256,9 +256,12 @@ int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_
  * GPU -- the tree (statistics, parent links, ordered child lists) in device memory, one
  * master workgroup inserting the rows in order, every decision on the device, the
  * reference's random() draws from Python's MT19937 stream run on the device; a level with
- * many children (>= CWQ_FIT_FORK_MIN, default 256) has its KL terms computed by helper
+ * many children (>= CWQ_FIT_FORK_MIN, default 64) has its KL terms computed by helper
  * workgroups on every CU (CWQ_FIT_HELPERS, default CUs - 1; 0 = one workgroup).  Builds the
  * same trees as the host-driven cwq_fit_kl / cwq_fit_node_op path (fit.py).  dim <= 1024.
+ * Errors: CWQ_ERR_OOM only for a node pool / child arena that cannot be allocated or
+ * runs out inside an insert (fit.py then continues on the host fitter); a chip-wide KL
+ * pass that did not complete is CWQ_ERR_HIP (fit.py raises).
  *   cwq_fit_create   a handle with room for cap_nodes nodes
  *   cwq_fit_load     the tree in slots 0..n_nodes-1: parent (host, -1 at the root),
  *                    children in list order as CSR (host child_ptr [n+1], child_idx),

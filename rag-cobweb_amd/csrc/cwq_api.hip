@@ -1326,7 +1326,7 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
 // Workspace of one chunk: X + the [nq][NI] internal arrays -- S_int and P always; BF and
 // LPF (path bottleneck, full log_prob) only for categorize / log_prob (`full`).
 size_t group_bytes_per_query(const cwq_index* ix) {
-  return ix->grp_mode ? (size_t)ix->G * 8 + (size_t)4 * std::max(ix->NI, 1) * 4 + 5 * 256 : 0;
+  return ix->grp_mode ? (size_t)ix->G * 16 + (size_t)4 * std::max(ix->NI, 1) * 4 + 5 * 256 : 0;
 }
 size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad, bool full = true) {
   return (size_t)nq_pad * ix->DP * 4 + (full ? 4 : 2) * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256 +
@@ -1348,7 +1348,7 @@ void carve_chunk(cwq_index* ix, Bump& b, Chunk& c, int nq, bool full = true) {
       c.LPF = b.take<float>(n);
     }
     if (ix->grp_mode) {
-      c.gsh = b.take<double>((size_t)c.nq_pad * ix->G);
+      c.gsh = b.take<double>((size_t)2 * c.nq_pad * ix->G);   // the shifts, then their error bounds
       c.Pg_lo = b.take<float>(n);
       c.Pg_hi = b.take<float>(n);
       c.Pc_lo = b.take<float>(n);
@@ -1650,11 +1650,13 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   const char* fpe = getenv("CWQ_PROBE_PREP");
   const bool fprep = fused && ix->NI == 1 && nqb == 1 && !i8 && ix->DP <= 1024 && !sel_unfused() &&
                      (fpe && *fpe && atoi(fpe) == 1);
-  if (fprep && !ix->sel_ctr) {   // the fused select's counter: zeroed once, reset by its last workgroup
+  if (fprep && !ix->sel_ctr)   // the fused select's counter (lives across calls)
     if ((rc = ix->alloc(&ix->sel_ctr, 1))) return rc;
-    HIPCHK(hipMemsetAsync(ix->sel_ctr, 0, 4, s));
-  }
   if (fprep) {
+    // re-zeroed on every such call: its last workgroup resets it too, but an aborted launch
+    // or one with another grid size would leave it nonzero and later calls would read stale
+    // thresholds (this opt-in path only; the default path's counter is zeroed by the prep)
+    HIPCHK(hipMemsetAsync(ix->sel_ctr, 0, 4, s));
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[1], s));
   } else if (fused) {
     HIPCHK(launch_sb_prep(sp, s));

@@ -5,9 +5,12 @@
 // The tree lives in device memory: a pool of node statistics (count, mean, meanSq =
 // Welford M2, CobwebTorchNode.py:31-68), parent links and per-node child lists in list
 // order (slabs of an arena; append at the end, remove with the tail shifted left, as
-// Python's list.append / list.remove).  One 1024-thread workgroup runs the inserts in
-// order; per tree level it computes every child's KL terms (one wave per child), then
-// one thread makes the reference's scalar decisions in its float32 op order:
+// Python's list.append / list.remove).  The launch is one master workgroup plus (CUs - 1)
+// helper workgroups, each of 512 threads (kFdThreads; one per CU).  The master runs the
+// inserts in order; per tree level every child's KL terms are computed (one wave per child;
+// a level with >= fork_min children -- CWQ_FIT_FORK_MIN, default 64 -- is forked: the master
+// publishes a job and every workgroup claims 4-child slices, fd_fork / fd_helper), then the
+// reference's scalar decisions are made in its float32 op order:
 //   two_best_children (CobwebTorchNode.py:374-420): gain = p1*KL(c+x || P+x) -
 //     p2*KL(c || P+x), sorted by (gain, count, random()) descending;
 //   pu_for_insert / pu_for_new_child / pu_for_merge / pu_for_split (:422-650), each a
@@ -18,9 +21,11 @@
 // device from the state the host hands over (random.getstate()) and handed back after,
 // so the draws -- b per level for the child sort, then best, new, [merge], [split] --
 // are the reference's.  KL (compute_score, CobwebTorchTree.py:344-364) per element in
-// the reference's fp32 op order (contraction off), the two D-sums in fp64 per lane
-// (lane stride 64) then a butterfly, rounded once -- exactly cwq_fit_kl's arithmetic,
-// so this and the host-driven fitter (fit.py TreeFitter.ifit) build identical trees.
+// the reference's fp32 op order (contraction off, correctly rounded logs: ref_logf), the
+// two D-sums in torch's own float32 cascade-sum order (cwq_refmath.h torch_sum2) -- the
+// reference's CPU arithmetic, and exactly cwq_fit_kl's, so this and the host-driven
+// fitter (fit.py TreeFitter.ifit) build identical trees.  Every cross-workgroup wait is
+// bounded; a join that times out ends the insert with FD_HANG (CWQ_ERR_HIP to the caller).
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <math.h>

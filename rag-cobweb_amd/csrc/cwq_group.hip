@@ -78,22 +78,33 @@ hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, in
 }
 
 // sh[q][g] = -2 x'.d_g in fp64 (x' = fl(x - c0) exactly as query_prep forms it; d_g = c_g - c0
-// in fp64, exact).  One wave per (query, group).
+// in fp64, exact).  One wave per (query, group).  she[q][g] bounds the fp64 evaluation error
+// of sh: products rounded once, ceil(D/64) sequential adds per lane, 6 butterfly levels, so
+// |err| <= gamma_{D/64+8} * 2 sum |x'_i d_i| -- relative to the sum of |terms|, not to |sh|,
+// which cancellation can make much smaller (a query nearly orthogonal to d_g).
 __global__ void group_shift_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c0,
-                                   const float* __restrict__ cent, int G, double* sh) {
+                                   const float* __restrict__ cent, int G, double* sh, double* she) {
   const int lane = threadIdx.x & 63;
   const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
   if (w >= nq * (int64_t)G) return;
   const int64_t qi = w / G;
   const int g = (int)(w % G);
-  double a = 0.0;
+  double a = 0.0, ab = 0.0;
   for (int d = lane; d < D; d += 64) {
     const float xc = q[qi * D + d] - c0[d];
     const double dd = (double)cent[(int64_t)g * D + d] - (double)c0[d];
-    a += (double)xc * dd;
+    const double t = (double)xc * dd;
+    a += t;
+    ab += fabs(t);
   }
-  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
-  if (lane == 0) sh[qi * G + g] = -2.0 * a;
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    ab += __shfl_xor(ab, off, 64);
+  }
+  if (lane == 0) {
+    sh[qi * G + g] = -2.0 * a;
+    she[qi * G + g] = 2.0 * ab * ((double)(D / 64 + 8) * 0x1.02p-53);
+  }
 }
 
 // Outward-rounded fp32 interval of t (fp64), widened by e.
@@ -107,8 +118,9 @@ __device__ __forceinline__ void out_round(double t, double e, float& lo, float& 
 // Pclo is set, categorize [P'c lo, hi] = Fc[p] * sh (zero for nodes without a group).
 __global__ void group_pprime_kernel(const float* __restrict__ P, int64_t ldP, int nq, int NI,
                                     const int* __restrict__ grp, const double* __restrict__ F,
-                                    const double* __restrict__ Fc, const double* __restrict__ sh, int G, float* Plo,
-                                    float* Phi, float* Pclo, float* Pchi) {
+                                    const double* __restrict__ Fc, const double* __restrict__ sh,
+                                    const double* __restrict__ she, int G, float* Plo, float* Phi, float* Pclo,
+                                    float* Pchi) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= (int64_t)nq * NI) return;
   const int64_t qi = i / NI;
@@ -125,16 +137,16 @@ __global__ void group_pprime_kernel(const float* __restrict__ P, int64_t ldP, in
     }
     return;
   }
-  const double s = sh[qi * G + g];
+  const double s = sh[qi * G + g], se = she[qi * G + g];
   const double a = F[p] * s;
   const double t = (double)pv + a;
   float lo, hi;
-  out_round(t, (fabs((double)pv) + fabs(a)) * 0x1p-50, lo, hi);
+  out_round(t, fabs(F[p]) * se + (fabs((double)pv) + fabs(a)) * 0x1p-50, lo, hi);
   Plo[o] = lo;
   Phi[o] = hi;
   if (Pclo) {
     const double c = Fc[p] * s;
-    out_round(c, fabs(c) * 0x1p-50, lo, hi);
+    out_round(c, fabs(Fc[p]) * se + fabs(c) * 0x1p-50, lo, hi);
     Pclo[o] = lo;
     Pchi[o] = hi;
   }
@@ -145,11 +157,12 @@ hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0,
                                  double* sh, float* Plo, float* Phi, float* Pclo, float* Pchi, hipStream_t s) {
   if (nq <= 0 || NI <= 0 || G <= 0) return hipSuccess;
   const int64_t nw = (int64_t)nq * G;
+  double* she = sh + nw;   // sh holds 2 nq G doubles: the shifts, then their error bounds
   hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, q, (int64_t)nq, D, c0, cent,
-                     G, sh);
+                     G, sh, she);
   const int64_t n = (int64_t)nq * NI;
   hipLaunchKernelGGL(group_pprime_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, ldP, nq, NI, grp, F,
-                     Fc, sh, G, Plo, Phi, Pclo, Pchi);
+                     Fc, sh, she, G, Plo, Phi, Pclo, Pchi);
   return hipGetLastError();
 }
 
@@ -201,15 +214,16 @@ __global__ void internal_chain_kernel(const IntFinishArgs f) {
     return;
   }
   const double sv = f.sh[(size_t)qi * f.G + g];
+  const double se = f.sh[(size_t)f.nq * f.G + (size_t)qi * f.G + g];   // its error bound (group_shift_kernel)
   const double a = f.F[i] * sv;
   const double tt = (double)P + a;
   float lo, hi;
-  out_round(tt, (fabs((double)P) + fabs(a)) * 0x1p-50, lo, hi);
+  out_round(tt, fabs(f.F[i]) * se + (fabs((double)P) + fabs(a)) * 0x1p-50, lo, hi);
   f.Plo[o] = lo;
   f.Phi[o] = hi;
   if (f.Pclo) {
     const double c = f.Fc[i] * sv;
-    out_round(c, fabs(c) * 0x1p-50, lo, hi);
+    out_round(c, fabs(f.Fc[i]) * se + fabs(c) * 0x1p-50, lo, hi);
     f.Pclo[o] = lo;
     f.Pchi[o] = hi;
   }
@@ -221,7 +235,7 @@ hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s) {
   if (f.G > 0) {   // the shifts first (one wave per (query, group))
     const int64_t nw = (int64_t)f.nq * f.G;
     hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, f.q, (int64_t)f.nq, f.D,
-                       f.c0, f.cent, f.G, f.sh);
+                       f.c0, f.cent, f.G, f.sh, f.sh + nw);
   }
   const int64_t n = (int64_t)f.nq * f.NI;
   hipLaunchKernelGGL(internal_chain_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f);

@@ -372,8 +372,11 @@ __device__ __forceinline__ void list64_insert(float& lk, int& lr, int lane, floa
 // Bitonic sort of one value per lane into a list64 list: descending by key, ascending row
 // on equal keys (the list order list64_insert keeps), an aux value carried along.  21
 // exchange steps instead of up to 64 serial inserts when a list is filled from empty.
+// cat (AUX only): categorize lists order equal keys by the smaller aux (the row's own lp)
+// first, then row -- list_before<true> (cwq_kernels.hip), so a list cut inside a tie at its
+// last key keeps the rows that attain it.
 template <bool AUX>
-__device__ __forceinline__ void wave_sort64(float& k, int& r, float& a, int lane) {
+__device__ __forceinline__ void wave_sort64(float& k, int& r, float& a, int lane, bool cat = false) {
 #pragma unroll
   for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
@@ -382,8 +385,9 @@ __device__ __forceinline__ void wave_sort64(float& k, int& r, float& a, int lane
       const int pr = __shfl_xor(r, st, 64);
       const float pa = AUX ? __shfl_xor(a, st, 64) : 0.f;
       const bool hold_better = ((lane & st) == 0) == ((lane & size) == 0);
-      const bool pbet = pk > k || (pk == k && pr < r);
-      const bool obet = k > pk || (k == pk && r < pr);
+      const bool ca = AUX && cat && pa != a;
+      const bool pbet = pk > k || (pk == k && (ca ? pa < a : pr < r));
+      const bool obet = k > pk || (k == pk && (ca ? a < pa : r < pr));
       if (hold_better ? pbet : obet) {
         k = pk;
         r = pr;
@@ -393,10 +397,16 @@ __device__ __forceinline__ void wave_sort64(float& k, int& r, float& a, int lane
   }
 }
 
+// (key, aux, row) list order: key descending; equal keys by row, or for categorize lists
+// (cat) by the smaller aux first, then row (list_before<true>, cwq_kernels.hip)
+__device__ __forceinline__ bool entry_before(float k, float a, int r, float k2, float a2, int r2, bool cat) {
+  return k > k2 || (k == k2 && (cat && a != a2 ? a < a2 : r < r2));
+}
+
 // list64_insert with an aux value carried along (final_wide_kernel's (key, lp, row) lists)
 __device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr, int lane, float ck, float ca, int cr,
-                                                  int K) {
-  const bool prec = lk > ck || (lk == ck && lr < cr);
+                                                  int K, bool cat = false) {
+  const bool prec = entry_before(lk, la, lr, ck, ca, cr, cat);
   const int pos = __popcll(__ballot(prec));
   if (pos < K) {
     const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));

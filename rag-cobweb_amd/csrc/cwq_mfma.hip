@@ -2228,18 +2228,19 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           lk = key == key ? key : -CWQ_INF;   // a NaN key never enters (as the insertions)
           la = lp;
           lr = lk == -CWQ_INF ? 0x7fffffff : rid;
-          wave_sort64<true>(lk, lr, la, lane);
+          wave_sort64<true>(lk, lr, la, lane, cat);
         }
-        const float tk = rl_f2(lk, K - 1);
+        // the list order is list_before<cat> (categorize: equal keys by own lp ascending)
+        const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
         const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-        uint64_t mask = __ballot(act && r0 != 0 && (nopf || key > tk || (key == tk && rid < tr)));
+        uint64_t mask = __ballot(act && r0 != 0 && (nopf || entry_before(key, lp, rid, tk, ta, tr, cat)));
         if (nopf && r0 == 0) mask = __ballot(act);
         while (mask) {
           const int b = __builtin_ctzll(mask);
           mask &= mask - 1;
           const float ck = rl_f2(key, b), ca = rl_f2(lp, b);
           const int cr = __builtin_amdgcn_readlane(rid, b);
-          const bool prec = lk > ck || (lk == ck && lr < cr);
+          const bool prec = entry_before(lk, la, lr, ck, ca, cr, cat);
           const int pos = __popcll(__ballot(prec));
           if (pos < K) {
             const float sk = __int_as_float(wave_shr1(__float_as_int(lk)));
@@ -2272,13 +2273,14 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
         for (int w = 1; w < nkw; ++w) {
           const float key = s_ml[w * 64 + lane], lp = s_ma[w * 64 + lane];
           const int rid = s_mr[w * 64 + lane];
-          const float tk = rl_f2(lk, K - 1);
+          const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
           const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-          uint64_t mask = __ballot(rid != 0x7fffffff && (key > tk || (key == tk && rid < tr)));
+          uint64_t mask = __ballot(rid != 0x7fffffff && entry_before(key, lp, rid, tk, ta, tr, cat));
           while (mask) {
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1;
-            list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K);
+            list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K,
+                              cat);
           }
         }
       }

@@ -25,7 +25,7 @@ import random as _random_mod
 import numpy as np
 import torch
 
-from ._lib import check, lib
+from ._lib import CWQ_ERR_OOM, check, lib
 from .tree import Node
 
 F32 = np.float32
@@ -346,9 +346,11 @@ class DeviceTreeFitter:
     def fit_batch(self, X):
         """Insert the rows of X in order; returns the node each row ended in (ifit's
         return value, CobwebTorchTree.py:123-141), as host Node objects.  If the device
-        pool cannot be allocated or runs out mid-insert, the remaining rows go through
-        the host-driven TreeFitter from the last exported tree and random() state (the
-        same tree either way)."""
+        pool cannot be allocated or runs out mid-insert (CWQ_ERR_OOM), the remaining rows
+        go through the host-driven TreeFitter from the last exported tree and random()
+        state (the same tree either way).  Any other failure -- a HIP error, bad
+        arguments, or a chip-wide KL pass that did not complete (a protocol fault) --
+        raises RuntimeError instead of hiding behind a slower fit."""
         import time
         L = lib()
         X = torch.as_tensor(X if torch.is_tensor(X) else np.asarray(X, F32), dtype=torch.float32)
@@ -367,26 +369,36 @@ class DeviceTreeFitter:
             old = self.rng.getstate()
             self.rng.setstate((old[0], tuple(int(v) for v in mt), old[2]))
 
+        def failed(rc, call):
+            """The host fallback's reason for a full pool; raise for anything else."""
+            msg = L.cwq_fit_last_error().decode()
+            if rc == CWQ_ERR_OOM:
+                return msg
+            raise RuntimeError(f"{call} failed (status {rc}): {msg}")
+
         while done < n:
             nodes, parent, cptr, cidx, count, mean, m2 = self._flatten()
             cap = self._pool_cap(len(nodes), n - done)
             h = ctypes.c_void_p()
             with torch.cuda.device(self.dev):
-                if L.cwq_fit_create(self.dev.index, self.D, float(self.tree.prior_var), cap, ctypes.byref(h)):
-                    fallback = L.cwq_fit_last_error().decode()
+                rc = L.cwq_fit_create(self.dev.index, self.D, float(self.tree.prior_var), cap, ctypes.byref(h))
+                if rc:
+                    fallback = failed(rc, "cwq_fit_create")
                     break
                 try:
-                    if L.cwq_fit_load(h, len(nodes), 0, _np_ptr(parent), _np_ptr(cptr), _np_ptr(cidx),
-                                      _np_ptr(count), _np_ptr(mean), _np_ptr(m2), _np_ptr(mt), sp):
-                        fallback = L.cwq_fit_last_error().decode()
+                    rc = L.cwq_fit_load(h, len(nodes), 0, _np_ptr(parent), _np_ptr(cptr), _np_ptr(cidx),
+                                        _np_ptr(count), _np_ptr(mean), _np_ptr(m2), _np_ptr(mt), sp)
+                    if rc:
+                        fallback = failed(rc, "cwq_fit_load")
                         break
                     loads += 1
                     t0 = time.perf_counter()
-                    if L.cwq_fit_insert(h, ctypes.c_void_p(X[done:].data_ptr()), n - done,
-                                        ctypes.c_void_p(leaf[done:].data_ptr()), _np_ptr(info), sp):
-                        # e.g. the pool ran out inside one insert: the device tree is
+                    rc = L.cwq_fit_insert(h, ctypes.c_void_p(X[done:].data_ptr()), n - done,
+                                          ctypes.c_void_p(leaf[done:].data_ptr()), _np_ptr(info), sp)
+                    if rc:
+                        # the pool ran out inside one insert: the device tree is
                         # mid-operation, so nothing of this load is kept
-                        fallback = L.cwq_fit_last_error().decode()
+                        fallback = failed(rc, "cwq_fit_insert")
                         break
                     t_kernel += time.perf_counter() - t0
                     used = int(info[3])
@@ -398,9 +410,10 @@ class DeviceTreeFitter:
                     MEAN = np.zeros((used, self.D), F32)
                     M2 = np.zeros((used, self.D), F32)
                     mt_new = mt.copy()
-                    if L.cwq_fit_export(h, _np_ptr(out2), _np_ptr(P), _np_ptr(CP), _np_ptr(CI), _np_ptr(CNT),
-                                        _np_ptr(MEAN), _np_ptr(M2), _np_ptr(mt_new), sp):
-                        fallback = L.cwq_fit_last_error().decode()
+                    rc = L.cwq_fit_export(h, _np_ptr(out2), _np_ptr(P), _np_ptr(CP), _np_ptr(CI), _np_ptr(CNT),
+                                          _np_ptr(MEAN), _np_ptr(M2), _np_ptr(mt_new), sp)
+                    if rc:
+                        fallback = failed(rc, "cwq_fit_export")
                         break
                 finally:
                     L.cwq_fit_destroy(h)

@@ -278,3 +278,21 @@ def test_chip_wide_fit_flat_768_matches_oracle_1k_prefix(pkg, monkeypatch):
         np.testing.assert_array_equal(m2, np.stack([x.meanSq for x in onodes]))
         assert random.random() == want_r
     assert len(ot.root.children) > 900
+
+@pytest.mark.parametrize("call,rc", [("cwq_fit_insert", -2), ("cwq_fit_load", -2), ("cwq_fit_create", -1)])
+def test_device_fit_non_oom_failure_raises(pkg, call, rc, monkeypatch):
+    """Only a full pool (CWQ_ERR_OOM) sends the rest of a batch to the host fitter.  A HIP
+    error -- which is how cwq_fit_insert reports a chip-wide KL pass that did not complete
+    (FD_HANG) -- or bad arguments raise: a protocol fault must not hide behind a slower fit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((40, 32)).astype(np.float32)
+    monkeypatch.setenv("CWQ_FIT_DEVICE", "1")
+    random.seed(3)
+    w = pkg.CobwebWrapper(corpus=[f"s{i}" for i in range(20)], corpus_embeddings=X[:20])
+    fitmod = __import__(type(w).__module__.rsplit(".", 1)[0] + ".fit", fromlist=["DeviceTreeFitter"])
+    L = fitmod.lib()
+    monkeypatch.setattr(L, call, lambda *a: rc)
+    with pytest.raises(RuntimeError, match=f"{call} failed \\(status {rc}\\)"):
+        w.add_sentences([f"s{i}" for i in range(20, 40)], X[20:])
