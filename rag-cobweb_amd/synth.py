@@ -138,3 +138,39 @@ def balanced_synth(X, branching, depth, seed=0):
     node_of_sentence[leaf_order.cpu()] = torch.arange(off, off + N)
     return dict(mean=mean, var=var, parent=torch.cat(parent).to(torch.int64).numpy(),
                 node_of_sentence=node_of_sentence.numpy(), n_internal=off)
+
+
+def tree_synth(X, parent, node_of_sentence):
+    """The statistics of a given tree STRUCTURE over the rows X: every node's count, mean
+    and meanSq by sequential Welford over the rows of its subtree (ascending row index),
+    var = compute_var (prior_var for a node without rows).  parent: BFS-ordered parent
+    array (-1 at the root); node_of_sentence: the node each row sits in.  Used to rebuild a
+    device-ifit tree's shape (e.g. config C2's) from its saved structure without re-running
+    ifit: the shape is ifit's, the statistics are batch Welford's (bit-different from the
+    incremental ones, so not a reference tree -- a workload for the query kernels)."""
+    N, D = X.shape
+    dev = X.device
+    par = torch.as_tensor(parent, dtype=torch.int64, device=dev)
+    nos = torch.as_tensor(node_of_sentence, dtype=torch.int64, device=dev)
+    Nn = par.numel()
+    rows = torch.arange(N, device=dev)
+    cur, nodes, rws = nos.clone(), [], []
+    while True:
+        live = cur >= 0
+        if not bool(live.any()):
+            break
+        nodes.append(cur[live])
+        rws.append(rows[live])
+        cur = torch.where(live, par[cur.clamp(min=0)], cur)
+    node_ids = torch.cat(nodes)
+    row_ids = torch.cat(rws)
+    order_key = torch.argsort(node_ids * N + row_ids)
+    order = row_ids[order_key]
+    cnt_per = torch.bincount(node_ids, minlength=Nn)
+    gptr = torch.zeros(Nn + 1, dtype=torch.int64, device=dev)
+    gptr[1:] = torch.cumsum(cnt_per, 0)
+    cnt, mu, m2 = welford_groups(X, order, gptr)
+    empty = cnt_per == 0
+    var = torch.where(empty[:, None], torch.full_like(m2, float(PRIOR_VAR)), _var_of(cnt.clamp(min=1), m2))
+    mu = torch.where(empty[:, None], torch.zeros_like(mu), mu)
+    return dict(mean=mu, var=var, parent=par.cpu().numpy(), node_of_sentence=nos.cpu().numpy(), count=cnt)

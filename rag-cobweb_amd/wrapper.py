@@ -374,15 +374,49 @@ class CobwebWrapper:
         return w
 
     @classmethod
-    def from_index(cls, index, sentences, encode_func=lambda x: x):
+    def from_index(cls, index, sentences, encode_func=lambda x: x, node_of_sentence=None):
         """A query-only wrapper over a prebuilt CobwebIndex (e.g. a flat-synth tree at C3/C4
         scale, where the host keeps no node objects): the Fast / rank-score / batch entry
-        points work; the add path and Basic's id expansion need the node tree."""
+        points work; the add path needs the node tree.  With node_of_sentence (the BFS node
+        of every sentence, as given to the index) Basic (cobweb_predict) works too: its id
+        expansion reads per-node sentence lists made on first use (_NodeSentences)."""
         w = cls(device=index.device, encode_func=encode_func)
         w.sentences = sentences          # any sequence (len + indexing); not copied
         w._index = index
         w._prediction_index_valid = True
+        if node_of_sentence is not None:
+            w._nodes = _NodeSentences(node_of_sentence, index.n_nodes)
         return w
 
     def __len__(self):
         return len(self.sentences)
+
+
+class _NodeSentences:
+    """nodes[i].sentence_id for a wrapper without host Node objects: the sentence ids of
+    BFS node i (ascending), made on first access and kept, so the in-place random.shuffle
+    of Basic's id expansion (CobwebWrapper.py:456) persists across calls as on the
+    reference's node lists."""
+
+    class _Ref:
+        __slots__ = ("sentence_id",)
+
+        def __init__(self, ids):
+            self.sentence_id = ids
+
+    def __init__(self, node_of_sentence, n_nodes):
+        nos = np.asarray(node_of_sentence, np.int64)
+        order = np.argsort(nos, kind="stable")
+        self._ids = order
+        self._ptr = np.searchsorted(nos[order], np.arange(n_nodes + 1))
+        self._made = {}
+
+    def __len__(self):
+        return len(self._ptr) - 1
+
+    def __getitem__(self, i):
+        r = self._made.get(i)
+        if r is None:
+            r = self._Ref([int(v) for v in self._ids[self._ptr[i]:self._ptr[i + 1]]])
+            self._made[i] = r
+        return r

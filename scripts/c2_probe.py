@@ -53,6 +53,14 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--calls", type=int, default=300, help="one-query calls timed per leg")
     ap.add_argument("--basic-only", action="store_true", help="only the Basic legs (e.g. under rocprofv3)")
+    ap.add_argument("--fast-only", action="store_true", help="only the Fast legs")
+    ap.add_argument("--legs", default="all",
+                    help="comma list of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
+    ap.add_argument("--save-struct", default=None,
+                    help="write the ifit tree's structure (BFS parent, node of each row) to this .npz")
+    ap.add_argument("--load-struct", default=None,
+                    help="skip ifit: the tree structure from a --save-struct file, node statistics by batch "
+                         "Welford over the same corpus (synth.tree_synth) -- the same shape for the query legs")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     X, Qn, pick = corpus(args.n, args.dim, args.clusters, args.nq)
@@ -62,31 +70,64 @@ def main():
     torch.cuda.synchronize()
     random.seed(2)
     t0 = time.perf_counter()
-    w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(args.n)], corpus_embeddings=X)
-    torch.cuda.synchronize()
-    t_fit = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    w.build_prediction_index()
+    if args.load_struct:
+        z = np.load(args.load_struct)
+        t = pkg.synth.tree_synth(torch.from_numpy(X).cuda(), z["parent"], z["node_of_sentence"])
+        t_fit = 0.0
+        t0 = time.perf_counter()
+        ix = pkg.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], [1.0] * 6, device="cuda:0")
+        w = pkg.CobwebWrapper.from_index(ix, [f"p{i}" for i in range(args.n)], node_of_sentence=t["node_of_sentence"])
+        del t
+    else:
+        w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(args.n)], corpus_embeddings=X)
+        torch.cuda.synchronize()
+        t_fit = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        w.build_prediction_index()
     torch.cuda.synchronize()
     t_ix = time.perf_counter() - t0
     ix = w._index
+    if args.save_struct:
+        nodes, parent, _, _, nos, _ = w.tree.flatten(args.n)
+        np.savez_compressed(args.save_struct, parent=parent.astype(np.int32), node_of_sentence=nos.astype(np.int32))
+        print(f"saved the tree structure to {args.save_struct}", flush=True)
     inf = ix.info
-    root_c = len(w.tree.root.children)
+    root_c = int((np.load(args.load_struct)['parent'] == 0).sum()) if args.load_struct else len(w.tree.root.children)
     print(f"filter rows: {ix.filter_info()}", flush=True)
-    print(f"C2 corpus {args.n}x{args.dim} ({args.clusters} clusters): device ifit {t_fit:.2f} s "
-          f"({args.n / t_fit:.0f} inserts/s); tree {inf['n_nodes']} nodes, {inf['internal_nodes']} internal, "
+    print(f"C2 corpus {args.n}x{args.dim} ({args.clusters} clusters): " +
+          ("tree structure loaded, batch-Welford stats " if args.load_struct else "") + f"device ifit {t_fit:.2f} s "
+          f"({args.n / max(t_fit, 1e-9):.0f} inserts/s); tree {inf['n_nodes']} nodes, {inf['internal_nodes']} internal, "
           f"max depth {inf['max_depth']}, root children {root_c}; index build {t_ix:.2f} s "
           f"({inf['device_bytes'] / 1e9:.2f} GB)", flush=True)
     Q = torch.from_numpy(Qn).cuda()
     k = args.k
     if not args.basic_only:
         fast_legs(args, w, ix, Q, Qn, pick, k)
-    basic_legs(args, w, ix, Q, Qn, k)
+    if not args.fast_only:
+        basic_legs(args, w, ix, Q, Qn, k)
     print("done", flush=True)
 
 
+def want(args, leg):
+    return args.legs == "all" or leg in args.legs.split(",")
+
+
 def fast_legs(args, w, ix, Q, Qn, pick, k):
-    # Fast batch
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, k)
+    ix.set_filter(-1)
+    if want(args, "fbatch"):
+        fast_batch(args, ix, Q, pick, k, ids0, s0)
+    for nq in (1, 8, 64):
+        if want(args, f"fpc{nq}"):
+            fast_percall(args, ix, Q, k, ids0, nq)
+    if want(args, "fphase"):
+        fast_phases(ix, Q, k)
+    if want(args, "fharness"):
+        fast_harness(args, w, Qn, k)
+
+
+def fast_batch(args, ix, Q, pick, k, ids0, s0):
     ix.set_filter(0)
     ids0, s0 = ix.score_topk(Q, k)
     t_scan = med(lambda: ix.score_topk(Q, k), 5)
@@ -105,21 +146,25 @@ def fast_legs(args, w, ix, Q, Qn, pick, k):
           f"fallback queries {st['fallback_queries']}; "
           f"perturbed passage ranked first {top1:.3f}", flush=True)
     print(f"  last call phases (HIP events, ms): " + ", ".join(f"{a} {b:.3f}" for a, b in tm.items()), flush=True)
-    # one query per call
-    for nq in (1, 8, 64):
-        qs = [Q[i:i + nq].contiguous() for i in range(0, min(args.nq, args.calls * nq), nq)][:args.calls]
-        ok = all(torch.equal(ix.score_topk(q, k)[0], ids0[i * nq:i * nq + nq]) for i, q in enumerate(qs[:20]))
-        ts = []
-        for q in qs:
-            t0 = time.perf_counter()
-            ix.score_topk(q, k)
-            torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t0)
-        ts.sort()
-        st = ix.last_stats()
-        print(f"Fast per call nq={nq} (score_topk, device tensor): median {ts[len(ts) // 2] * 1e6:.1f} us, "
-              f"p10 {ts[len(ts) // 10] * 1e6:.1f} us; path {st['path']} int8 {st['int8_pass']}; "
-              f"== exact {ok}", flush=True)
+
+
+def fast_percall(args, ix, Q, k, ids0, nq):
+    qs = [Q[i:i + nq].contiguous() for i in range(0, min(args.nq, args.calls * nq), nq)][:args.calls]
+    ok = all(torch.equal(ix.score_topk(q, k)[0], ids0[i * nq:i * nq + nq]) for i, q in enumerate(qs[:20]))
+    ts = []
+    for q in qs:
+        t0 = time.perf_counter()
+        ix.score_topk(q, k)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    st = ix.last_stats()
+    print(f"Fast per call nq={nq} (score_topk, device tensor): median {ts[len(ts) // 2] * 1e6:.1f} us, "
+          f"p10 {ts[len(ts) // 10] * 1e6:.1f} us; path {st['path']} int8 {st['int8_pass']}; "
+          f"== exact {ok}", flush=True)
+
+
+def fast_phases(ix, Q, k):
     # one query per call: phase times from HIP events (median over 30 calls)
     ix.set_timing(True)
     ph = []
@@ -129,6 +174,9 @@ def fast_legs(args, w, ix, Q, Qn, pick, k):
     ix.set_timing(False)
     print("  per-call phases (HIP events, median ms): " +
           ", ".join(f"{n} {sorted(p[n] for p in ph)[15]:.4f}" for n in ph[0] if n.endswith("_ms")), flush=True)
+
+
+def fast_harness(args, w, Qn, k):
     ts = []
     for i in range(args.calls):
         t0 = time.perf_counter()
@@ -140,13 +188,20 @@ def fast_legs(args, w, ix, Q, Qn, pick, k):
 
 
 def basic_legs(args, w, ix, Q, Qn, k):
-    # Basic
     nodes, found, calls = ix.categorize(Q, k, w.max_init_search)
-    t_b = med(lambda: ix.categorize(Q, k, w.max_init_search), 5)
-    cst = ix.last_categorize_stats()
-    print(f"Basic batch nq={args.nq}: {t_b * 1e3:.3f} ms = {args.nq / t_b:.0f} q/s; found-k "
-          f"{float((found == k).float().mean()):.3f}; log_prob calls/query mean {float(calls.float().mean()):.0f}; "
-          f"resolved {cst}", flush=True)
+    if want(args, "bbatch"):
+        t_b = med(lambda: ix.categorize(Q, k, w.max_init_search), 5)
+        cst = ix.last_categorize_stats()
+        print(f"Basic batch nq={args.nq}: {t_b * 1e3:.3f} ms = {args.nq / t_b:.0f} q/s; found-k "
+              f"{float((found == k).float().mean()):.3f}; log_prob calls/query mean "
+              f"{float(calls.float().mean()):.0f}; resolved {cst}", flush=True)
+    if not want(args, "bpc"):
+        return
+    ok = True
+    for i in range(20):   # one-query calls == the batch's rows
+        n1, f1, c1 = ix.categorize(Q[i:i + 1].contiguous(), k, w.max_init_search)
+        ok &= torch.equal(n1[0], nodes[i]) and int(f1[0]) == int(found[i]) and int(c1[0]) == int(calls[i])
+    print(f"Basic one-query calls == batch rows (20 queries): {ok}", flush=True)
     ts = []
     for i in range(min(args.calls, 200)):
         t0 = time.perf_counter()

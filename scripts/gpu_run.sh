@@ -10,6 +10,8 @@
 #   prof            rocprofv3 --kernel-trace --stats of a short bench run -> gpurun_out/TAG_prof/
 #   py:SCRIPT:ARGS  python3 scripts/SCRIPT ARGS (ARGS split on ',')  -> gpurun_out/TAG_SCRIPT.log
 #   rprof:SCRIPT:ARGS  the same probe under rocprofv3 --kernel-trace --stats -> gpurun_out/TAG_SCRIPT_prof/
+#   tl:SCRIPT:ARGS  kernel + copy timeline of the probe's last calls (rocpd; TL_N kernels, default 60)
+#                   -> gpurun_out/TAG_SCRIPT_timeline.txt
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -46,6 +48,17 @@ for step in "$@"; do
           python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --recall-queries 0 > gpurun_out/${TAG}_prof.log 2>&1 \
           || { tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
       tail -1 gpurun_out/${TAG}_prof.log ;;
+    tl:*)
+      IFS=: read -r kind script args <<< "$step"
+      name=${script%.py}
+      IFS=, read -r -a argv <<< "$args"
+      timeout -k 10 ${PY_TIMEOUT:-600} rocprofv3 --kernel-trace --memory-copy-trace --output-format rocpd \
+          -d gpurun_out/${TAG}_${name}_tl -o run -- python3 -u scripts/$script "${argv[@]}" \
+          > gpurun_out/${TAG}_${name}_tl.log 2>&1 || { tail -20 gpurun_out/${TAG}_${name}_tl.log; exit 1; }
+      db=$(find gpurun_out/${TAG}_${name}_tl -name '*.db' | head -1)
+      python3 scripts/rocpd_summary.py "$db" --timeline ${TL_N:-60} > gpurun_out/${TAG}_${name}_timeline.txt 2>&1
+      rm -f "$db"
+      tail -${PY_TAIL:-70} gpurun_out/${TAG}_${name}_timeline.txt ;;
     py:*|rprof:*)
       IFS=: read -r kind script args <<< "$step"
       name=${script%.py}
