@@ -210,6 +210,19 @@ int cwq_set_filter(cwq_index* idx, int mode);
 int cwq_last_stats(cwq_index* idx, int64_t* out6);
 
 /*
+ * Group pruning of the Fast query (clustered trees whose rows are
+ * group-centred, every level weight >= 0): per (query, depth-1 group) a certified upper
+ * bound of every key in the group; the exact internal pass runs for each query's best group
+ * and then only for the groups whose bound reaches the filter's first threshold.  Results
+ * are unchanged (bit-identical to the exact scan); CWQ_GROUP_PRUNE=0 turns it off (at index
+ * creation: never built; per call: not used).  Replaces no reference call: the reference
+ * evaluates every node (CobwebWrapper.py:222-241).
+ * cwq_last_prune_stats(out4): [pruning available on this index, queries of the last Fast
+ * call's pruned chunk (0: not pruned), its stage-B (query, group) pairs, groups].
+ */
+int cwq_last_prune_stats(cwq_index* idx, int64_t* out4);
+
+/*
  * Sequential Welford statistics of row groups (synthetic-tree builder).
  * For group g, folds rows X[order[group_ptr[g]] .. order[group_ptr[g+1]-1]] in
  * that order with exactly the fp32 op sequence of CobwebTorchNode.increment_counts

@@ -18,7 +18,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 HEADER = os.path.join(HERE, "..", "include", "cobweb_query.h")
-SOURCES = ["cwq_kernels.hip", "cwq_api.hip", "cwq_fit.hip", "cwq_mfma.hip", "cwq_whiten.hip", "cwq_stream.hip", "cwq_fitdev.hip", "cwq_group.hip"]
+SOURCES = ["cwq_kernels.hip", "cwq_api.hip", "cwq_fit.hip", "cwq_mfma.hip", "cwq_whiten.hip", "cwq_stream.hip", "cwq_fitdev.hip", "cwq_group.hip", "cwq_prune.hip"]
 OUT = os.path.join(HERE, "libcwq.so")
 ARCH = os.environ.get("CWQ_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC",

@@ -134,6 +134,14 @@ struct cwq_index {
   float* grp_c = nullptr;
   int* grp_par = nullptr;
   double *grp_F = nullptr, *grp_Fc = nullptr;
+  // group pruning of the Fast query (cwq_prune.hip; group-centred trees with every level
+  // weight >= 0): the pruning group of each internal node, group-major internal node lists,
+  // per-group bound constants.  prune_ctr: the last call's stage-B pair count (diagnostics).
+  bool prune_ok = false;
+  int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
+  GroupBound* gbound = nullptr;
+  const int* prune_ctr = nullptr;
+  int64_t prune_nq = 0;
   // internal-node bounds (hierarchical trees): bf16 operand rows, their RowF constants,
   // row-major fp32 A/B copies for the exact chain in final_kernel.  int_path (default):
   // the Fast filter reads the path prefix P of leaf parents only, so there is one row per
@@ -200,6 +208,7 @@ struct cwq_index {
   int reserve(size_t b) {
     if (b <= ws_size) return CWQ_OK;
     if (ws_ev_live) (void)hipEventSynchronize(ws_ev);   // earlier calls' kernels may still read it
+    prune_ctr = nullptr;
     if (ws) (void)hipFree(ws);
     ws = nullptr;
     ws_size = 0;
@@ -277,7 +286,10 @@ struct WsUse {
   cwq_index* ix;
   hipStream_t s;
   int rc;
-  WsUse(cwq_index* i, hipStream_t st) : ix(i), s(st) { rc = ix->ws_begin(s); }
+  WsUse(cwq_index* i, hipStream_t st) : ix(i), s(st) {
+    ix->prune_ctr = nullptr;   // a pointer into the workspace: valid until the next call
+    rc = ix->ws_begin(s);
+  }
   ~WsUse() {
     if (rc == CWQ_OK) (void)ix->ws_end(s);   // ws_begin failed: nothing was queued on s
   }
@@ -589,6 +601,126 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   return CWQ_OK;
 }
 
+// Group pruning constants (cwq_prune.hip).  Groups are the subtrees of the
+// depth-1 internal nodes; members are their internal nodes and the leaf-class rows below
+// them (a row that is itself an internal node belongs to that node's group).  Needs the
+// group-centred mode (group centres), the row-major A/B copies (exact pass of a group), and
+// every level weight and row weight >= 0 (the key bound adds upper bounds of lp' with
+// non-negative coefficients).  CWQ_GROUP_PRUNE=0 at index creation leaves it off.
+int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::vector<int64_t>& int_nodes,
+                const std::vector<int>& par_int, const std::vector<float>& w_int, const std::vector<int64_t>& rows,
+                const std::vector<int>& int_id, const std::vector<RowMeta>& meta, const std::vector<int>& row_par,
+                const std::vector<int>& row_flags, hipStream_t s) {
+  const char* e = getenv("CWQ_GROUP_PRUNE");
+  if ((e && *e && atoi(e) == 0) || !ix->grp_mode || ix->G <= 0 || !ix->int_Ar || ix->NI < 2 || ix->DP > 2048)
+    return CWQ_OK;
+  const int NI = ix->NI, NL = ix->NL, G = ix->G;
+  for (float w : w_int)
+    if (!(w >= 0.f)) return CWQ_OK;
+  for (int r = 0; r < NL; ++r)
+    if (!(meta[r].cw >= 0.f) || !(meta[r].invL >= 0.f)) return CWQ_OK;
+  // pruning group of every internal node: its depth-1 ancestor (plan_groups' numbering)
+  std::vector<int> gint(NI, -1);
+  int ng = 0;
+  for (int i = 1; i < NI; ++i) gint[i] = par_int[i] == 0 ? ng++ : (par_int[i] > 0 ? gint[par_int[i]] : -1);
+  if (ng != G) return CWQ_OK;   // plan_groups numbers the same depth-1 nodes
+  // members: internal nodes 1.., then rows
+  std::vector<int64_t> mnode;
+  std::vector<float> miv;
+  std::vector<int> mgrp;
+  for (int i = 1; i < NI; ++i) {
+    mnode.push_back(int_nodes[i]);
+    miv.push_back(0.f);
+    mgrp.push_back(gint[i]);
+  }
+  std::vector<int> rgrp(NL, -1);
+  for (int r = 0; r < NL; ++r) {
+    const int own = int_id[rows[r]];
+    rgrp[r] = own >= 0 ? gint[own] : (row_par[r] > 0 ? gint[row_par[r]] : -1);
+    mnode.push_back(rows[r]);
+    miv.push_back(r < ix->NL_iso ? meta[r].iv : 0.f);
+    mgrp.push_back(rgrp[r]);
+  }
+  const int64_t nm = (int64_t)mnode.size();
+  int64_t* d_mnode = nullptr;
+  float* d_miv = nullptr;
+  int* d_mgrp = nullptr;
+  double4* d_out = nullptr;
+  int rc;
+  if ((rc = ix->upload(&d_mnode, mnode, s)) || (rc = ix->upload(&d_miv, miv, s)) || (rc = ix->upload(&d_mgrp, mgrp, s)) ||
+      (rc = ix->alloc(&d_out, nm)))
+    return rc;
+  HIPCHK(launch_prune_members(mean, var, ix->D, d_mnode, d_miv, d_mgrp, ix->grp_c, nm, d_out, s));
+  std::vector<double4> mo(nm);
+  std::vector<float> ldi(NI);
+  HIPCHK(hipMemcpyAsync(mo.data(), d_out, nm * sizeof(double4), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ldi.data(), ix->logdet_int, NI * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<GroupBound> gb(G);
+  std::vector<double> d2max(G, 0.0), m2max(G, 0.0);
+  for (auto& b : gb) {
+    b = GroupBound{};
+    b.wmin = INFINITY;
+    b.wmax = 0.0;
+    b.ldmin = INFINITY;
+    b.ldabs = 0.0;
+    b.iLmin = b.Cmin = INFINITY;
+    b.iLmax = b.Cmax = -INFINITY;
+    b.valid = 0;
+  }
+  for (int64_t m = 0; m < nm; ++m) {
+    const int g = mgrp[m];
+    if (g < 0) continue;
+    GroupBound& b = gb[g];
+    b.wmin = std::min(b.wmin, mo[m].x);
+    b.wmax = std::max(b.wmax, mo[m].y);
+    d2max[g] = std::max(d2max[g], mo[m].z);
+    m2max[g] = std::max(m2max[g], mo[m].w);
+    const double ld = m < NI - 1 ? (double)ldi[m + 1] : (double)meta[m - (NI - 1)].logdet;
+    b.ldmin = std::min(b.ldmin, ld);
+    b.ldabs = std::max(b.ldabs, std::fabs(ld));
+  }
+  // the key coefficients of the usable rows: 1/L and C = invL * sum_{path, a != root} w_a + cw
+  std::vector<double> wsum(NI, 0.0);   // sum of w over the path of internal node i, the root excluded
+  for (int i = 1; i < NI; ++i) wsum[i] = wsum[par_int[i]] + (double)w_int[i];
+  for (int r = 0; r < NL; ++r) {
+    const int g = rgrp[r];
+    if (g < 0 || !(row_flags[r] & FLAG_HAS_SENT)) continue;
+    GroupBound& b = gb[g];
+    const double iL = meta[r].invL, C = iL * (row_par[r] > 0 ? wsum[row_par[r]] : 0.0) + (double)meta[r].cw;
+    b.iLmin = std::min(b.iLmin, iL);
+    b.iLmax = std::max(b.iLmax, iL);
+    b.Cmin = std::min(b.Cmin, C * (1.0 - 0x1p-40));
+    b.Cmax = std::max(b.Cmax, C * (1.0 + 0x1p-40));
+    b.valid = 1;
+  }
+  for (int g = 0; g < G; ++g) {
+    GroupBound& b = gb[g];
+    b.r = std::sqrt(d2max[g]) * (1.0 + 0x1p-40) + 1e-30;
+    b.mmax = std::sqrt(m2max[g]) * (1.0 + 0x1p-40);
+    b.wmin *= 1.0 - 0x1p-40;
+    b.wmax *= 1.0 + 0x1p-40;
+    if (!(b.wmin > 0.0) || !std::isfinite(b.wmax) || !std::isfinite(b.ldmin)) b.valid = b.valid ? -1 : 0;
+  }
+  for (auto& b : gb)
+    if (b.valid < 0) return CWQ_OK;   // a member without a finite positive weight: no bound
+  // group-major internal node lists (ascending internal id)
+  std::vector<int> gptr(G + 1, 0), gnodes;
+  for (int i = 1; i < NI; ++i)
+    if (gint[i] >= 0) gptr[gint[i] + 1]++;
+  for (int g = 0; g < G; ++g) gptr[g + 1] += gptr[g];
+  gnodes.assign(gptr[G], 0);
+  std::vector<int> fillp(gptr.begin(), gptr.end() - 1);
+  for (int i = 1; i < NI; ++i)
+    if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
+  if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
+      (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)))
+    return rc;
+  HIPCHK(hipStreamSynchronize(s));
+  ix->prune_ok = true;
+  return CWQ_OK;
+}
+
 }  // namespace
 
 namespace {
@@ -859,6 +991,8 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
     HIPCHK(hipStreamSynchronize(s));   // the rowid host vector is freed on return
     ix->int_bounds = true;
   }
+  if ((rc = build_prune(ix.get(), mean, var, int_nodes, par_int, w_int, rows, int_id, meta, row_par, row_flags, s)))
+    return rc;
   if ((rc = ix->alloc(&ix->dummy, 64))) return rc;
   // the per-call path's int8 row panel is built here, with the index, when its policy
   // holds (flat trees, >= kI8MinBytes of int8 rows, room on the device): no allocation or
@@ -990,6 +1124,65 @@ int group_tables(cwq_index* ix, Chunk& c, const float* q, bool cat, hipStream_t 
   HIPCHK(launch_group_prefixes(q, c.nq, ix->D, ix->iso_c, ix->grp_c, ix->G, c.P, c.ldP, ix->NI, ix->grp_par, ix->grp_F,
                                ix->grp_Fc, c.gsh, c.Pg_lo, c.Pg_hi, cat ? c.Pc_lo : nullptr, cat ? c.Pc_hi : nullptr,
                                s));
+  return CWQ_OK;
+}
+
+// Group pruning (cwq_prune.hip) of a Fast chunk: on by default where the index built its
+// constants (build_prune); CWQ_GROUP_PRUNE=0 turns it off per call (in-process A/Bs).
+bool use_prune(const cwq_index* ix) {
+  if (!ix->prune_ok) return false;
+  const char* e = getenv("CWQ_GROUP_PRUNE");
+  return !(e && *e && atoi(e) == 0);
+}
+size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 20 + 16 : 0; }
+
+// Stage A of the pruned Fast chunk, in place of run_internal + group_tables: the root's raw
+// sums, the group shifts and distances, KUB and g*, the exact pass of g*, the tables.  The
+// caller runs prune_stage_b once the filter's first threshold is on the device.
+int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& pa, hipStream_t s) {
+  const int nq = c.nq, G = ix->G;
+  memset(&pa, 0, sizeof(pa));
+  pa.nq = nq;
+  pa.G = G;
+  pa.NI = ix->NI;
+  pa.DP = ix->DP;
+  pa.D = ix->D;
+  pa.ldS = ix->NI;
+  pa.X = c.X;
+  pa.Ar = ix->int_Ar;
+  pa.Br = ix->int_Br;
+  pa.par_int = ix->par_int;
+  pa.w_int = ix->w_int;
+  pa.logdet_int = ix->logdet_int;
+  pa.gint = ix->prn_gint;
+  pa.gi_ptr = ix->gi_ptr;
+  pa.gi_nodes = ix->gi_nodes;
+  pa.gb = ix->gbound;
+  double* dist2 = b.take<double>((size_t)c.nq_pad * G);
+  pa.dist2 = dist2;
+  pa.S = c.S_int;
+  pa.P = c.P;
+  pa.Plo = c.Pg_lo;
+  pa.Phi = c.Pg_hi;
+  pa.grp = ix->grp_par;
+  pa.F = ix->grp_F;
+  pa.sh = c.gsh;
+  pa.fillP = ix->NL_an > 0 ? 1 : 0;
+  pa.kub = b.take<float>((size_t)c.nq_pad * G);
+  pa.gstar = b.take<int>((size_t)c.nq_pad);
+  pa.pairs = b.take<int2>((size_t)c.nq_pad * G);
+  pa.ctr = b.take<int>(64);
+  HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, nq, c.S_int, ix->NI, s));   // the root
+  HIPCHK(launch_group_shift(q, nq, ix->D, ix->iso_c, ix->grp_c, G, c.gsh, dist2, s));
+  HIPCHK(launch_prune_stage_a(pa, ix->cus, s));
+  c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
+  ix->prune_ctr = pa.ctr;
+  ix->prune_nq = nq;
+  return CWQ_OK;
+}
+
+int prune_stage_b(cwq_index* ix, const PruneArgs& pa, const float* T, int64_t ldT, hipStream_t s) {
+  HIPCHK(launch_prune_stage_b(pa, T, ldT, ix->cus, s));
   return CWQ_OK;
 }
 
@@ -1326,7 +1519,7 @@ int run_leaf_scan(cwq_index* ix, const Chunk& c, int epi, bool cat, int kl, floa
 // Workspace of one chunk: X + the [nq][NI] internal arrays -- S_int and P always; BF and
 // LPF (path bottleneck, full log_prob) only for categorize / log_prob (`full`).
 size_t group_bytes_per_query(const cwq_index* ix) {
-  return ix->grp_mode ? (size_t)ix->G * 16 + (size_t)4 * std::max(ix->NI, 1) * 4 + 5 * 256 : 0;
+  return ix->grp_mode ? (size_t)ix->G * 16 + (size_t)4 * std::max(ix->NI, 1) * 4 + 5 * 256 + prune_bytes_per_query(ix) : 0;
 }
 size_t chunk_bytes(const cwq_index* ix, int64_t nq_pad, bool full = true) {
   return (size_t)nq_pad * ix->DP * 4 + (full ? 4 : 2) * (size_t)nq_pad * std::max(ix->NI, 1) * 4 + 8 * 256 +
@@ -1610,6 +1803,9 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                ((size_t)2 * std::max(ix->DP, ix->DPB) + (size_t)ix->NI * (ix->DP / 16) + ix->NI) * 4 <= 65536 &&
                !getenv("CWQ_SB_UNFUSED");
   SbPrepArgs sp;
+  const bool prn = !ib && use_prune(ix);
+  PruneArgs pra;
+  if (prn) fused = false;
   if (fused) {
     memset(&sp, 0, sizeof(sp));
     sp.q = q;
@@ -1665,6 +1861,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     HIPCHK(launch_pad_queries(q, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
+    } else if (prn) {
+      if ((rc = prune_stage_a(ix, c, q, b, pra, s))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q, 0))) {
       return rc;
     }
@@ -1755,6 +1953,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.sel_ctr = nullptr;
   a.fprep = 0;
   if (!fsel) HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
+  if (prn && (rc = prune_stage_b(ix, pra, tl + (K - 1), 64, s))) return rc;   // the groups T0 cannot exclude
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
   if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)
     StreamArgs a8 = a;
@@ -1835,7 +2034,7 @@ size_t iso_filter_bytes_per_query(const cwq_index* ix, int n_rt) {
 }
 
 int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int K, bool cat, bool ib, Bump& b,
-                   IsoFilter& o, hipStream_t s) {
+                   IsoFilter& o, hipStream_t s, const PruneArgs* prune = nullptr) {
   const int nqc = c.nq;
   const int n_rt = (int)(ix->ld_f / kFgTile);
   const int n_rts = ix->ld_s / kFgTile;
@@ -1915,6 +2114,12 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.ldlb = ix->ld_s / g.lbg;
   HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
   HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
+  if (prune) {   // group pruning: the groups whose key bound reaches the threshold (stage B)
+    int rc;
+    if ((rc = prune_stage_b(ix, *prune, tl + (K - 1), 64, s))) return rc;
+    if (pmm)   // the multi-parent tiles' prefix ranges again, with stage B's tables
+      HIPCHK(launch_tile_prange(c.Pg_lo, c.Pg_hi, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s, &pb));
+  }
   // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
   // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is
   // raised to the K-th largest candidate lower bound, so later phases emit fewer
@@ -2019,14 +2224,18 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                     : (size_t)nq_pad * ((size_t)slabs * K * 12 + (size_t)K * 12) + (size_t)nqf * filt_q + 4096 * 8;
     const bool ib = filt && use_int_bounds(ix);
     if (ib) need += int_bounds_bytes(ix, nqf);
+    const bool prn = filt && !ib && !general && use_prune(ix);
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
     carve_chunk(ix, b, c, nqc, false);
+    PruneArgs pra;
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q + q0 * ix->D, nqf, b, s))) return rc;
+    } else if (prn) {
+      if ((rc = prune_stage_a(ix, c, q + q0 * ix->D, b, pra, s))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q + q0 * ix->D, filt ? 0 : -1))) {
       return rc;
     }
@@ -2043,7 +2252,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         // isotropic rows: sample bounds -> thresholds -> MFMA filter -> candidates ->
         // exact rerank into list slot 0; anisotropic rows: exact scan into slots 1..
         IsoFilter fo;
-        if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, K, false, ib, b, fo, s))) return rc;
+        if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, K, false, ib, b, fo, s, prn ? &pra : nullptr))) return rc;
         int* qcnt = fo.qcnt;
         int* nex = fo.nex;
         okf = fo.okf;
@@ -2142,6 +2351,7 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   DevGuard dg(ix->device);
   for (float& t : ix->t_ms) t = 0.f;
   for (int64_t& t : ix->stats) t = 0;
+  ix->prune_nq = 0;
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
   ScanCfgScope scs(nq);
@@ -2159,6 +2369,23 @@ extern "C" int cwq_set_filter(cwq_index* ix, int mode) {
 extern "C" int cwq_last_stats(cwq_index* ix, int64_t* out) {
   if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
   for (int i = 0; i < 6; ++i) out[i] = ix->stats[i];
+  return CWQ_OK;
+}
+
+extern "C" int cwq_last_prune_stats(cwq_index* ix, int64_t* out) {
+  if (!ix || !out) return fail(CWQ_ERR_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  out[0] = ix->prune_ok ? 1 : 0;
+  out[1] = ix->prune_ctr ? ix->prune_nq : 0;
+  out[2] = 0;
+  out[3] = ix->G;
+  if (ix->prune_ctr) {
+    int v = 0;
+    if (ix->ws_ev_live) HIPCHK(hipEventSynchronize(ix->ws_ev));
+    HIPCHK(hipMemcpy(&v, ix->prune_ctr, sizeof(int), hipMemcpyDeviceToHost));
+    out[2] = v;
+  }
   return CWQ_OK;
 }
 

@@ -82,29 +82,47 @@ hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, in
 // of sh: products rounded once, ceil(D/64) sequential adds per lane, 6 butterfly levels, so
 // |err| <= gamma_{D/64+8} * 2 sum |x'_i d_i| -- relative to the sum of |terms|, not to |sh|,
 // which cancellation can make much smaller (a query nearly orthogonal to d_g).
+// dist2 (optional, group pruning): |x - c_g|^2 in fp64 -- each difference of two floats is
+// exact in fp64 and each square of it too (<= 50 significant bits), so the only error is
+// the fp64 summation's, <= gamma_{D/64+7} dist2 (relative; cwq_prune.hip takes 2^-40).
 __global__ void group_shift_kernel(const float* __restrict__ q, int64_t nq, int D, const float* __restrict__ c0,
-                                   const float* __restrict__ cent, int G, double* sh, double* she) {
+                                   const float* __restrict__ cent, int G, double* sh, double* she, double* dist2) {
   const int lane = threadIdx.x & 63;
   const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
   if (w >= nq * (int64_t)G) return;
   const int64_t qi = w / G;
   const int g = (int)(w % G);
-  double a = 0.0, ab = 0.0;
+  double a = 0.0, ab = 0.0, e2 = 0.0;
   for (int d = lane; d < D; d += 64) {
-    const float xc = q[qi * D + d] - c0[d];
-    const double dd = (double)cent[(int64_t)g * D + d] - (double)c0[d];
+    const float x = q[qi * D + d];
+    const float xc = x - c0[d];
+    const float cg = cent[(int64_t)g * D + d];
+    const double dd = (double)cg - (double)c0[d];
     const double t = (double)xc * dd;
     a += t;
     ab += fabs(t);
+    const double u = (double)x - (double)cg;
+    e2 += u * u;
   }
   for (int off = 32; off > 0; off >>= 1) {
     a += __shfl_xor(a, off, 64);
     ab += __shfl_xor(ab, off, 64);
+    e2 += __shfl_xor(e2, off, 64);
   }
   if (lane == 0) {
     sh[qi * G + g] = -2.0 * a;
     she[qi * G + g] = 2.0 * ab * ((double)(D / 64 + 8) * 0x1.02p-53);
+    if (dist2) dist2[qi * G + g] = e2;
   }
+}
+
+hipError_t launch_group_shift(const float* q, int nq, int D, const float* c0, const float* cent, int G, double* sh,
+                              double* dist2, hipStream_t s) {
+  if (nq <= 0 || G <= 0) return hipSuccess;
+  const int64_t nw = (int64_t)nq * G;
+  hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, q, (int64_t)nq, D, c0, cent,
+                     G, sh, sh + nw, dist2);
+  return hipGetLastError();
 }
 
 // Outward-rounded fp32 interval of t (fp64), widened by e.
@@ -159,7 +177,7 @@ hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0,
   const int64_t nw = (int64_t)nq * G;
   double* she = sh + nw;   // sh holds 2 nq G doubles: the shifts, then their error bounds
   hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, q, (int64_t)nq, D, c0, cent,
-                     G, sh, she);
+                     G, sh, she, nullptr);
   const int64_t n = (int64_t)nq * NI;
   hipLaunchKernelGGL(group_pprime_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, ldP, nq, NI, grp, F,
                      Fc, sh, she, G, Plo, Phi, Pclo, Pchi);
@@ -235,7 +253,7 @@ hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s) {
   if (f.G > 0) {   // the shifts first (one wave per (query, group))
     const int64_t nw = (int64_t)f.nq * f.G;
     hipLaunchKernelGGL(group_shift_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, f.q, (int64_t)f.nq, f.D,
-                       f.c0, f.cent, f.G, f.sh, f.sh + nw);
+                       f.c0, f.cent, f.G, f.sh, f.sh + nw, nullptr);
   }
   const int64_t n = (int64_t)f.nq * f.NI;
   hipLaunchKernelGGL(internal_chain_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, f);

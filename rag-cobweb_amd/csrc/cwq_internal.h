@@ -165,6 +165,47 @@ struct IntFinishArgs {
   float* Plo; float* Phi; float* Pclo; float* Pchi;
 };
 hipError_t launch_internal_finish(const IntFinishArgs& f, hipStream_t s);
+
+// ---- group pruning for the Fast query on group-centred trees (cwq_prune.hip) ----
+// Per (query, group g): an upper bound KUB of every Fast key of the rows below the depth-1
+// node g, from the query's distance to the group centre.  Stage A computes
+// the exact internal pass only for each query's best group g* (argmax KUB); every other
+// (query, node) gets the sentinel prefix kPruneSent in the filters' tables (its rows can
+// never be candidates).  Once the filter's first threshold T[q] (<= tau_K) is known, stage
+// B computes the groups with KUB >= T[q]; the groups left are certified to hold no top-K row.
+constexpr float kPruneSent = -1e24f;   // the pruned prefix (any real prefix is > kPruneCut)
+constexpr float kPruneCut = -1e20f;
+struct GroupBound {   // per group, fp64 (cwq_api.hip build_prune)
+  double r;           // >= max |mu_a - c_g| over the group's members (internal nodes and rows)
+  double wmin, wmax;  // min / max per-dimension weight (A^2 or iv) over the members
+  double ldmin, ldabs;   // min logdet, max |logdet| over the members
+  double mmax;        // >= max |mu_a|
+  double iLmin, iLmax, Cmin, Cmax;   // usable rows: 1/L and C = invL * sum_{path, a != root} w_a + cw
+  int valid;          // the group has a usable row (else never relevant)
+  int pad_;
+};
+struct PruneArgs {
+  int nq, G, NI, DP, D;
+  int64_t ldS;                  // [nq][ldS] tables (S_int, P, Pg_lo, Pg_hi)
+  const float* X;               // the chunk's padded query slices (kXQ interleave)
+  const float* Ar; const float* Br;   // row-major fp32 A, B of the internal nodes [NI][DP]
+  const int* par_int; const float* w_int; const float* logdet_int;
+  const int* gint;              // pruning group of each internal node (-1: the root)
+  const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists
+  const GroupBound* gb;
+  const double* dist2;          // [nq][G] |x - c_g|^2 (group_shift_kernel)
+  float* S; float* P;           // [nq][ldS]
+  float* Plo; float* Phi;       // the filters' shifted prefix tables (group-centred rows)
+  const int* grp; const double* F; const double* sh;   // centring group, F, shifts + errors [2][nq][G]
+  int fillP;                    // also write the sentinel into P (anisotropic leaf rows read P)
+  float* kub;                   // [nq][G] key upper bounds (rounded up)
+  int* gstar;                   // [nq] best group (-1: none)
+  int2* pairs; int* ctr;        // stage B pair list; ctr[0] pair count, ctr[1..2] work counters
+};
+hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s);
+hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT, int cus, hipStream_t s);
+hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
+                                const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);
 hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
                          const float* lkey, int R, float* T2, hipStream_t s);
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
@@ -594,6 +635,9 @@ hipError_t launch_gather_rows_f32(const float* mean, int D, const int64_t* nodes
                                   hipStream_t s);
 hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c0,
                               const float* cent, const int* grp, double* root2, double* grp2, hipStream_t s);
+// sh [2][nq][G]: -2 x'.d_g and its error bound; dist2 (optional) [nq][G]: |x - c_g|^2 in fp64
+hipError_t launch_group_shift(const float* q, int nq, int D, const float* c0, const float* cent, int G, double* sh,
+                              double* dist2, hipStream_t s);
 hipError_t launch_group_prefixes(const float* q, int nq, int D, const float* c0, const float* cent, int G,
                                  const float* P, int64_t ldP, int NI, const int* grp, const double* F, const double* Fc,
                                  double* sh, float* Plo, float* Phi, float* Pclo, float* Pchi, hipStream_t s);

@@ -1445,6 +1445,9 @@ __global__ __launch_bounds__(256) void tile_prange_kernel(const float* __restric
     if (act) {
       const int p0 = max(T.par, w0), p1 = min(T.par_hi, w0 + span - 1);
       for (int p = p0; p <= p1; ++p) {
+        // a pruned parent (cwq_prune.hip: sentinel prefix) holds no candidate: it must not
+        // widen the range the other parents' rows are pretested with
+        if (s_hi[ql][p - w0] <= kPruneCut) continue;
         const float a = s_lo[ql][p - w0] * T.invL, b = s_hi[ql][p - w0] * T.invL;
         mn = fminf(mn, fminf(a, b));
         mx = fmaxf(mx, fmaxf(a, b));

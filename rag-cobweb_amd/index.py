@@ -178,6 +178,14 @@ class CobwebIndex:
                 "int8_pass": bool(int(out[2]) & 256),
                 "candidates": int(out[3]), "exact_reranks": int(out[4]), "sample_rows": int(out[5])}
 
+    def last_prune_stats(self):
+        """Group pruning of the last Fast call (cwq_last_prune_stats): whether the
+        index has it, the queries of the pruned chunk (0: not pruned), the (query, group)
+        pairs its stage B computed beyond each query's best group, and the group count."""
+        out = np.zeros(4, np.int64)
+        check(self._L.cwq_last_prune_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"available": bool(out[0]), "queries": int(out[1]), "extra_pairs": int(out[2]), "groups": int(out[3])}
+
     def last_categorize_stats(self):
         """How the last categorize call resolved its queries (cwq_last_stats after
         cwq_categorize): counting over the bottleneck order, heap replay, the two-level
