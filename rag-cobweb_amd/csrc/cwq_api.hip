@@ -139,6 +139,7 @@ struct cwq_index {
   // per-group bound constants.  prune_ctr: the last call's stage-B pair count (diagnostics).
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
+  int prn_max_chunks = 1;
   GroupBound* gbound = nullptr;
   const int* prune_ctr = nullptr;
   int64_t prune_nq = 0;
@@ -713,6 +714,8 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   std::vector<int> fillp(gptr.begin(), gptr.end() - 1);
   for (int i = 1; i < NI; ++i)
     if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
+  ix->prn_max_chunks = 1;
+  for (int g = 0; g < G; ++g) ix->prn_max_chunks = std::max(ix->prn_max_chunks, (gptr[g + 1] - gptr[g] + 63) / 64);
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
       (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)))
     return rc;
@@ -1157,6 +1160,7 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& p
   pa.gint = ix->prn_gint;
   pa.gi_ptr = ix->gi_ptr;
   pa.gi_nodes = ix->gi_nodes;
+  pa.max_chunks = ix->prn_max_chunks;
   pa.gb = ix->gbound;
   double* dist2 = b.take<double>((size_t)c.nq_pad * G);
   pa.dist2 = dist2;

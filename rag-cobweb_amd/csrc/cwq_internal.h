@@ -192,6 +192,7 @@ struct PruneArgs {
   const int* par_int; const float* w_int; const float* logdet_int;
   const int* gint;              // pruning group of each internal node (-1: the root)
   const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists
+  int max_chunks;               // max over groups of ceil(nodes / 64): tasks per pair
   const GroupBound* gb;
   const double* dist2;          // [nq][G] |x - c_g|^2 (group_shift_kernel)
   float* S; float* P;           // [nq][ldS]

@@ -28,6 +28,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "cwq_internal.h"
 
 namespace cwq {
@@ -205,27 +207,30 @@ __global__ void prune_pairs_kernel(const PruneArgs a, const float* __restrict__ 
   }
 }
 
-// The exact internal pass of (query, group) pairs: persistent workgroups claim pairs from
-// a counter (stage A: pair p = (p, g*(p)); B: the list), stage the query's slices in LDS,
-// and per chunk of 64 of the group's nodes form every (node, 16-dim slice) partial in
-// parallel -- exact_aniso_S's fma chain -- then one thread per node adds its partials in
-// slice order: the scan kernel's raw sums bit for bit.  Every workgroup leaves when the
-// counter passes the pair count.
+// The exact internal pass of (query, group) pairs: persistent workgroups claim (pair, chunk
+// of 64 of the group's nodes) tasks from a counter (stage A: pair p = (p, g*(p)); B: the
+// list), stage the query's slices in LDS, form every (node, 16-dim slice) partial of the
+// chunk in parallel -- exact_aniso_S's fma chain -- and one thread per node adds its
+// partials in slice order: the scan kernel's raw sums bit for bit.  A one-query call spreads
+// a group's chunks over as many workgroups.  Every workgroup leaves when the counter passes
+// the task count.
 constexpr int kPrThreads = 256, kPrChunk = 64;
 __global__ __launch_bounds__(kPrThreads) void prune_scan_kernel(const PruneArgs a, int stage_b, int* claim) {
   extern __shared__ float s_dyn[];
   const int NV16 = a.DP / 16, LDP = NV16 + 1;
   float* s_x = s_dyn;                  // [DP] the query's slices
   float* s_part = s_dyn + a.DP;        // [kPrChunk][LDP]
-  __shared__ int s_p;
+  __shared__ int s_t;
   const int tid = threadIdx.x;
-  const int npairs = stage_b ? a.ctr[0] : a.nq;
+  const int mc = a.max_chunks;
+  const int64_t ntask = (int64_t)(stage_b ? a.ctr[0] : a.nq) * mc;
   for (;;) {
-    if (tid == 0) s_p = atomicAdd(claim, 1);
+    if (tid == 0) s_t = atomicAdd(claim, 1);
     __syncthreads();
-    const int p = s_p;
+    const int t = s_t;
     __syncthreads();
-    if (p >= npairs) break;
+    if (t >= ntask) break;
+    const int p = t / mc, ch = t - p * mc;
     int q, g;
     if (stage_b) {
       const int2 pr = a.pairs[p];
@@ -236,45 +241,44 @@ __global__ __launch_bounds__(kPrThreads) void prune_scan_kernel(const PruneArgs 
       g = a.gstar[p];
     }
     if (g < 0) continue;
+    const int c0 = a.gi_ptr[g] + ch * kPrChunk, b1 = a.gi_ptr[g + 1];
+    if (c0 >= b1) continue;   // uniform over the workgroup
+    const int cnt = min(kPrChunk, b1 - c0);
     const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
     for (int d = tid; d < a.DP; d += kPrThreads) {
       const int v = d >> 4, j = d & 15;
       s_x[d] = xq[(size_t)v * kXQ * 16 + j];
     }
     __syncthreads();
-    const int b0 = a.gi_ptr[g], b1 = a.gi_ptr[g + 1];
-    for (int c0 = b0; c0 < b1; c0 += kPrChunk) {
-      const int cnt = min(kPrChunk, b1 - c0);
-      for (int it = tid; it < cnt * NV16; it += kPrThreads) {
-        const int e = it / NV16, v = it - e * NV16;
-        const int node = a.gi_nodes[c0 + e];
-        const float* __restrict__ ar = a.Ar + (size_t)node * a.DP + v * 16;
-        const float* __restrict__ br = a.Br + (size_t)node * a.DP + v * 16;
-        float4 a4[4], b4[4];
+    for (int it = tid; it < cnt * NV16; it += kPrThreads) {
+      const int e = it / NV16, v = it - e * NV16;
+      const int node = a.gi_nodes[c0 + e];
+      const float* __restrict__ ar = a.Ar + (size_t)node * a.DP + v * 16;
+      const float* __restrict__ br = a.Br + (size_t)node * a.DP + v * 16;
+      float4 a4[4], b4[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
-          b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
-        }
-        float part;
+      for (int j = 0; j < 4; ++j) {
+        a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
+        b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
+      }
+      float part;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float4 ta = a4[j >> 2], tb = b4[j >> 2];
-          const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
-          const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
-          const float t = fmaf(s_x[v * 16 + j], aj, -bj);
-          part = (j == 0) ? t * t : fmaf(t, t, part);
-        }
-        s_part[e * LDP + v] = part;
+      for (int j = 0; j < 16; ++j) {
+        const float4 ta = a4[j >> 2], tb = b4[j >> 2];
+        const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
+        const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
+        const float tt = fmaf(s_x[v * 16 + j], aj, -bj);
+        part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
       }
-      __syncthreads();
-      if (tid < cnt) {
-        float acc = 0.f;
-        for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
-        a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
-      }
-      __syncthreads();
+      s_part[e * LDP + v] = part;
     }
+    __syncthreads();
+    if (tid < cnt) {
+      float acc = 0.f;
+      for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+      a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
+    }
+    __syncthreads();
   }
 }
 
@@ -302,7 +306,7 @@ hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s) {
   if (a.nq <= 0) return hipSuccess;
   if (hipError_t e = hipMemsetAsync(a.ctr, 0, 4 * sizeof(int), s)) return e;
   hipLaunchKernelGGL(prune_bound_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, s, a);
-  const int wgs = std::max(1, std::min(a.nq, cus * 4));
+  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)a.nq * a.max_chunks, (int64_t)cus * 4));
   hipLaunchKernelGGL(prune_scan_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_scan_lds(a.DP), s, a, 0, a.ctr + 1);
   const int64_t n = (int64_t)a.nq * a.NI;
   hipLaunchKernelGGL(prune_prefix_all_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
@@ -314,9 +318,10 @@ hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT,
   if (a.nq <= 0 || a.G <= 0) return hipSuccess;
   const int64_t n = (int64_t)a.nq * a.G;
   hipLaunchKernelGGL(prune_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, T, ldT);
-  const int wgs = std::max(1, (int)std::min<int64_t>(n, (int64_t)cus * 4));
+  const int wgs = std::max(1, (int)std::min<int64_t>(n * a.max_chunks, (int64_t)cus * 4));
   hipLaunchKernelGGL(prune_scan_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_scan_lds(a.DP), s, a, 1, a.ctr + 2);
-  hipLaunchKernelGGL(prune_prefix_pairs_kernel, dim3((unsigned)wgs), dim3(256), 0, s, a, a.ctr + 3);
+  const int wgp = std::max(1, (int)std::min<int64_t>(n, (int64_t)cus * 4));
+  hipLaunchKernelGGL(prune_prefix_pairs_kernel, dim3((unsigned)wgp), dim3(256), 0, s, a, a.ctr + 3);
   return hipGetLastError();
 }
 

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--calls", type=int, default=300, help="one-query calls timed per leg")
     ap.add_argument("--basic-only", action="store_true", help="only the Basic legs (e.g. under rocprofv3)")
     ap.add_argument("--fast-only", action="store_true", help="only the Fast legs")
+    ap.add_argument("--ab-prune", action="store_true",
+                    help="run the Fast legs with group pruning off (CWQ_GROUP_PRUNE=0) and on, in one process")
     ap.add_argument("--legs", default="all",
                     help="comma list of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
     ap.add_argument("--save-struct", default=None,
@@ -102,7 +104,17 @@ def main():
     Q = torch.from_numpy(Qn).cuda()
     k = args.k
     if not args.basic_only:
-        fast_legs(args, w, ix, Q, Qn, pick, k)
+        if args.ab_prune:
+            for mode in ("0", None, "0", None):
+                if mode is None:
+                    os.environ.pop("CWQ_GROUP_PRUNE", None)
+                else:
+                    os.environ["CWQ_GROUP_PRUNE"] = mode
+                print(f"-- group pruning {'off' if mode else 'on'}", flush=True)
+                fast_legs(args, w, ix, Q, Qn, pick, k)
+            os.environ.pop("CWQ_GROUP_PRUNE", None)
+        else:
+            fast_legs(args, w, ix, Q, Qn, pick, k)
     if not args.fast_only:
         basic_legs(args, w, ix, Q, Qn, k)
     print("done", flush=True)
@@ -146,6 +158,7 @@ def fast_batch(args, ix, Q, pick, k, ids0, s0):
           f"fallback queries {st['fallback_queries']}; "
           f"perturbed passage ranked first {top1:.3f}", flush=True)
     print(f"  last call phases (HIP events, ms): " + ", ".join(f"{a} {b:.3f}" for a, b in tm.items()), flush=True)
+    print(f"  prune stats: {ix.last_prune_stats()}", flush=True)
 
 
 def fast_percall(args, ix, Q, k, ids0, nq):
