@@ -141,8 +141,8 @@ struct cwq_index {
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
   int prn_max_chunks = 1;
   GroupBound* gbound = nullptr;
-  const int* prune_ctr = nullptr;
-  int64_t prune_nq = 0;
+  int* prune_ctr = nullptr;     // device [8]: per chunk pair count + claim counters, [4] the call's pair total
+  int64_t prune_nq = 0;         // queries the last Fast call pruned (0: none)
   // internal-node bounds (hierarchical trees): bf16 operand rows, their RowF constants,
   // row-major fp32 A/B copies for the exact chain in final_kernel.  int_path (default):
   // the Fast filter reads the path prefix P of leaf parents only, so there is one row per
@@ -209,7 +209,6 @@ struct cwq_index {
   int reserve(size_t b) {
     if (b <= ws_size) return CWQ_OK;
     if (ws_ev_live) (void)hipEventSynchronize(ws_ev);   // earlier calls' kernels may still read it
-    prune_ctr = nullptr;
     if (ws) (void)hipFree(ws);
     ws = nullptr;
     ws_size = 0;
@@ -288,7 +287,6 @@ struct WsUse {
   hipStream_t s;
   int rc;
   WsUse(cwq_index* i, hipStream_t st) : ix(i), s(st) {
-    ix->prune_ctr = nullptr;   // a pointer into the workspace: valid until the next call
     rc = ix->ws_begin(s);
   }
   ~WsUse() {
@@ -717,8 +715,10 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   ix->prn_max_chunks = 1;
   for (int g = 0; g < G; ++g) ix->prn_max_chunks = std::max(ix->prn_max_chunks, (gptr[g + 1] - gptr[g] + 63) / 64);
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
-      (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)))
+      (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)) ||
+      (rc = ix->alloc(&ix->prune_ctr, 8)))
     return rc;
+  HIPCHK(hipMemsetAsync(ix->prune_ctr, 0, 8 * sizeof(int), s));
   HIPCHK(hipStreamSynchronize(s));
   ix->prune_ok = true;
   return CWQ_OK;
@@ -1175,13 +1175,12 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& p
   pa.kub = b.take<float>((size_t)c.nq_pad * G);
   pa.gstar = b.take<int>((size_t)c.nq_pad);
   pa.pairs = b.take<int2>((size_t)c.nq_pad * G);
-  pa.ctr = b.take<int>(64);
+  pa.ctr = ix->prune_ctr;   // the handle's (calls on it are serialised): [4] survives a fallback re-run
   HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, nq, c.S_int, ix->NI, s));   // the root
   HIPCHK(launch_group_shift(q, nq, ix->D, ix->iso_c, ix->grp_c, G, c.gsh, dist2, s));
-  HIPCHK(launch_prune_stage_a(pa, ix->cus, s));
+  HIPCHK(launch_prune_stage_a(pa, ix->cus, s, ix->prune_nq == 0));   // the call's first pruned chunk: total reset
   c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
-  ix->prune_ctr = pa.ctr;
-  ix->prune_nq = nq;
+  ix->prune_nq += nq;
   return CWQ_OK;
 }
 
@@ -2381,13 +2380,13 @@ extern "C" int cwq_last_prune_stats(cwq_index* ix, int64_t* out) {
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   out[0] = ix->prune_ok ? 1 : 0;
-  out[1] = ix->prune_ctr ? ix->prune_nq : 0;
+  out[1] = ix->prune_nq;
   out[2] = 0;
   out[3] = ix->G;
-  if (ix->prune_ctr) {
+  if (ix->prune_ctr && ix->prune_nq > 0) {
     int v = 0;
     if (ix->ws_ev_live) HIPCHK(hipEventSynchronize(ix->ws_ev));
-    HIPCHK(hipMemcpy(&v, ix->prune_ctr, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&v, ix->prune_ctr + 4, sizeof(int), hipMemcpyDeviceToHost));
     out[2] = v;
   }
   return CWQ_OK;

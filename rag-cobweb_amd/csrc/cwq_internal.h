@@ -201,9 +201,9 @@ struct PruneArgs {
   int fillP;                    // also write the sentinel into P (anisotropic leaf rows read P)
   float* kub;                   // [nq][G] key upper bounds (rounded up)
   int* gstar;                   // [nq] best group (-1: none)
-  int2* pairs; int* ctr;        // stage B pair list; ctr[0] pair count, ctr[1..2] work counters
+  int2* pairs; int* ctr;        // stage B pair list; ctr[0] pair count, [1..3] claim counters, [4] call total
 };
-hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s);
+hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s, bool first);
 hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT, int cus, hipStream_t s);
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
                                 const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);

@@ -204,6 +204,7 @@ __global__ void prune_pairs_kernel(const PruneArgs a, const float* __restrict__ 
   if (a.kub[t] >= Tq || !(Tq == Tq)) {
     const int j = atomicAdd(&a.ctr[0], 1);
     a.pairs[j] = make_int2(q, g);
+    atomicAdd(&a.ctr[4], 1);   // the call's total (diagnostics)
   }
 }
 
@@ -300,11 +301,12 @@ __global__ __launch_bounds__(256) void prune_prefix_pairs_kernel(const PruneArgs
 
 size_t prune_scan_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
 
-// Stage A: group shifts and distances, the root's raw sum (the caller's exact root pass has
-// written S[q][0]), bounds and g*, the exact pass of g*, the tables.  ctr: 4 ints, zeroed here.
-hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s) {
+// Stage A: bounds and g* (the caller has written the root's raw sums S[q][0] and the group
+// shifts and distances), the exact pass of g*, the tables.  ctr[0..3] zeroed here, and
+// ctr[4] (the call's stage-B pair total) on the call's first pruned chunk.
+hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s, bool first) {
   if (a.nq <= 0) return hipSuccess;
-  if (hipError_t e = hipMemsetAsync(a.ctr, 0, 4 * sizeof(int), s)) return e;
+  if (hipError_t e = hipMemsetAsync(a.ctr, 0, (first ? 5 : 4) * sizeof(int), s)) return e;
   hipLaunchKernelGGL(prune_bound_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, s, a);
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)a.nq * a.max_chunks, (int64_t)cus * 4));
   hipLaunchKernelGGL(prune_scan_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_scan_lds(a.DP), s, a, 0, a.ctr + 1);
