@@ -1186,6 +1186,45 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& p
 
 int prune_stage_b(cwq_index* ix, const PruneArgs& pa, const float* T, int64_t ldT, hipStream_t s) {
   HIPCHK(launch_prune_stage_b(pa, T, ldT, ix->cus, s));
+  if (getenv("CWQ_PRUNE_DEBUG")) {   // diagnostics: the first queries' bounds and thresholds
+    const int nq = std::min(pa.nq, 3), G = pa.G;
+    std::vector<float> kub((size_t)nq * G), th(nq), S0(nq);
+    std::vector<int> gs(nq), ctr(8);
+    std::vector<GroupBound> gb(G);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(kub.data(), pa.kub, kub.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(gs.data(), pa.gstar, nq * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ctr.data(), pa.ctr, 32, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(gb.data(), pa.gb, G * sizeof(GroupBound), hipMemcpyDeviceToHost));
+    for (int i = 0; i < nq; ++i) {
+      HIPCHK(hipMemcpy(&th[i], T + (size_t)i * ldT, 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&S0[i], pa.S + (size_t)i * pa.ldS, 4, hipMemcpyDeviceToHost));
+    }
+    std::vector<double> d2((size_t)nq * G);
+    HIPCHK(hipMemcpy(d2.data(), pa.dist2, d2.size() * 8, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[prune] nq %d G %d pairs %d total %d\n", pa.nq, G, ctr[0], ctr[4]);
+    for (int i = 0; i < nq; ++i) {
+      float mx = -INFINITY, mn = INFINITY;
+      for (int g = 0; g < G; ++g)
+        if (g != gs[i]) {
+          mx = std::max(mx, kub[(size_t)i * G + g]);
+          mn = std::min(mn, kub[(size_t)i * G + g]);
+        }
+      const int g = gs[i];
+      fprintf(stderr, "[prune] q %d S0 %g T %g g* %d kub* %g others [%g, %g]\n", i, S0[i], th[i], g,
+              g >= 0 ? kub[(size_t)i * G + g] : NAN, mn, mx);
+      if (g >= 0) {
+        const GroupBound& b = gb[g];
+        fprintf(stderr, "[prune]   g* r %g wmin %g wmax %g ldmin %g ldabs %g mmax %g iL [%g %g] C [%g %g] dist2 %g\n",
+                b.r, b.wmin, b.wmax, b.ldmin, b.ldabs, b.mmax, b.iLmin, b.iLmax, b.Cmin, b.Cmax, d2[(size_t)i * G + g]);
+        const int o = (g + 1) % G;
+        const GroupBound& c = gb[o];
+        fprintf(stderr, "[prune]   g %d r %g wmin %g wmax %g ldmin %g ldabs %g mmax %g iL [%g %g] C [%g %g] dist2 %g kub %g\n",
+                o, c.r, c.wmin, c.wmax, c.ldmin, c.ldabs, c.mmax, c.iLmin, c.iLmax, c.Cmin, c.Cmax,
+                d2[(size_t)i * G + o], kub[(size_t)i * G + o]);
+      }
+    }
+  }
   return CWQ_OK;
 }
 
