@@ -140,6 +140,7 @@ struct cwq_index {
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
   int prn_max_chunks = 1;
+  int *gs_ptr = nullptr, *gs_rows = nullptr;   // per group: up to 64 usable isotropic rows (the seed threshold)
   GroupBound* gbound = nullptr;
   int* prune_ctr = nullptr;     // device [8]: per chunk pair count + claim counters, [4] the call's pair total
   int64_t prune_nq = 0;         // queries the last Fast call pruned (0: none)
@@ -714,6 +715,18 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
   ix->prn_max_chunks = 1;
   for (int g = 0; g < G; ++g) ix->prn_max_chunks = std::max(ix->prn_max_chunks, (gptr[g + 1] - gptr[g] + 63) / 64);
+  // the seed threshold's rows: up to 64 usable isotropic rows of each group, spread over it
+  std::vector<std::vector<int>> grows(G);
+  for (int r = 0; r < ix->NL_iso; ++r)
+    if (rgrp[r] >= 0 && (row_flags[r] & FLAG_HAS_SENT)) grows[rgrp[r]].push_back(r);
+  std::vector<int> sptr2(G + 1, 0), srows2;
+  for (int g = 0; g < G; ++g) {
+    const int n = (int)grows[g].size(), m = std::min(n, 64);
+    for (int j = 0; j < m; ++j) srows2.push_back(grows[g][(int64_t)j * n / m]);
+    sptr2[g + 1] = (int)srows2.size();
+  }
+  if (srows2.empty()) srows2.push_back(0);
+  if ((rc = ix->upload(&ix->gs_ptr, sptr2, s)) || (rc = ix->upload(&ix->gs_rows, srows2, s))) return rc;
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
       (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)) ||
       (rc = ix->alloc(&ix->prune_ctr, 8)))
@@ -1139,11 +1152,14 @@ bool use_prune(const cwq_index* ix) {
 }
 size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 20 + 16 : 0; }
 
-// Stage A of the pruned Fast chunk, in place of run_internal + group_tables: the root's raw
-// sums, the group shifts and distances, KUB and g*, the exact pass of g*, the tables.  The
-// caller runs prune_stage_b once the filter's first threshold is on the device.
-int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& pa, hipStream_t s) {
+// The pruned Fast chunk's internal pass, in place of run_internal + group_tables: the root's
+// raw sums, the group shifts and distances, KUB and g*, the exact pass of g* and its
+// tables (stage A); the seed threshold from g*'s sample rows; then stage B: the groups
+// whose bound reaches it.  K: the call's top-K.
+int prune_stage_b(cwq_index* ix, const PruneArgs& pa, const float* T, int64_t ldT, hipStream_t s);
+int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, PruneArgs& pa, hipStream_t s) {
   const int nq = c.nq, G = ix->G;
+  int rc;
   memset(&pa, 0, sizeof(pa));
   pa.nq = nq;
   pa.G = G;
@@ -1179,6 +1195,11 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, Bump& b, PruneArgs& p
   HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, nq, c.S_int, ix->NI, s));   // the root
   HIPCHK(launch_group_shift(q, nq, ix->D, ix->iso_c, ix->grp_c, G, c.gsh, dist2, s));
   HIPCHK(launch_prune_stage_a(pa, ix->cus, s, ix->prune_nq == 0));   // the call's first pruned chunk: total reset
+  // the seed threshold from g*'s sample rows (exact keys), then stage B
+  float* Tseed = b.take<float>((size_t)c.nq_pad);
+  HIPCHK(launch_prune_seed(c.X, ix->iso_Mf, ix->DP, nq, K, pa.gstar, ix->gs_ptr, ix->gs_rows, ix->row_meta, ix->row_par,
+                           c.P, ix->NI, Tseed, s));
+  if ((rc = prune_stage_b(ix, pa, Tseed, 1, s))) return rc;
   c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
   ix->prune_nq += nq;
   return CWQ_OK;
@@ -1904,7 +1925,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
     } else if (prn) {
-      if ((rc = prune_stage_a(ix, c, q, b, pra, s))) return rc;
+      if ((rc = prune_stage_a(ix, c, q, K, b, pra, s))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q, 0))) {
       return rc;
     }
@@ -1995,7 +2016,6 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.sel_ctr = nullptr;
   a.fprep = 0;
   if (!fsel) HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
-  if (prn && (rc = prune_stage_b(ix, pra, tl + (K - 1), 64, s))) return rc;   // the groups T0 cannot exclude
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
   if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)
     StreamArgs a8 = a;
@@ -2076,7 +2096,7 @@ size_t iso_filter_bytes_per_query(const cwq_index* ix, int n_rt) {
 }
 
 int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int K, bool cat, bool ib, Bump& b,
-                   IsoFilter& o, hipStream_t s, const PruneArgs* prune = nullptr) {
+                   IsoFilter& o, hipStream_t s) {
   const int nqc = c.nq;
   const int n_rt = (int)(ix->ld_f / kFgTile);
   const int n_rts = ix->ld_s / kFgTile;
@@ -2156,12 +2176,7 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.ldlb = ix->ld_s / g.lbg;
   HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
   HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
-  if (prune) {   // group pruning: the groups whose key bound reaches the threshold (stage B)
-    int rc;
-    if ((rc = prune_stage_b(ix, *prune, tl + (K - 1), 64, s))) return rc;
-    if (pmm)   // the multi-parent tiles' prefix ranges again, with stage B's tables
-      HIPCHK(launch_tile_prange(c.Pg_lo, c.Pg_hi, c.ldP, c.pT, nqc, ix->iso_tf, n_rt, pmm, nqf, s, &pb));
-  }
+
   // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
   // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is
   // raised to the K-th largest candidate lower bound, so later phases emit fewer
@@ -2277,7 +2292,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q + q0 * ix->D, nqf, b, s))) return rc;
     } else if (prn) {
-      if ((rc = prune_stage_a(ix, c, q + q0 * ix->D, b, pra, s))) return rc;
+      if ((rc = prune_stage_a(ix, c, q + q0 * ix->D, K, b, pra, s))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q + q0 * ix->D, filt ? 0 : -1))) {
       return rc;
     }
@@ -2294,7 +2309,7 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
         // isotropic rows: sample bounds -> thresholds -> MFMA filter -> candidates ->
         // exact rerank into list slot 0; anisotropic rows: exact scan into slots 1..
         IsoFilter fo;
-        if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, K, false, ib, b, fo, s, prn ? &pra : nullptr))) return rc;
+        if ((rc = run_iso_filter(ix, c, q + q0 * ix->D, nqf, K, false, ib, b, fo, s))) return rc;
         int* qcnt = fo.qcnt;
         int* nex = fo.nex;
         okf = fo.okf;

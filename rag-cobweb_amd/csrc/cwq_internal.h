@@ -205,6 +205,9 @@ struct PruneArgs {
 };
 hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s, bool first);
 hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT, int cus, hipStream_t s);
+hipError_t launch_prune_seed(const float* X, const float* Mf, int DP, int nq, int K, const int* gstar,
+                             const int* gs_ptr, const int* gs_rows, const RowMeta* meta, const int* par,
+                             const float* P, int64_t ldP, float* T, hipStream_t s);   // cwq_mfma.hip
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
                                 const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);
 hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
