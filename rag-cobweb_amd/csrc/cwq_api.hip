@@ -1129,6 +1129,7 @@ struct Chunk {
   // [Pg_lo, Pg_hi] and categorize [Pc_lo, Pc_hi] -- and the per-(query, group) shifts
   float *Pg_lo = nullptr, *Pg_hi = nullptr, *Pc_lo = nullptr, *Pc_hi = nullptr;
   double* gsh = nullptr;
+  float* Tseed = nullptr;   // group pruning's seed threshold [nq] (a lower bound of tau_K), or none
   int grp_done = -1;   // the group tables run_internal's fused pass wrote: -1 none, 0 Fast, 1 + categorize
 };
 
@@ -1196,10 +1197,10 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, Prune
   HIPCHK(launch_group_shift(q, nq, ix->D, ix->iso_c, ix->grp_c, G, c.gsh, dist2, s));
   HIPCHK(launch_prune_stage_a(pa, ix->cus, s, ix->prune_nq == 0));   // the call's first pruned chunk: total reset
   // the seed threshold from g*'s sample rows (exact keys), then stage B
-  float* Tseed = b.take<float>((size_t)c.nq_pad);
+  c.Tseed = b.take<float>((size_t)c.nq_pad);
   HIPCHK(launch_prune_seed(c.X, ix->iso_Mf, ix->DP, nq, K, pa.gstar, ix->gs_ptr, ix->gs_rows, ix->row_meta, ix->row_par,
-                           c.P, ix->NI, Tseed, s));
-  if ((rc = prune_stage_b(ix, pa, Tseed, 1, s))) return rc;
+                           c.P, ix->NI, c.Tseed, s));
+  if ((rc = prune_stage_b(ix, pa, c.Tseed, 1, s))) return rc;
   c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
   ix->prune_nq += nq;
   return CWQ_OK;
@@ -1994,6 +1995,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     a.sel_ctr = fprep ? ix->sel_ctr : sel_ctr;
     a.sel_lk = tl;
     a.sel_lr = tr;
+    a.sel_floor = c.Tseed;   // group pruning: the probe saw only the groups kept
   }
   if (fprep) {
     a.fprep = 1;
@@ -2014,8 +2016,12 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   }
   HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
   a.sel_ctr = nullptr;
+  a.sel_floor = nullptr;
   a.fprep = 0;
-  if (!fsel) HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
+  if (!fsel) {
+    HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
+    if (c.Tseed) HIPCHK(launch_raise_threshold(tl + (K - 1), 64, c.Tseed, nqc, s));
+  }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[5], s));
   if (i8) {   // the filter pass over the int8 panel (the probe above: bf16, a tighter T0)
     StreamArgs a8 = a;
@@ -2176,6 +2182,8 @@ int run_iso_filter(cwq_index* ix, Chunk& c, const float* qsrc, int64_t nqf, int 
   g.ldlb = ix->ld_s / g.lbg;
   HIPCHK(launch_fgemm(Xb, ix->iso_Sb, g, ix->cus, s));
   HIPCHK(launch_select(lb, g.ldlb, nqc, (int)g.ldlb, K, tl, tr, s));
+  // group pruning: the sample saw only the groups kept; its seed threshold is a floor
+  if (!cat && c.Tseed) HIPCHK(launch_raise_threshold(tl + (K - 1), 64, c.Tseed, nqc, s));
 
   // 2. filter launches over row-tile phases (fg_phase_cuts: 1/32, 2/32, 5/32, 8/32,
   // 16/32 of the tiles); after each the candidates go to per-query lists and T[q] is

@@ -208,6 +208,7 @@ hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT,
 hipError_t launch_prune_seed(const float* X, const float* Mf, int DP, int nq, int K, const int* gstar,
                              const int* gs_ptr, const int* gs_rows, const RowMeta* meta, const int* par,
                              const float* P, int64_t ldP, float* T, hipStream_t s);   // cwq_mfma.hip
+hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s);
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
                                 const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);
 hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI, int nq, const int* par_int,
@@ -611,6 +612,7 @@ struct StreamArgs {
   int* sel_ctr;
   float* sel_lk;
   int* sel_lr;
+  const float* sel_floor;      // optional [nq]: the K-th entry written is max(it, floor) (group pruning's seed)
   // probe with the query prep fused (flat trees, nq <= 16, bf16; fprep set): every workgroup
   // forms the bf16 query fragments, the {|x'|^2, |x_hi|, |x_lo|} terms and the root's exact
   // prefix itself (sb_prep_kernel's arithmetic), and workgroup 0 also writes them to Xb /

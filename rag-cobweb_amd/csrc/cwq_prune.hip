@@ -299,6 +299,19 @@ __global__ __launch_bounds__(256) void prune_prefix_pairs_kernel(const PruneArgs
   }
 }
 
+// T[q * ldT] = max(T, Tfloor[q]) (both lower bounds of tau_K; the filter's sample / probe
+// threshold sees only the groups pruning kept, the seed only the best group's sample rows).
+__global__ void raise_threshold_kernel(float* T, int64_t ldT, const float* __restrict__ Tfloor, int nq) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq) T[(size_t)q * ldT] = fmaxf(T[(size_t)q * ldT], Tfloor[q]);
+}
+
+hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(raise_threshold_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, T, ldT, Tfloor, nq);
+  return hipGetLastError();
+}
+
 size_t prune_scan_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
 
 // Stage A: bounds and g* (the caller has written the root's raw sums S[q][0] and the group

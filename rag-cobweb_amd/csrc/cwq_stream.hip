@@ -442,6 +442,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         float lk;
         int lr;
         select_wave(a.lb + (size_t)q * a.ldlb, (int)a.n_probe, a.K, lane, lk, lr);
+        if (a.sel_floor && lane == a.K - 1) lk = fmaxf(lk, a.sel_floor[q]);
         a.sel_lk[(size_t)q * 64 + lane] = lk;
         a.sel_lr[(size_t)q * 64 + lane] = lr;
       }
