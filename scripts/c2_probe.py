@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--ab-prune", action="store_true",
                     help="run the Fast legs with group pruning off (CWQ_GROUP_PRUNE=0) and on, in one process")
     ap.add_argument("--legs", default="all",
-                    help="comma list of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
+                    help="list (comma or +) of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
     ap.add_argument("--save-struct", default=None,
                     help="write the ifit tree's structure (BFS parent, node of each row) to this .npz")
     ap.add_argument("--load-struct", default=None,
@@ -121,7 +121,7 @@ def main():
 
 
 def want(args, leg):
-    return args.legs == "all" or leg in args.legs.split(",")
+    return args.legs == "all" or leg in args.legs.replace("+", ",").split(",")
 
 
 def fast_legs(args, w, ix, Q, Qn, pick, k):
