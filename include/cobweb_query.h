@@ -207,6 +207,15 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  * bottleneck tie].
  */
 int cwq_set_filter(cwq_index* idx, int mode);
+/*
+ * cwq_score_topk with host memory on both sides: q (host [nq*dim]) in, ids (host [nq*k])
+ * and scores (host [nq*k] or NULL) out; returns synchronized.  The reference harness's
+ * timed call shape (benchmark_utils.py:801-805: cobweb_predict_fast on a numpy embedding,
+ * CobwebWrapper.py:428-433 -> :210-265).  Same results as cwq_score_topk.
+ */
+int cwq_score_topk_host(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                        void* stream);
+
 int cwq_last_stats(cwq_index* idx, int64_t* out6);
 
 /*

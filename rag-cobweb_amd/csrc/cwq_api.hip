@@ -183,6 +183,13 @@ struct cwq_index {
   bool ws_idle = false;   // set by a call that ends with its stream synchronized: no event needed
   int* hflags = nullptr;   // pinned host copy of the per-query filter flags (one D2H per chunk)
   size_t hflags_n = 0;
+  // cwq_score_topk_host: pinned staging of the host queries, their device copy, and mapped
+  // (coherent) host memory the kernels write the results into
+  void* hq = nullptr;
+  void* dq = nullptr;
+  size_t hq_n = 0;
+  void* hout = nullptr;
+  size_t hout_n = 0;
   // fallback re-runs (cwq_score_topk / cwq_categorize): gathered queries, their results
   // and the device index lists, kept between calls (grown on demand)
   void* fb = nullptr;
@@ -267,6 +274,31 @@ struct cwq_index {
     if (fb) (void)hipFree(fb);
     if (fb2) (void)hipFree(fb2);
     if (hflags) (void)hipHostFree(hflags);
+    if (hq) (void)hipHostFree(hq);
+    if (dq) (void)hipFree(dq);
+    if (hout) (void)hipHostFree(hout);
+  }
+  int host_io(size_t qbytes, size_t obytes) {
+    if (qbytes > hq_n) {
+      if (hq) (void)hipHostFree(hq);
+      if (dq) (void)hipFree(dq);
+      hq = dq = nullptr;
+      hq_n = 0;
+      const size_t b = (size_t)round_up((int64_t)qbytes, 1 << 16);
+      if (hipHostMalloc(&hq, b, hipHostMallocDefault) != hipSuccess || hipMalloc(&dq, b) != hipSuccess)
+        return fail(CWQ_ERR_OOM, "host query staging allocation failed");
+      hq_n = b;
+    }
+    if (obytes > hout_n) {
+      if (hout) (void)hipHostFree(hout);
+      hout = nullptr;
+      hout_n = 0;
+      const size_t b = (size_t)round_up((int64_t)obytes, 1 << 16);
+      if (hipHostMalloc(&hout, b, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(CWQ_ERR_OOM, "host result buffer allocation failed");
+      hout_n = b;
+    }
+    return CWQ_OK;
   }
   int host_flags(size_t n) {
     if (n <= hflags_n) return CWQ_OK;
@@ -2422,6 +2454,40 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
   return score_topk_impl(ix, q, nq, k, ids, scores, s, true);
+}
+
+// The reference harness's call with host memory on both sides (benchmark_utils.py:801-805:
+// a numpy query in, sentence ids out): the query is copied into pinned staging and sent with
+// one async copy, the kernels write the ids / scores straight into mapped host memory, and
+// the call returns synchronized -- no torch tensors, no device allocations, no separate
+// device-to-host copy per call.
+extern "C" int cwq_score_topk_host(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
+                                   void* stream) {
+  if (!ix || (!q && nq > 0) || (!ids && nq > 0)) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  for (float& t : ix->t_ms) t = 0.f;
+  for (int64_t& t : ix->stats) t = 0;
+  ix->prune_nq = 0;
+  hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
+  if (wu.rc) return wu.rc;
+  const size_t qb = (size_t)nq * ix->D * 4, ib = (size_t)round_up(nq * k * 8, 256), sb = (size_t)nq * k * 4;
+  int rc;
+  if ((rc = ix->host_io(qb, ib + sb))) return rc;
+  memcpy(ix->hq, q, qb);
+  HIPCHK(hipMemcpyAsync(ix->dq, ix->hq, qb, hipMemcpyHostToDevice, s));
+  int64_t* hid = (int64_t*)ix->hout;
+  float* hsc = (float*)((char*)ix->hout + ib);
+  if ((rc = score_topk_impl(ix, (const float*)ix->dq, nq, k, hid, hsc, s, true))) return rc;
+  HIPCHK(sync_spin(s));
+  ix->ws_idle = true;   // synchronized
+  memcpy(ids, hid, (size_t)nq * k * 8);
+  if (scores) memcpy(scores, hsc, sb);
+  return CWQ_OK;
 }
 
 extern "C" int cwq_set_filter(cwq_index* ix, int mode) {

@@ -231,6 +231,22 @@ class CobwebIndex:
                                      _stream_raw(self.device.index)))
         return ids, scores
 
+    def score_topk_host(self, q, k):
+        """score_topk for a host (numpy) query batch -> numpy (ids [nq, k] int64, scores [nq, k]
+        float32), the reference harness's call shape (cwq_score_topk_host: pinned staging in,
+        the kernels write the results into mapped host memory; no torch tensors per call)."""
+        q = np.ascontiguousarray(np.asarray(q, dtype=np.float32))
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be [nq, {self.dim}]")
+        nq, k = q.shape[0], int(k)
+        ids = np.empty((nq, k), np.int64)
+        scores = np.empty((nq, k), np.float32)
+        check(self._L.cwq_score_topk_host(self._h, q.ctypes.data, nq, k, ids.ctypes.data, scores.ctypes.data,
+                                          _stream_raw(self.device.index)))
+        return ids, scores
+
     def rank_scores(self, q):
         """All sentence scores (A8), [nq, n_sent]."""
         q = self._queries(q)

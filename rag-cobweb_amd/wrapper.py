@@ -251,13 +251,18 @@ class CobwebWrapper:
     def cobweb_predict_indexed(self, input, k=5, return_ids=False, is_embedding=False):
         """CobwebWrapper.py:210-265 ("Cobweb Fast")."""
         self.build_prediction_index()
-        x = self._embed(input, is_embedding)
         n = self._index.n_sent if self._leaf_to_path_indices is None else len(self._leaf_to_path_indices)
         if n == 0:
             return []
-        ids, _ = self._index.score_topk(x[None, :], min(k, n))
+        emb = input if is_embedding else self.encode_func([input])[0]
+        if not torch.is_tensor(emb):
+            # a host embedding (the harness's numpy query): host memory in and out
+            ids, _ = self._index.score_topk_host(np.asarray(emb, dtype=np.float32).reshape(1, -1), min(k, n))
+        else:
+            ids, _ = self._index.score_topk(self._embed(emb, True)[None, :], min(k, n))
+        row = ids[0].tolist()
         out = []
-        for s in ids[0].tolist():
+        for s in row:
             if 0 <= s < len(self.sentences):
                 out.append(s if return_ids else self.sentences[s])
         return out
