@@ -1183,24 +1183,29 @@ bool use_prune(const cwq_index* ix) {
   const char* e = getenv("CWQ_GROUP_PRUNE");
   return !(e && *e && atoi(e) == 0);
 }
-size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 20 + 16 : 0; }
+size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 28 + 16 : 0; }
 
-// The pruned Fast chunk's internal pass, in place of run_internal + group_tables: the root's
-// raw sums, the group shifts and distances, KUB and g*, the exact pass of g* and its
-// tables (stage A); the seed threshold from g*'s sample rows; then stage B: the groups
-// whose bound reaches it.  K: the call's top-K.
-int prune_stage_b(cwq_index* ix, const PruneArgs& pa, const float* T, int64_t ldT, hipStream_t s);
-int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, PruneArgs& pa, hipStream_t s) {
+// The pruned Fast chunk's internal pass, in place of run_internal + group_tables (four
+// launches, cwq_prune.hip): the group shifts and the bound terms; the root, KUB, g* and g*'s
+// exact pass and tables (stage A); the seed threshold from g*'s sample rows, the stage-B
+// pairs and the sentinel fill; stage B.  K: the call's top-K.  T0 (optional): the seed is
+// also written there (the per-call filter's threshold: no probe pass).
+int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipStream_t s, float* T0 = nullptr,
+                   int64_t ldT0 = 0) {
   const int nq = c.nq, G = ix->G;
-  int rc;
+  PruneArgs pa;
   memset(&pa, 0, sizeof(pa));
   pa.nq = nq;
   pa.G = G;
   pa.NI = ix->NI;
   pa.DP = ix->DP;
   pa.D = ix->D;
+  pa.K = K;
   pa.ldS = ix->NI;
+  pa.q = q;
   pa.X = c.X;
+  pa.c0 = ix->iso_c;
+  pa.cent = ix->grp_c;
   pa.Ar = ix->int_Ar;
   pa.Br = ix->int_Br;
   pa.par_int = ix->par_int;
@@ -1209,10 +1214,8 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, Prune
   pa.gint = ix->prn_gint;
   pa.gi_ptr = ix->gi_ptr;
   pa.gi_nodes = ix->gi_nodes;
-  pa.max_chunks = ix->prn_max_chunks;
   pa.gb = ix->gbound;
-  double* dist2 = b.take<double>((size_t)c.nq_pad * G);
-  pa.dist2 = dist2;
+  pa.kpart = b.take<double>((size_t)2 * c.nq_pad * G);
   pa.S = c.S_int;
   pa.P = c.P;
   pa.Plo = c.Pg_lo;
@@ -1225,60 +1228,36 @@ int prune_stage_a(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, Prune
   pa.gstar = b.take<int>((size_t)c.nq_pad);
   pa.pairs = b.take<int2>((size_t)c.nq_pad * G);
   pa.ctr = ix->prune_ctr;   // the handle's (calls on it are serialised): [4] survives a fallback re-run
-  HIPCHK(launch_int_small(c.X, ix->int_A, ix->int_B, ix->ld_int, 1, ix->DP, nq, c.S_int, ix->NI, s));   // the root
-  HIPCHK(launch_group_shift(q, nq, ix->D, ix->iso_c, ix->grp_c, G, c.gsh, dist2, s));
-  HIPCHK(launch_prune_stage_a(pa, ix->cus, s, ix->prune_nq == 0));   // the call's first pruned chunk: total reset
-  // the seed threshold from g*'s sample rows (exact keys), then stage B
+  pa.gs_ptr = ix->gs_ptr;
+  pa.gs_rows = ix->gs_rows;
+  pa.Mf = ix->iso_Mf;
+  pa.meta = ix->row_meta;
+  pa.row_par = ix->row_par;
   c.Tseed = b.take<float>((size_t)c.nq_pad);
-  HIPCHK(launch_prune_seed(c.X, ix->iso_Mf, ix->DP, nq, K, pa.gstar, ix->gs_ptr, ix->gs_rows, ix->row_meta, ix->row_par,
-                           c.P, ix->NI, c.Tseed, s));
-  if ((rc = prune_stage_b(ix, pa, c.Tseed, 1, s))) return rc;
-  c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
-  ix->prune_nq += nq;
-  return CWQ_OK;
-}
-
-int prune_stage_b(cwq_index* ix, const PruneArgs& pa, const float* T, int64_t ldT, hipStream_t s) {
-  HIPCHK(launch_prune_stage_b(pa, T, ldT, ix->cus, s));
+  pa.Tseed = c.Tseed;
+  pa.T0 = T0;
+  pa.ldT0 = ldT0;
+  HIPCHK(launch_prune(pa, ix->cus, ix->prune_nq == 0, s));   // the call's first pruned chunk resets the total
   if (getenv("CWQ_PRUNE_DEBUG")) {   // diagnostics: the first queries' bounds and thresholds
-    const int nq = std::min(pa.nq, 3), G = pa.G;
-    std::vector<float> kub((size_t)nq * G), th(nq), S0(nq);
-    std::vector<int> gs(nq), ctr(8);
-    std::vector<GroupBound> gb(G);
+    const int n = std::min(nq, 3);
+    std::vector<float> kub((size_t)n * G), th(n);
+    std::vector<int> gs(n), ctr(8);
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipMemcpy(kub.data(), pa.kub, kub.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(gs.data(), pa.gstar, nq * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(gs.data(), pa.gstar, n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(ctr.data(), pa.ctr, 32, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(gb.data(), pa.gb, G * sizeof(GroupBound), hipMemcpyDeviceToHost));
-    for (int i = 0; i < nq; ++i) {
-      HIPCHK(hipMemcpy(&th[i], T + (size_t)i * ldT, 4, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(&S0[i], pa.S + (size_t)i * pa.ldS, 4, hipMemcpyDeviceToHost));
-    }
-    std::vector<double> d2((size_t)nq * G);
-    HIPCHK(hipMemcpy(d2.data(), pa.dist2, d2.size() * 8, hipMemcpyDeviceToHost));
-    fprintf(stderr, "[prune] nq %d G %d pairs %d total %d\n", pa.nq, G, ctr[0], ctr[4]);
-    for (int i = 0; i < nq; ++i) {
-      float mx = -INFINITY, mn = INFINITY;
+    HIPCHK(hipMemcpy(th.data(), pa.Tseed, n * 4, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[prune] nq %d G %d pairs %d total %d\n", nq, G, ctr[0], ctr[4]);
+    for (int i = 0; i < n; ++i) {
+      float mx = -INFINITY;
       for (int g = 0; g < G; ++g)
-        if (g != gs[i]) {
-          mx = std::max(mx, kub[(size_t)i * G + g]);
-          mn = std::min(mn, kub[(size_t)i * G + g]);
-        }
-      const int g = gs[i];
-      fprintf(stderr, "[prune] q %d S0 %g T %g g* %d kub* %g others [%g, %g]\n", i, S0[i], th[i], g,
-              g >= 0 ? kub[(size_t)i * G + g] : NAN, mn, mx);
-      if (g >= 0) {
-        const GroupBound& b = gb[g];
-        fprintf(stderr, "[prune]   g* r %g wmin %g wmax %g ldmin %g ldabs %g mmax %g iL [%g %g] C [%g %g] dist2 %g\n",
-                b.r, b.wmin, b.wmax, b.ldmin, b.ldabs, b.mmax, b.iLmin, b.iLmax, b.Cmin, b.Cmax, d2[(size_t)i * G + g]);
-        const int o = (g + 1) % G;
-        const GroupBound& c = gb[o];
-        fprintf(stderr, "[prune]   g %d r %g wmin %g wmax %g ldmin %g ldabs %g mmax %g iL [%g %g] C [%g %g] dist2 %g kub %g\n",
-                o, c.r, c.wmin, c.wmax, c.ldmin, c.ldabs, c.mmax, c.iLmin, c.iLmax, c.Cmin, c.Cmax,
-                d2[(size_t)i * G + o], kub[(size_t)i * G + o]);
-      }
+        if (g != gs[i]) mx = std::max(mx, kub[(size_t)i * G + g]);
+      fprintf(stderr, "[prune] q %d T %g g* %d kub* %g others max %g\n", i, th[i], gs[i],
+              gs[i] >= 0 ? kub[(size_t)i * G + gs[i]] : NAN, mx);
     }
   }
+  c.grp_done = 0;   // the Fast tables are written (group_tables is a no-op)
+  ix->prune_nq += nq;
   return CWQ_OK;
 }
 
@@ -1900,7 +1879,6 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                !getenv("CWQ_SB_UNFUSED");
   SbPrepArgs sp;
   const bool prn = !ib && use_prune(ix);
-  PruneArgs pra;
   if (prn) fused = false;
   if (fused) {
     memset(&sp, 0, sizeof(sp));
@@ -1958,7 +1936,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
     } else if (prn) {
-      if ((rc = prune_stage_a(ix, c, q, K, b, pra, s))) return rc;
+      // the seed threshold goes straight to the filter's T0: no probe pass
+      if ((rc = prune_internal(ix, c, q, K, b, s, tl + (K - 1), 64))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q, 0))) {
       return rc;
     }
@@ -2046,11 +2025,13 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     a.fldP = std::max(ix->NI, 1);
     a.fqcnt = qcnt;
   }
-  HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
+  // group pruning: the seed threshold (exact keys of the best group's sample rows) is T0 --
+  // the probe would only see the groups kept, so it is skipped
+  if (!prn) HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
   a.sel_ctr = nullptr;
   a.sel_floor = nullptr;
   a.fprep = 0;
-  if (!fsel) {
+  if (!fsel && !prn) {
     HIPCHK(launch_select(lb, ldlb, nqc, (int)a.n_probe, K, tl, tr, s));
     if (c.Tseed) HIPCHK(launch_raise_threshold(tl + (K - 1), 64, c.Tseed, nqc, s));
   }
@@ -2326,13 +2307,12 @@ int score_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
     carve_chunk(ix, b, c, nqc, false);
-    PruneArgs pra;
     if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q + q0 * ix->D, nqf, b, s))) return rc;
     } else if (prn) {
-      if ((rc = prune_stage_a(ix, c, q + q0 * ix->D, K, b, pra, s))) return rc;
+      if ((rc = prune_internal(ix, c, q + q0 * ix->D, K, b, s))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q + q0 * ix->D, filt ? 0 : -1))) {
       return rc;
     }

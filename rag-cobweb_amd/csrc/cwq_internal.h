@@ -21,6 +21,18 @@ struct RowMeta {
 
 enum Epi { EPI_RAW = 0, EPI_KEY = 1, EPI_TOPK = 2 };
 
+// The exact key of an isotropic row from its raw sum acc = sum_d (x_d - mu_d)^2 (16-dim
+// fma partials summed in slice order): lp = -(logdet + dconst + iv acc)/2, Fast key
+// fmaf(pp, invL, cw lp) (pp = the parent's prefix), categorize min(pp, lp) (pp = BF).  One
+// expression shared by the rerank kernels and group pruning's seed, so their keys agree bit
+// for bit with each other and with the scan's epilogue.
+__device__ __forceinline__ float iso_key_tail(float acc, const RowMeta& md, float pp, float& lp, int cat,
+                                              float dconst) {
+  const float S = md.iv * acc;
+  lp = -0.5f * (md.logdet + dconst + S);
+  return cat ? fminf(pp, lp) : fmaf(pp, md.invL, md.cw * lp);
+}
+
 // Row flags
 constexpr int FLAG_HAS_SENT = 1;   // the row's node holds >= 1 sentence
 constexpr int FLAG_INT_COPY = 2;   // the row duplicates an internal node that holds sentences
@@ -185,29 +197,33 @@ struct GroupBound {   // per group, fp64 (cwq_api.hip build_prune)
   int pad_;
 };
 struct PruneArgs {
-  int nq, G, NI, DP, D;
+  int nq, G, NI, DP, D, K;
   int64_t ldS;                  // [nq][ldS] tables (S_int, P, Pg_lo, Pg_hi)
+  const float* q;               // the caller's queries [nq][D]
   const float* X;               // the chunk's padded query slices (kXQ interleave)
+  const float* c0;              // the root centre; cent: group centres [G][D]
+  const float* cent;
   const float* Ar; const float* Br;   // row-major fp32 A, B of the internal nodes [NI][DP]
   const int* par_int; const float* w_int; const float* logdet_int;
   const int* gint;              // pruning group of each internal node (-1: the root)
   const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists
-  int max_chunks;               // max over groups of ceil(nodes / 64): tasks per pair
   const GroupBound* gb;
-  const double* dist2;          // [nq][G] |x - c_g|^2 (group_shift_kernel)
+  double* kpart;                // [2][nq][G]: P0-free part of KUB, and the margin's magnitude term
   float* S; float* P;           // [nq][ldS]
   float* Plo; float* Phi;       // the filters' shifted prefix tables (group-centred rows)
-  const int* grp; const double* F; const double* sh;   // centring group, F, shifts + errors [2][nq][G]
+  const int* grp; const double* F; double* sh;   // centring group, F, shifts + errors [2][nq][G]
   int fillP;                    // also write the sentinel into P (anisotropic leaf rows read P)
   float* kub;                   // [nq][G] key upper bounds (rounded up)
   int* gstar;                   // [nq] best group (-1: none)
-  int2* pairs; int* ctr;        // stage B pair list; ctr[0] pair count, [1..3] claim counters, [4] call total
+  int2* pairs; int* ctr;        // stage B pair list; ctr[0] pair count, [3] claim counter, [4] call total
+  // the seed threshold: up to 64 sample rows per group, their exact keys (cwq_mfma.hip's arithmetic)
+  const int* gs_ptr; const int* gs_rows; const float* Mf; const RowMeta* meta; const int* row_par;
+  float* Tseed;                 // [nq]
+  float* T0; int64_t ldT0;      // optional: also written (the per-call filter's threshold, no probe)
 };
-hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s, bool first);
-hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT, int cus, hipStream_t s);
-hipError_t launch_prune_seed(const float* X, const float* Mf, int DP, int nq, int K, const int* gstar,
-                             const int* gs_ptr, const int* gs_rows, const RowMeta* meta, const int* par,
-                             const float* P, int64_t ldP, float* T, hipStream_t s);   // cwq_mfma.hip
+// launches: front (shifts + the P0-free bound terms), stage A (root, KUB, g*, g*'s exact pass
+// and prefixes), seed (T, stage-B pairs, sentinel fill), stage B (the pairs' exact passes)
+hipError_t launch_prune(const PruneArgs& a, int cus, bool first, hipStream_t s);
 hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s);
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
                                 const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);

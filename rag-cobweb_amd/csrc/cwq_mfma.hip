@@ -1657,9 +1657,7 @@ __device__ __forceinline__ float exact_iso_key(const float* __restrict__ X, cons
     for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + v * 16 + j * 4);
     slice(xg[(size_t)v * kXQ], m4);
   }
-  const float S = md.iv * acc;
-  lp = -0.5f * (md.logdet + dconst + S);
-  return cat ? fminf(pp, lp) : fmaf(pp, md.invL, md.cw * lp);   // categorize: pp = BF[parent]
+  return iso_key_tail(acc, md, pp, lp, cat, dconst);   // categorize: pp = BF[parent]
 }
 
 // Raw sum S = sum_d (x_d A_d - B_d)^2 of internal node i for query q in the exact scan's
@@ -1886,47 +1884,6 @@ __global__ __launch_bounds__(256) void final_kernel(const float* __restrict__ X,
     ok_flag[q] = ok ? 1 : 0;
     if (n_exact) n_exact[q] = nx;
   }
-}
-
-// Group pruning's seed threshold (cwq_prune.hip): per query, the exact Fast
-// keys of up to 64 sample rows of its best group g* (their parents' exact prefixes are
-// stage A's; exact_iso_key: the rerank's keys bit for bit), T[q] = the K-th largest -- K
-// distinct rows have keys >= T, so T <= tau_K.  Fewer than K usable sample rows: -inf
-// (stage B then computes every group).  One wave per query.
-__global__ void prune_seed_kernel(const float* __restrict__ X, const float* __restrict__ Mf, int DP, int nq, int K,
-                                  const int* __restrict__ gstar, const int* __restrict__ gs_ptr,
-                                  const int* __restrict__ gs_rows, const RowMeta* __restrict__ meta,
-                                  const int* __restrict__ par, const float* __restrict__ P, int64_t ldP, float* T) {
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * (int)(blockDim.x / 64) + (int)(threadIdx.x >> 6);
-  if (q >= nq) return;
-  const int g = gstar[q];
-  const int n = g >= 0 ? min(64, gs_ptr[g + 1] - gs_ptr[g]) : 0;
-  float key = -CWQ_INF;
-  int rid = 0x7fffffff;
-  if (lane < n) {
-    const int rr = gs_rows[gs_ptr[g] + lane];
-    const RowMeta md = meta[rr];
-    const int p = par[rr];
-    const float pp = p >= 0 ? P[(size_t)q * ldP + p] : 0.f;
-    float lp;
-    key = exact_iso_key(X, Mf, DP, q, rr, md, pp, lp);
-    if (!(key == key)) key = -CWQ_INF;
-    rid = rr;
-  }
-  float dummy = 0.f;
-  wave_sort64<false>(key, rid, dummy, lane);
-  const float tk = __shfl(key, K - 1, 64);
-  if (lane == 0) T[q] = n >= K ? tk : -CWQ_INF;
-}
-
-hipError_t launch_prune_seed(const float* X, const float* Mf, int DP, int nq, int K, const int* gstar,
-                             const int* gs_ptr, const int* gs_rows, const RowMeta* meta, const int* par,
-                             const float* P, int64_t ldP, float* T, hipStream_t s) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, X, Mf, DP, nq, K, gstar, gs_ptr,
-                     gs_rows, meta, par, P, ldP, T);
-  return hipGetLastError();
 }
 
 // final for small batches (nq <= kFinalWideMaxQ, the per-call paths): one 512-thread

@@ -84,58 +84,6 @@ hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, con
   return hipGetLastError();
 }
 
-// The root's exact prefix, as internal_chain_kernel / prefix_level_kernel form it.
-__device__ __forceinline__ float prune_root_prefix(const PruneArgs& a, int q) {
-  const float lp = -0.5f * (a.logdet_int[0] + a.S[(size_t)q * a.ldS]);
-  return a.w_int[0] * lp;
-}
-
-// KUB[q][g] for every group and g*(q) = argmax (ties: the smaller g).  One wave per query.
-__global__ void prune_bound_kernel(const PruneArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int q = blockIdx.x * (int)(blockDim.x / 64) + (int)(threadIdx.x >> 6);
-  if (q >= a.nq) return;
-  const double P0 = (double)prune_root_prefix(a, q);
-  double best = -INFINITY;
-  int bg = 0x7fffffff;
-  for (int g = lane; g < a.G; g += 64) {
-    const GroupBound b = a.gb[g];
-    double kub = -INFINITY;
-    if (b.valid) {
-      const double e2 = a.dist2[(size_t)q * a.G + g];
-      const double dist_lo = sqrt(e2 * (1.0 - 0x1p-40)) * (1.0 - 0x1p-50);
-      const double dist_hi = sqrt(e2 * (1.0 + 0x1p-40)) * (1.0 + 0x1p-50);
-      const double dlo = fmax(0.0, dist_lo - b.r);
-      // S_fp32 >= (1 - 2^-16) (sqrt(wmin) dlo - 2^-23 sqrt(wmax) mmax)_+^2: the t = x A - B
-      // rounding (B = fl(mu A)) and the fp32 sums' relative error (< 64 * 2^-24)
-      const double sv = sqrt(b.wmin) * dlo - 0x1p-23 * sqrt(b.wmax) * b.mmax;
-      const double SLB = sv > 0.0 ? (1.0 - 0x1p-16) * sv * sv : 0.0;
-      // lp'_fp32 = fl(-0.5 fl(logdet + S)) <= -logdet/2 + 2^-22 |logdet| - (1/2 - 2^-22) S_fp32
-      const double UB = -0.5 * b.ldmin + 0x1p-22 * b.ldabs - (0.5 - 0x1p-22) * SLB;
-      // |lp'| of any member, for the rounding margin of the keys' fp32 chains
-      const double shv = sqrt(b.wmax) * (dist_hi + b.r) + 0x1p-23 * sqrt(b.wmax) * b.mmax;
-      const double mag = 0.5 * (b.ldabs + (1.0 + 0x1p-16) * shv * shv) * (1.0 + 0x1p-20);
-      kub = fmax(b.iLmin * P0, b.iLmax * P0) + fmax(b.Cmin * UB, b.Cmax * UB);
-      // the exact key's fp32 chain (<= 64 fmaf steps + the final fmaf): < 2^-17 of its terms
-      kub += 0x1p-16 * (b.iLmax * fabs(P0) + b.Cmax * mag);
-    }
-    a.kub[(size_t)q * a.G + g] = b.valid ? __double2float_ru(kub) : -INFINITY;
-    if (b.valid && (kub > best || (kub == best && g < bg))) {
-      best = kub;
-      bg = g;
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ob = __shfl_xor(best, off, 64);
-    const int og = __shfl_xor(bg, off, 64);
-    if (ob > best || (ob == best && og < bg)) {
-      best = ob;
-      bg = og;
-    }
-  }
-  if (lane == 0) a.gstar[q] = bg == 0x7fffffff ? -1 : bg;
-}
-
 // Exact prefix of internal node i for query q from the raw sums S (the node's ancestors all
 // computed): internal_chain_kernel's arithmetic, top-down, bit for bit.
 __device__ __forceinline__ float prune_chain_prefix(const PruneArgs& a, int q, int i) {
@@ -174,83 +122,73 @@ __device__ __forceinline__ void prune_write_prefix(const PruneArgs& a, int q, in
   a.Phi[o] = __double2float_ru(tt + e);
 }
 
-// Stage A tables over every (query, node): the root and the nodes of g*(q) exact, the rest
-// the sentinel.
-__global__ void prune_prefix_all_kernel(const PruneArgs a) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)a.nq * a.NI) return;
-  const int q = (int)(t / a.NI);
-  const int i = (int)(t % a.NI);
-  const int g = a.gint[i];
-  if (i == 0 || (g >= 0 && g == a.gstar[q])) {
-    prune_write_prefix(a, q, i);
-    return;
+// Front: per (query, group), one wave: the group shift -2 x'.d_g and its error bound (as
+// group_shift_kernel), |x - c_g|^2, and the bound terms of KUB that do not depend on the
+// root's prefix P0: kpart[0] = max(Cmin UB, Cmax UB), kpart[1] = Cmax mag (the margin's).
+//   every member a of g: S_a >= wmin (|x - c_g| - r_g)_+^2 in real arithmetic; the fp32 S
+//   >= (1 - 2^-16) (sqrt(wmin) dlo - 2^-23 sqrt(wmax) mmax)_+^2 (t = x A - B with B = fl(mu
+//   A), the partial sums' relative error < 64 * 2^-24); lp'_fp32 = fl(-0.5 fl(logdet + S))
+//   <= -logdet/2 + 2^-22 |logdet| - (1/2 - 2^-22) S_fp32 = UB; |lp'| <= mag.
+__global__ void prune_front_kernel(const PruneArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (w >= (int64_t)a.nq * a.G) return;
+  const int64_t qi = w / a.G;
+  const int g = (int)(w % a.G);
+  double d1 = 0.0, ab = 0.0, e2 = 0.0;
+  for (int d = lane; d < a.D; d += 64) {
+    const float x = a.q[qi * a.D + d];
+    const float xc = x - a.c0[d];
+    const float cg = a.cent[(int64_t)g * a.D + d];
+    const double dd = (double)cg - (double)a.c0[d];
+    const double t = (double)xc * dd;
+    d1 += t;
+    ab += fabs(t);
+    const double u = (double)x - (double)cg;
+    e2 += u * u;
   }
-  const size_t o = (size_t)q * a.ldS + i;
-  a.Plo[o] = kPruneSent;
-  a.Phi[o] = kPruneSent;
-  if (a.fillP) a.P[o] = kPruneSent;
+  for (int off = 32; off > 0; off >>= 1) {
+    d1 += __shfl_xor(d1, off, 64);
+    ab += __shfl_xor(ab, off, 64);
+    e2 += __shfl_xor(e2, off, 64);
+  }
+  if (lane != 0) return;
+  const size_t o = (size_t)qi * a.G + g;
+  a.sh[o] = -2.0 * d1;
+  a.sh[(size_t)a.nq * a.G + o] = 2.0 * ab * ((double)(a.D / 64 + 8) * 0x1.02p-53);
+  const GroupBound b = a.gb[g];
+  double kp = -INFINITY, m2 = 0.0;
+  if (b.valid) {
+    // e2: exact differences, squares and fp64 sums: relative error < 2^-40
+    const double dist_lo = sqrt(e2 * (1.0 - 0x1p-40)) * (1.0 - 0x1p-50);
+    const double dist_hi = sqrt(e2 * (1.0 + 0x1p-40)) * (1.0 + 0x1p-50);
+    const double dlo = fmax(0.0, dist_lo - b.r);
+    const double sv = sqrt(b.wmin) * dlo - 0x1p-23 * sqrt(b.wmax) * b.mmax;
+    const double SLB = sv > 0.0 ? (1.0 - 0x1p-16) * sv * sv : 0.0;
+    const double UB = -0.5 * b.ldmin + 0x1p-22 * b.ldabs - (0.5 - 0x1p-22) * SLB;
+    const double shv = sqrt(b.wmax) * (dist_hi + b.r) + 0x1p-23 * sqrt(b.wmax) * b.mmax;
+    const double mag = 0.5 * (b.ldabs + (1.0 + 0x1p-16) * shv * shv) * (1.0 + 0x1p-20);
+    kp = fmax(b.Cmin * UB, b.Cmax * UB);
+    m2 = b.Cmax * mag;
+  }
+  a.kpart[o] = kp;
+  a.kpart[(size_t)a.nq * a.G + o] = m2;
 }
 
-// Stage B pair list: (q, g) with g != g*(q) and KUB[q][g] >= T[q] (T = -inf or NaN: every
-// valid group).
-__global__ void prune_pairs_kernel(const PruneArgs a, const float* __restrict__ T, int64_t ldT) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= (int64_t)a.nq * a.G) return;
-  const int q = (int)(t / a.G);
-  const int g = (int)(t % a.G);
-  if (g == a.gstar[q] || !a.gb[g].valid) return;
-  const float Tq = T[(size_t)q * ldT];
-  if (a.kub[t] >= Tq || !(Tq == Tq)) {
-    const int j = atomicAdd(&a.ctr[0], 1);
-    a.pairs[j] = make_int2(q, g);
-    atomicAdd(&a.ctr[4], 1);   // the call's total (diagnostics)
-  }
-}
-
-// The exact internal pass of (query, group) pairs: persistent workgroups claim (pair, chunk
-// of 64 of the group's nodes) tasks from a counter (stage A: pair p = (p, g*(p)); B: the
-// list), stage the query's slices in LDS, form every (node, 16-dim slice) partial of the
-// chunk in parallel -- exact_aniso_S's fma chain -- and one thread per node adds its
-// partials in slice order: the scan kernel's raw sums bit for bit.  A one-query call spreads
-// a group's chunks over as many workgroups.  Every workgroup leaves when the counter passes
-// the task count.
-constexpr int kPrThreads = 256, kPrChunk = 64;
-__global__ __launch_bounds__(kPrThreads) void prune_scan_kernel(const PruneArgs a, int stage_b, int* claim) {
-  extern __shared__ float s_dyn[];
-  const int NV16 = a.DP / 16, LDP = NV16 + 1;
-  float* s_x = s_dyn;                  // [DP] the query's slices
-  float* s_part = s_dyn + a.DP;        // [kPrChunk][LDP]
-  __shared__ int s_t;
+// The exact internal pass of one (query, group) pair by one workgroup: the query's slices in
+// LDS; per chunk of kPrChunk of the group's nodes every (node, 16-dim slice) partial in
+// parallel -- exact_aniso_S's fma chain -- and one thread per node adding them in slice
+// order (the scan kernel's raw sums bit for bit); then the nodes' prefixes and tables.
+constexpr int kPrThreads = 512, kPrChunk = 128;
+__device__ void prune_pair(const PruneArgs& a, int q, int g, float* s_x, float* s_part) {
   const int tid = threadIdx.x;
-  const int mc = a.max_chunks;
-  const int64_t ntask = (int64_t)(stage_b ? a.ctr[0] : a.nq) * mc;
-  for (;;) {
-    if (tid == 0) s_t = atomicAdd(claim, 1);
-    __syncthreads();
-    const int t = s_t;
-    __syncthreads();
-    if (t >= ntask) break;
-    const int p = t / mc, ch = t - p * mc;
-    int q, g;
-    if (stage_b) {
-      const int2 pr = a.pairs[p];
-      q = pr.x;
-      g = pr.y;
-    } else {
-      q = p;
-      g = a.gstar[p];
-    }
-    if (g < 0) continue;
-    const int c0 = a.gi_ptr[g] + ch * kPrChunk, b1 = a.gi_ptr[g + 1];
-    if (c0 >= b1) continue;   // uniform over the workgroup
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+  for (int d = tid; d < a.DP; d += kPrThreads) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+  __syncthreads();
+  const int b0 = a.gi_ptr[g], b1 = a.gi_ptr[g + 1];
+  for (int c0 = b0; c0 < b1; c0 += kPrChunk) {
     const int cnt = min(kPrChunk, b1 - c0);
-    const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
-    for (int d = tid; d < a.DP; d += kPrThreads) {
-      const int v = d >> 4, j = d & 15;
-      s_x[d] = xq[(size_t)v * kXQ * 16 + j];
-    }
-    __syncthreads();
     for (int it = tid; it < cnt * NV16; it += kPrThreads) {
       const int e = it / NV16, v = it - e * NV16;
       const int node = a.gi_nodes[c0 + e];
@@ -281,22 +219,216 @@ __global__ __launch_bounds__(kPrThreads) void prune_scan_kernel(const PruneArgs 
     }
     __syncthreads();
   }
+  // the raw sums complete and visible before the chain walks read them back
+  __threadfence();
+  __syncthreads();
+  for (int j = b0 + tid; j < b1; j += kPrThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
+  __syncthreads();   // s_x reused by the next pair
 }
 
-// Stage B prefixes: persistent workgroups over the pair list, threads over the group's nodes.
-__global__ __launch_bounds__(256) void prune_prefix_pairs_kernel(const PruneArgs a, int* claim) {
+size_t prune_pair_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
+
+// Stage A, one workgroup per query: the root's raw sum (exact_aniso_S's arithmetic, bit for
+// bit), its prefix P0 and the root's tables; KUB[q][g] = max(iLmin P0, iLmax P0) + kpart +
+// 2^-16 (iLmax |P0| + Cmax mag) (the exact key's fp32 chain: <= 64 fmaf steps and the final
+// fmaf, < 2^-17 of its terms), rounded up; g* = argmax (ties: the smaller g); then g*'s
+// exact pass and prefixes (prune_pair).
+__global__ __launch_bounds__(kPrThreads) void prune_stage_a_kernel(const PruneArgs a) {
+  extern __shared__ float s_dyn[];
+  float* s_x = s_dyn;
+  float* s_part = s_dyn + a.DP;
+  __shared__ float s_p0;
+  __shared__ double s_best[kPrThreads / 64];
+  __shared__ int s_bg[kPrThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x;
+  const int NV16 = a.DP / 16;
+  // the root: 16-dim partials in parallel, added in slice order by thread 0
+  const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+  if (tid < NV16) {
+    const int v = tid;
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float tt = fmaf(xq[(size_t)v * kXQ * 16 + j], a.Ar[v * 16 + j], -a.Br[v * 16 + j]);
+      part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+    }
+    s_dyn[v] = part;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float acc = 0.f;
+    for (int v = 0; v < NV16; ++v) acc += s_dyn[v];
+    a.S[(size_t)q * a.ldS] = acc;
+    const float lp = -0.5f * (a.logdet_int[0] + acc);
+    const float P0 = a.w_int[0] * lp;
+    s_p0 = P0;
+    const size_t o = (size_t)q * a.ldS;
+    a.P[o] = P0;
+    a.Plo[o] = P0;
+    a.Phi[o] = P0;
+  }
+  __syncthreads();
+  const double P0 = (double)s_p0;
+  double best = -INFINITY;
+  int bg = 0x7fffffff;
+  for (int g = tid; g < a.G; g += kPrThreads) {
+    const GroupBound b = a.gb[g];
+    const size_t o = (size_t)q * a.G + g;
+    double kub = -INFINITY;
+    if (b.valid) {
+      kub = fmax(b.iLmin * P0, b.iLmax * P0) + a.kpart[o] +
+            0x1p-16 * (b.iLmax * fabs(P0) + a.kpart[(size_t)a.nq * a.G + o]);
+      if (kub > best || (kub == best && g < bg)) {
+        best = kub;
+        bg = g;
+      }
+    }
+    a.kub[o] = b.valid ? __double2float_ru(kub) : -INFINITY;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ob = __shfl_xor(best, off, 64);
+    const int og = __shfl_xor(bg, off, 64);
+    if (ob > best || (ob == best && og < bg)) {
+      best = ob;
+      bg = og;
+    }
+  }
+  if (lane == 0) {
+    s_best[wave] = best;
+    s_bg[wave] = bg;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kPrThreads / 64; ++w)
+      if (s_best[w] > best || (s_best[w] == best && s_bg[w] < bg)) {
+        best = s_best[w];
+        bg = s_bg[w];
+      }
+    s_bg[0] = bg == 0x7fffffff ? -1 : bg;
+    a.gstar[q] = s_bg[0];
+  }
+  __syncthreads();
+  const int g = s_bg[0];
+  if (g >= 0) prune_pair(a, q, g, s_x, s_part);
+}
+
+// Seed threshold and stage-B pairs, one workgroup per query (blocks >= nq: the sentinel fill
+// of every (query, node) outside the root and g*).  The exact keys of up to 64 sample rows of
+// g* (their parents' prefixes are stage A's): every (row, slice) partial in parallel, summed
+// in slice order and finished by iso_key_tail -- the rerank's keys bit for bit -- so T = the
+// K-th largest over distinct rows is <= tau_K (fewer than K rows: -inf).  Then the groups
+// g != g* with KUB >= T go to the pair list.
+constexpr int kSeedThreads = 256;
+__global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArgs a) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= a.nq) {   // sentinel fill
+    const int64_t t = ((int64_t)blockIdx.x - a.nq) * kSeedThreads + tid;
+    if (t >= (int64_t)a.nq * a.NI) return;
+    const int q = (int)(t / a.NI), i = (int)(t % a.NI);
+    const int g = a.gint[i];
+    if (i == 0 || (g >= 0 && g == a.gstar[q])) return;
+    const size_t o = (size_t)q * a.ldS + i;
+    a.Plo[o] = kPruneSent;
+    a.Phi[o] = kPruneSent;
+    if (a.fillP) a.P[o] = kPruneSent;
+    return;
+  }
+  extern __shared__ float s_part[];   // [64][NV16 + 1]
+  __shared__ float s_T;
+  const int q = blockIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  const int g = a.gstar[q];
+  const int n = g >= 0 ? min(64, a.gs_ptr[g + 1] - a.gs_ptr[g]) : 0;
+  const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+  for (int it = tid; it < n * NV16; it += kSeedThreads) {
+    const int e = it / NV16, v = it - e * NV16;
+    const int rr = a.gs_rows[a.gs_ptr[g] + e];
+    const float* __restrict__ mr = a.Mf + (size_t)rr * a.DP + v * 16;
+    float4 m4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 t4 = m4[j >> 2];
+      const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+      const float t = xq[(size_t)v * kXQ * 16 + j] - mj;
+      part = (j == 0) ? t * t : fmaf(t, t, part);
+    }
+    s_part[e * LDP + v] = part;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float key = -__builtin_inff();
+    int rid = 0x7fffffff;
+    if (lane < n) {
+      const int rr = a.gs_rows[a.gs_ptr[g] + lane];
+      float acc = 0.f;
+      for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+      const int p = a.row_par[rr];
+      const float pp = p >= 0 ? a.P[(size_t)q * a.ldS + p] : 0.f;
+      float lp;
+      key = iso_key_tail(acc, a.meta[rr], pp, lp, 0, 0.f);
+      if (!(key == key)) key = -__builtin_inff();
+      rid = rr;
+    }
+    float dummy = 0.f;
+    wave_sort64<false>(key, rid, dummy, lane);
+    const float tk = __shfl(key, a.K - 1, 64);
+    if (lane == 0) {
+      const float T = n >= a.K ? tk : -__builtin_inff();
+      s_T = T;
+      a.Tseed[q] = T;
+      if (a.T0) a.T0[(size_t)q * a.ldT0] = T;
+    }
+  }
+  __syncthreads();
+  const float T = s_T;
+  for (int gg = tid; gg < a.G; gg += kSeedThreads) {
+    if (gg == g || !a.gb[gg].valid) continue;
+    if (a.kub[(size_t)q * a.G + gg] >= T || !(T == T)) {
+      const int j = atomicAdd(&a.ctr[0], 1);
+      a.pairs[j] = make_int2(q, gg);
+      atomicAdd(&a.ctr[4], 1);   // the call's total (diagnostics)
+    }
+  }
+}
+
+// Stage B: persistent workgroups claim the pairs; every workgroup leaves when the claim
+// counter passes the pair count.
+__global__ __launch_bounds__(kPrThreads) void prune_stage_b_kernel(const PruneArgs a) {
+  extern __shared__ float s_dyn[];
+  float* s_x = s_dyn;
+  float* s_part = s_dyn + a.DP;
   __shared__ int s_p;
   const int npairs = a.ctr[0];
   for (;;) {
-    if (threadIdx.x == 0) s_p = atomicAdd(claim, 1);
+    if (threadIdx.x == 0) s_p = atomicAdd(&a.ctr[3], 1);
     __syncthreads();
     const int p = s_p;
     __syncthreads();
     if (p >= npairs) break;
     const int2 pr = a.pairs[p];
-    const int b0 = a.gi_ptr[pr.y], b1 = a.gi_ptr[pr.y + 1];
-    for (int j = b0 + threadIdx.x; j < b1; j += blockDim.x) prune_write_prefix(a, pr.x, a.gi_nodes[j]);
+    prune_pair(a, pr.x, pr.y, s_x, s_part);
   }
+}
+
+// The whole pruned internal pass of a chunk: front, stage A, seed (+ fill), stage B.
+// ctr[0..3] zeroed here, and ctr[4] (the call's stage-B pair total) on its first pruned chunk.
+hipError_t launch_prune(const PruneArgs& a, int cus, bool first, hipStream_t s) {
+  if (a.nq <= 0) return hipSuccess;
+  if (a.DP % 16 || a.DP / 16 > kPrThreads) return hipErrorInvalidValue;
+  if (hipError_t e = hipMemsetAsync(a.ctr, 0, (first ? 5 : 4) * sizeof(int), s)) return e;
+  const int64_t nw = (int64_t)a.nq * a.G;
+  hipLaunchKernelGGL(prune_front_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(prune_stage_a_kernel, dim3((unsigned)a.nq), dim3(kPrThreads), prune_pair_lds(a.DP), s, a);
+  const int64_t nfill = ((int64_t)a.nq * a.NI + kSeedThreads - 1) / kSeedThreads;
+  hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads),
+                     (size_t)64 * (a.DP / 16 + 1) * 4, s, a);
+  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(nw, cus));
+  hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_pair_lds(a.DP), s, a);
+  return hipGetLastError();
 }
 
 // T[q * ldT] = max(T, Tfloor[q]) (both lower bounds of tau_K; the filter's sample / probe
@@ -309,34 +441,6 @@ __global__ void raise_threshold_kernel(float* T, int64_t ldT, const float* __res
 hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
   hipLaunchKernelGGL(raise_threshold_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, T, ldT, Tfloor, nq);
-  return hipGetLastError();
-}
-
-size_t prune_scan_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
-
-// Stage A: bounds and g* (the caller has written the root's raw sums S[q][0] and the group
-// shifts and distances), the exact pass of g*, the tables.  ctr[0..3] zeroed here, and
-// ctr[4] (the call's stage-B pair total) on the call's first pruned chunk.
-hipError_t launch_prune_stage_a(const PruneArgs& a, int cus, hipStream_t s, bool first) {
-  if (a.nq <= 0) return hipSuccess;
-  if (hipError_t e = hipMemsetAsync(a.ctr, 0, (first ? 5 : 4) * sizeof(int), s)) return e;
-  hipLaunchKernelGGL(prune_bound_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, s, a);
-  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)a.nq * a.max_chunks, (int64_t)cus * 4));
-  hipLaunchKernelGGL(prune_scan_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_scan_lds(a.DP), s, a, 0, a.ctr + 1);
-  const int64_t n = (int64_t)a.nq * a.NI;
-  hipLaunchKernelGGL(prune_prefix_all_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-// Stage B, after the first threshold T[q * ldT] (<= tau_K) is on the device.
-hipError_t launch_prune_stage_b(const PruneArgs& a, const float* T, int64_t ldT, int cus, hipStream_t s) {
-  if (a.nq <= 0 || a.G <= 0) return hipSuccess;
-  const int64_t n = (int64_t)a.nq * a.G;
-  hipLaunchKernelGGL(prune_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, T, ldT);
-  const int wgs = std::max(1, (int)std::min<int64_t>(n * a.max_chunks, (int64_t)cus * 4));
-  hipLaunchKernelGGL(prune_scan_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_scan_lds(a.DP), s, a, 1, a.ctr + 2);
-  const int wgp = std::max(1, (int)std::min<int64_t>(n, (int64_t)cus * 4));
-  hipLaunchKernelGGL(prune_prefix_pairs_kernel, dim3((unsigned)wgp), dim3(256), 0, s, a, a.ctr + 3);
   return hipGetLastError();
 }
 
