@@ -1209,6 +1209,22 @@ __device__ void wheap_push(HeapEnt* h, int64_t& n, const HeapEnt& e, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Push internal node u's children (their full lp from LPF, pscore = u's, BFS index): the
+// lanes load up to 64 children's keys at once, then lane 0 sifts them in one by one in child
+// order -- the same pushes as one load round trip per child, without the round trips.
+__device__ void wheap_push_children(HeapEnt* h, int64_t& n, const SimArgs& a, int q, int u, float pscore, int lane) {
+  const int cb = a.int_child_begin[u], ce = a.int_child_end[u];
+  for (int c0 = cb; c0 < ce; c0 += 64) {
+    const int c = c0 + lane;
+    const bool ok = c < ce;
+    const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
+    const int tb = ok ? a.int_bfs[c] : 0;
+    const int m = min(64, ce - c0);
+    for (int j = 0; j < m; ++j)
+      wheap_push(h, n, HeapEnt{__shfl(lpf, j, 64), pscore, __shfl(tb, j, 64), c0 + j}, lane);
+  }
+}
+
 // best (first in heap order) of the lanes' candidates; lanes with ok == false ignored;
 // returns the winning lane (-1 if none)
 __device__ __forceinline__ int wave_best(bool ok, float sc, float ps, int tb) {
@@ -1320,8 +1336,7 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
     if (is_int) {
       const int u = e.node;
       calls += a.int_nchild[u];
-      for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
-        wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c}, lane);
+      wheap_push_children(h, hn, a, q, u, e.score, lane);
       if (dense) {
         for (int pass = 0; pass < 2; ++pass) {
           const int r0 = pass ? a.int_leaf_b0[u] : a.int_leaf_a0[u];
@@ -1442,8 +1457,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
         status = 1;
         break;
       }
-      for (int c = a.int_child_begin[u]; c < a.int_child_end[u]; ++c)
-        wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI + c], e.score, a.int_bfs[c], c}, lane);
+      wheap_push_children(h, hn, a, q, u, e.score, lane);
       for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint)
         uint64_t bm = __ballot(l == 0 ? p1 == u : p2 == u);
         while (bm) {

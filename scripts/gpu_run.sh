@@ -3,7 +3,7 @@
 #   gpurun -- bash scripts/gpu_run.sh TAG STEP [STEP ...]
 # Steps (run in order, each under its own time limit; the script stops at the first failure):
 #   suite           the whole -m gpu suite                      -> gpurun_out/TAG_pytest_gpu.log
-#   tests:EXPR      pytest -m gpu -k EXPR                        -> gpurun_out/TAG_pytest_k.log
+#   tests:EXPR      pytest -m gpu -k EXPR ('+' means ' or ')      -> gpurun_out/TAG_pytest_k.log
 #   pmc             PMC passes of the filter kernel, summarised  -> gpurun_out/pmc_fgemm.json
 #   smoke           __graft_entry__.smoke()                       -> gpurun_out/TAG_smoke.log
 #   bench           bench.py --steps 10 --warmup 3 (with the pmc step's JSON if it ran)
@@ -26,8 +26,10 @@ for step in "$@"; do
           > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest_gpu.log; exit 1; }
       tail -2 gpurun_out/${TAG}_pytest_gpu.log ;;
     tests:*)
+      kexpr=${step#tests:}
+      kexpr=${kexpr//+/ or }   # tests:a+b -> -k "a or b"
       timeout -k 10 600 python -u -m pytest -p no:cacheprovider -v --timeout 300 --timeout-method thread -m gpu tests \
-          -k "${step#tests:}" > gpurun_out/${TAG}_pytest_k.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest_k.log; exit 1; }
+          -k "$kexpr" > gpurun_out/${TAG}_pytest_k.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest_k.log; exit 1; }
       tail -2 gpurun_out/${TAG}_pytest_k.log ;;
     pmc)
       bash scripts/pmc.sh "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
