@@ -2616,6 +2616,96 @@ namespace {
 // cwq_categorize body.  allow_filter: the isotropic leaf rows go through the bf16-MFMA
 // filter with the categorize key (run_iso_filter, cat); queries whose candidate lists
 // overflow are re-run with allow_filter = false (the exact scan of every leaf row).
+// Categorize's top-R row list for a few queries (nq <= kStreamMaxQ) through the per-call
+// stream filter instead of the batch pipeline (sample pass, select, five fgemm launches with
+// bucket / tighten): query prep, probe + fused select, one pass, final_wide_kernel with the
+// categorize key -- the key min(BFk[parent], lp_full) bounded by the categorize RowF and
+// min'ed with BFk in the kernels (cwq_stream.hip), exact keys and the list order of
+// list_before<true> in final_wide.  BFk: the chunk's BF (list 1) or the second-level T2
+// (the two-level replay's list 2).  The list goes to slot 0 of pkey/paux/prow (stride lstride),
+// the per-query certified flags to okf (a query whose candidates overflow: 0).
+size_t stream_cat_bytes(const cwq_index* ix, int nqc) {
+  const int nq16 = (nqc + 15) / 16 * 16;
+  const int64_t ldlb = round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024;
+  return (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)nqc * 4 + (size_t)(5 * nqc + 1) * 4 +
+         (size_t)nqc * kFgCapQ * 12 + (size_t)nqc * 64 * 16 + (size_t)nqc * ldlb * 4 + 16 * 256;
+}
+bool stream_cat_ok(const cwq_index* ix, int nqc, int R) {
+  return ix->iso_Mb && ix->NL_iso >= kStreamMinRows && nqc <= kStreamMaxQ && R <= kFiltMaxK &&
+         stream_lds_bytes((nqc + 15) / 16, ix->DPB) <= (size_t)kStreamMaxLds && final_wide_rows(ix->DP, kFgCapQ) > 0 &&
+         !getenv("CWQ_CAT_STREAM_OFF");
+}
+int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, const float* BFk, float dfull, float* pkey,
+                    float* paux, int* prow, int64_t lstride, int* okf, Bump& b, hipStream_t s) {
+  const int nqb = (nqc + 15) / 16, nq16 = nqb * 16;
+  const int capq = kFgCapQ;
+  uint16_t* Xb = b.take<uint16_t>((size_t)nq16 * ix->DPB);
+  float4* qinfo = b.take<float4>(nq16);
+  float* T = b.take<float>(nqc);
+  int* qcnt = b.take<int>((size_t)5 * nqc + 1);   // [qcnt | ok | n_exact | qover | done | select counter]
+  int* nex = qcnt + 2 * nqc;
+  int* qover = qcnt + 3 * nqc;
+  int* done = qcnt + 4 * nqc;
+  int* sel_ctr = qcnt + 5 * nqc;
+  int* crow = b.take<int>((size_t)nqc * capq);
+  float* cu = b.take<float>((size_t)nqc * capq);
+  float* cl = b.take<float>((size_t)nqc * capq);
+  float* lkb = b.take<float>((size_t)nqc * 64);
+  int* lrb = b.take<int>((size_t)nqc * 64);
+  const int64_t ldlb = round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024;
+  float* lb = b.take<float>((size_t)nqc * ldlb);
+  float* tl = b.take<float>((size_t)nqc * 64);
+  int* tr = b.take<int>((size_t)nqc * 64);
+  // the counters (qcnt, qover, done, the fused select's) zeroed by the prep's block 0
+  HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s, qcnt, (int)(5 * nqc + 1)));
+  const FiltConsts fc = filt_consts(ix->DPB);
+  StreamArgs a;
+  memset(&a, 0, sizeof(a));
+  a.DPB = ix->DPB;
+  a.nq = nqc;
+  a.nqb = nqb;
+  a.nrows = ix->NL_iso;
+  a.K = R;
+  a.Xb = Xb;
+  a.qinfo = qinfo;
+  a.Mb = ix->iso_Mb;
+  a.rf = ix->cat_rf;
+  const bool grp = ix->grp_mode && c.Pc_lo;
+  a.P = grp ? c.Pc_lo : (c.BF ? c.BF : ix->dummy);   // non-group rows: invL 0 (no prefix term)
+  a.Phi = grp ? c.Pc_hi : nullptr;
+  a.ldP = std::max(ix->NI, 1);
+  a.pT = 0;
+  a.BFk = BFk;
+  a.ldBF = std::max(ix->NI, 1);
+  a.eps_n = (float)fc.eps_n;
+  a.slack = (float)fc.slack;
+  a.T = T;
+  a.qcnt = qcnt;
+  a.qover = qover;
+  a.capq = capq;
+  a.crow = crow;
+  a.cu = cu;
+  a.cl = cl;
+  const int64_t ngroups = (ix->NL_iso + 15) / 16;
+  int64_t n_probe = std::min<int64_t>(std::max<int64_t>((int64_t)3 * R * ngroups / 1024, (int64_t)8 * R), ngroups);
+  a.probe_stride = std::max<int64_t>(1, ngroups / std::max<int64_t>(n_probe, 1));
+  a.n_probe = std::min<int64_t>(n_probe, (ngroups + a.probe_stride - 1) / a.probe_stride);
+  a.lb = lb;
+  a.ldlb = ldlb;
+  a.T0 = tl;
+  a.ldT0 = 64;
+  a.sel_ctr = sel_ctr;
+  a.sel_lk = tl;
+  a.sel_lr = tr;
+  HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
+  a.sel_ctr = nullptr;
+  HIPCHK(launch_stream(a, 0, stream_wgs(ix), s));
+  HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta, ix->row_par,
+                      BFk ? BFk : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, lstride, okf, nex, lkb, lrb,
+                      done, nullptr, 1, dfull, s));
+  return CWQ_OK;
+}
+
 int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
                     int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
@@ -2637,6 +2727,11 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   int64_t cq = chunk_queries(ix, nq, (size_t)cap_list * 16 + (size_t)max_slabs * R * 12 + R * 12 + filt_q);
   if (filt && cq < nq) cq = std::max<int64_t>(kFgTile, cq / kFgTile * kFgTile);   // whole query tiles
   std::vector<int64_t> fredo;   // queries the filter could not certify
+  // a few queries (the reference's one cobweb_predict per query): the lists through the
+  // per-call stream filter (stream_cat_list), and a two-level replay of every query of the
+  // call reuses the chunk's internal pass instead of gathering and recomputing it
+  const bool scat = filt && nq <= cq && stream_cat_ok(ix, (int)nq, R);
+  const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
@@ -2646,6 +2741,9 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 8) + 16 * 256 +
                   (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
+    if (scat)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
+      need += 2 * stream_cat_bytes(ix, nqc) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
+                                                                 (size_t)R * 12 + (size_t)cap2 * 16 + 16) + 32 * 256;
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
     Chunk c;
@@ -2664,7 +2762,17 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     int nst = 0;
     std::vector<char> fbad(nqc, 0);
     int* okf_d = nullptr;   // filter: per-query list-certified flags
-    if (filt) {
+    std::vector<int> okh(filt ? nqc : 0);
+    if (filt && scat) {
+      // anisotropic rows: the exact scan into slots 1..; isotropic rows: the stream filter
+      // with the categorize key -> exact keys in list slot 0
+      if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 2, 1, slabs)))
+        return rc;
+      okf_d = b.take<int>((size_t)nq_pad);
+      if ((rc = stream_cat_list(ix, c, q + q0 * ix->D, nqc, R, c.BF, dfull, pkey, paux, prow, (int64_t)nst * R, okf_d, b,
+                                s)))
+        return rc;
+    } else if (filt) {
       // isotropic rows: the filter with the categorize key -> exact keys in list slot 0;
       // anisotropic rows: the exact scan into slots 1..
       IsoFilter fo;
@@ -2676,14 +2784,6 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
                           pkey, paux, prow, (int64_t)nst * R, fo.okf, fo.nex, fo.tlk, fo.tr, fo.tdone, nullptr, 1, dfull,
                           s));
       okf_d = fo.okf;
-      std::vector<int> okh(nqc);
-      HIPCHK(hipMemcpyAsync(okh.data(), fo.okf, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      for (int i = 0; i < nqc; ++i)
-        if (!okh[i]) {
-          fbad[i] = 1;
-          fredo.push_back(q0 + i);
-        }
     } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 3, 0, slabs))) {
       return rc;
     }
@@ -2742,7 +2842,14 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HIPCHK(launch_simulate(sa, s));
     std::vector<int> st(nqc);
     HIPCHK(hipMemcpyAsync(st.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
+    // the filter's certified flags come back with the status (one sync)
+    if (okf_d) HIPCHK(hipMemcpyAsync(okh.data(), okf_d, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < (int)okh.size(); ++i)
+      if (!okh[i]) {
+        fbad[i] = 1;
+        fredo.push_back(q0 + i);
+      }
     std::vector<int> redo;
     for (int i = 0; i < nqc; ++i)
       if (st[i] && !fbad[i]) redo.push_back(i);   // filter failures are re-run whole below
@@ -2756,7 +2863,53 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     // inside a tie: a second exact leaf scan keyed by the second-level bottleneck, then
     // the replay on both lists; what it cannot certify goes to the DENSE re-run below.
     const char* tle = getenv("CWQ_CAT_TWO");
-    if (ix->NI > 0 && !ix->any_int_sent && !complete && R == 64 && !(tle && *tle && atoi(tle) == 0)) {
+    const bool two = ix->NI > 0 && !ix->any_int_sent && !complete && R == 64 && !(tle && *tle && atoi(tle) == 0);
+    if (two && scat && (int)redo.size() == nqc) {
+      // every query of the call: the replay on the chunk itself -- its BF / LPF, the group
+      // term tables and list 1 (okey) stay on the device; list 2 by the stream filter keyed
+      // by T2 (plus the anisotropic rows' exact scan); results straight into the outputs
+      const size_t ldI = (size_t)std::max(ix->NI, 1);
+      float* T2 = b.take<float>((size_t)nq_pad * ldI);
+      float* pk2 = b.take<float>((size_t)nq_pad * slabs * R);
+      float* pa2 = b.take<float>((size_t)nq_pad * slabs * R);
+      int* pr2 = b.take<int>((size_t)nq_pad * slabs * R);
+      float* l2k = b.take<float>((size_t)nq_pad * R);
+      float* l2a = b.take<float>((size_t)nq_pad * R);
+      int* l2r = b.take<int>((size_t)nq_pad * R);
+      HeapEnt* heap2 = b.take<HeapEnt>((size_t)nq_pad * cap2);
+      int* status2 = b.take<int>((size_t)nq_pad);
+      int* okf2 = b.take<int>((size_t)nq_pad);
+      HIPCHK(launch_cat_t2(c.BF, c.LPF, (int64_t)ldI, ix->NI, nqc, ix->par_int, okey, R, T2, s));
+      Chunk c2t = c;
+      c2t.BF = T2;   // the categorize key reads min(T2[parent], lp)
+      int nst2 = 0;
+      if ((rc = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
+        return rc;
+      if ((rc = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2, b,
+                                s)))
+        return rc;
+      HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
+      SimArgs st2 = sa;
+      st2.pre_status = 0;
+      st2.lkey2 = l2k;
+      st2.laux2 = l2a;
+      st2.lrow2 = l2r;
+      st2.T2 = T2;
+      st2.heap = heap2;
+      st2.heap_cap = cap2;
+      st2.status = status2;
+      HIPCHK(launch_simulate_two(st2, s));
+      std::vector<int> hs(nqc), ho(nqc);
+      HIPCHK(hipMemcpyAsync(hs.data(), status2, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(ho.data(), okf2, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      std::vector<int> left;
+      for (int i = 0; i < nqc; ++i) {
+        if (hs[i] || !ho[i]) left.push_back(i);   // uncertified, or list 2 overflowed: DENSE
+        else ++ix->stats[5];
+      }
+      redo.swap(left);
+    } else if (two) {
       std::vector<float> h1k((size_t)nqc * R), h1a((size_t)nqc * R);
       std::vector<int> h1r((size_t)nqc * R);
       HIPCHK(hipMemcpyAsync(h1k.data(), okey, h1k.size() * 4, hipMemcpyDeviceToHost, s));
@@ -2764,7 +2917,6 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(hipMemcpyAsync(h1r.data(), orow, h1r.size() * 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       std::vector<int> left;
-      const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
       const size_t per_q2 = chunk_bytes(ix, kQPad) / kQPad + (size_t)std::max(ix->NI, 1) * 4 + (size_t)cap2 * 16 +
                             (size_t)R * 12 * 2 + 64 + (size_t)k * 8 + (size_t)ix->D * 4 +
                             (size_t)R * 12 * (pick_nslab(ix, ix->NL_iso, 1) + pick_nslab(ix, ix->NL_an, 1) + 2) *

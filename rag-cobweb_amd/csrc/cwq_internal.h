@@ -629,6 +629,11 @@ struct StreamArgs {
   float* sel_lk;
   int* sel_lr;
   const float* sel_floor;      // optional [nq]: the K-th entry written is max(it, floor) (group pruning's seed)
+  // categorize (cwq_categorize's per-call lists): the key is min(BFk[q][parent], lp) -- both
+  // bounds are min'ed with it (BFk: the path bottleneck BF, or the second-level T2); rf are
+  // then the categorize RowF (cat_rf) and P / Phi its group-term tables
+  const float* BFk;
+  int64_t ldBF;
   // probe with the query prep fused (flat trees, nq <= 16, bf16; fprep set): every workgroup
   // forms the bf16 query fragments, the {|x'|^2, |x_hi|, |x_lo|} terms and the root's exact
   // prefix itself (sb_prep_kernel's arithmetic), and workgroup 0 also writes them to Xb /

@@ -2062,7 +2062,9 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     s_ns = 0;
     s_nx = 0;
   }
-  const bool ok = ov == 0 && n >= K && n <= capq && Tq > -CWQ_INF;   // uniform over the block
+  // T = -inf (categorize lists whose probe saw fewer than K finite keys): every row with a
+  // finite bound is a candidate, so the list is complete while it did not overflow
+  const bool ok = ov == 0 && n <= capq && (Tq > -CWQ_INF ? n >= K : Tq == -CWQ_INF);   // uniform over the block
   // the rest of the lists' l and u (one more round trip, every load of it in flight at once)
   const int nst = ok ? min(n, kFwCand) : 0;
   {

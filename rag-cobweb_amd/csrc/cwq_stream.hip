@@ -220,8 +220,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   // one load per wave)
   int cpar = -3;
   float cP[MQB], cPh[MQB];   // lower / upper bound of the parent prefix (equal when exact)
+  float cB[MQB];             // categorize: the parent's bottleneck (BFk)
 #pragma unroll
-  for (int qb = 0; qb < MQB; ++qb) cP[qb] = cPh[qb] = 0.f;
+  for (int qb = 0; qb < MQB; ++qb) cP[qb] = cPh[qb] = 0.f, cB[qb] = CWQ_INF;
   const float* Pu = a.Phi ? a.Phi : a.P;
   auto panel = [&](int64_t gi) {
     const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
@@ -341,7 +342,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
         for (int qb = 0; qb < MQB; ++qb) {
           cP[qb] = cPh[qb] = 0.f;
+          cB[qb] = CWQ_INF;
           if (!qok[qb] || cpar < 0) continue;
+          if (MODE != 2 && a.BFk) cB[qb] = a.BFk[(size_t)(qb * 16 + r16) * a.ldBF + cpar];
           if (fprep) {   // flat tree: the root is every row's parent
             cP[qb] = cPh[qb] = s_pr[qb * 16 + r16];
           } else if (a.pb.dot) {
@@ -366,9 +369,13 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         const float dot = I8 ? (float)acc[qb][j] * (qi[qb].w * rf[j].R0) : (float)acc[qb][j];
         fg_bounds2(dot, (I8 ? 0x1p-21f : 0x1p-23f) * fabsf(dot), qi[qb], rf[j], cPh[qb] * rf[j].invL,
                    cP[qb] * rf[j].invL, a.eps_n, a.slack, u, l);
+        if (a.BFk) {   // categorize: min(BFk[parent], lp) is monotone in lp (CWQ_INF: no parent)
+          u = fminf(u, cB[qb]);
+          l = fminf(l, cB[qb]);
+        }
         if (MODE == 1) {
           pmax[qb] = fmaxf(pmax[qb], l);
-        } else if (u >= Tq[qb]) {
+        } else if (u >= Tq[qb] && u > -CWQ_INF) {   // (a -inf bound: a -inf key, never listed)
           const int q = qb * 16 + r16;
           // live threshold: fold l into its row block, then publish min over the blocks
           // (rare: ~K x a few candidates per query after the first groups)

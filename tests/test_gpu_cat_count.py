@@ -141,3 +141,36 @@ def test_two_level_replay_on_clustered_ifit_tree(gpu, filt):
         if (k, mx) == (10, 100000):
             two = st["two_level"]
     assert two >= 0.5 * Q.shape[0], two
+
+
+@pytest.mark.parametrize("nq", [1, 8, 64])
+def test_small_calls_stream_lists_equal_dense(gpu, nq):
+    """Calls of <= 64 queries take the per-call stream filter for both lists (the categorize
+    key min(BF or T2 [parent], lp) in cwq_stream.hip) and replay the two-level lists on the
+    chunk itself.  On the clustered device-ifit tree (every query ends in a bottleneck tie)
+    and a two-level tree, pop order, n_found and calls equal the DENSE re-run and the batch
+    call's rows, k = 10 and k = 64, max_nodes cutting inside the search too."""
+    import random
+    rng = np.random.default_rng(7)
+    n, d, nc = 20_000, 64, 40
+    C = rng.standard_normal((nc, d)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, nc, n)] + 0.3 * rng.standard_normal((n, d))).astype(np.float32)
+    random.seed(7)
+    w = gpu.CobwebWrapper(corpus=None, corpus_embeddings=X)
+    w.build_prediction_index()
+    Qn = np.concatenate([X[:96] + 0.05 * rng.standard_normal((96, d)),
+                         C[rng.integers(0, nc, 32)] + 0.3 * rng.standard_normal((32, d))]).astype(np.float32)
+    Q = torch.from_numpy(Qn).cuda()
+    Xt = torch.from_numpy(X).cuda()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(8)
+    t = gpu.synth.two_level_synth(Xt, torch.randint(0, 300, (n,), generator=g, device="cuda:0"))
+    ix2 = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    for ix in (w._index, ix2):
+        for k, mx in [(10, 100000), (64, 100000), (10, 40)]:
+            ref, _ = _run(ix, Q, k, mx, CWQ_CAT_COUNT="0", CWQ_CAT_TWO="0")
+            for a in range(0, 128, nq):
+                got, st = _run(ix, Q[a:a + nq].contiguous(), k, mx)
+                for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
+                    assert torch.equal(x[a:a + nq], y), (name, k, mx, a, st)
+    ix2.close()
