@@ -828,7 +828,21 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     s_cnt[2] = 0;    // its fill
   }
   f32x4 acc[8][4];
+#if FG_STAMP
+  // diagnostic: per-tile timestamps of wave 0 of workgroups 0..63, tiles 0..15: [wg][tile][4]
+  // (setup start, setup barrier passed, K loop done, epilogue done) after the stage stamps
+  unsigned long long* tsp = (a.stamp && blockIdx.x < 64 && tid == 0) ? a.stamp + 16384 + (size_t)blockIdx.x * 64 : nullptr;
+#define FG_TS(k)                                                                  \
+  do {                                                                            \
+    if (tsp && tile_no < 16) tsp[tile_no * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FG_TS(k) \
+  do {           \
+  } while (0)
+#endif
   for (;;) {
+    FG_TS(0);
     const int q0 = qt * FT, r0 = rt * FT;
     // ---- tile setup: per-query terms in LDS, per-row terms in registers ----
     TileF tf;
@@ -905,6 +919,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     }
     if (dyn && tid == 0) s_cnt[8] = claimv;   // the tile after this one
     __syncthreads();   // stage 0 landed, setup visible
+    FG_TS(1);
     if (dyn) next_i = __builtin_amdgcn_readfirstlane(s_cnt[8]);   // uniform: scalar tile loads
     // FG_LEAN: the previous tile's record counter (every thread read it before this
     // barrier) is cleared for the tile after this one
@@ -990,6 +1005,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
       FG_ST(4);
     }
 #undef FG_ST
+    FG_TS(2);
     // ---- epilogue ----
     // The stage buffer just consumed is free until the next tile's first K step
     // re-issues it: 4 KiB per wave of it hold one 32x32 block for the scalar paths.
@@ -1290,6 +1306,7 @@ __global__ __launch_bounds__(512) void fgemm_kernel(const __bf16* __restrict__ X
     }
   next_tile:
     i = next_i;
+    FG_TS(3);
     ++tile_no;
     if (i >= ntl) break;
     if (!dyn) next_i = i + nw_x;

@@ -13,3 +13,15 @@ for g in range(2):
     print(f"group {g}: n={len(sel)}  mem {np.median(d[:, 0]):.0f}  wait-in {np.median(d[:, 1]):.0f}  "
           f"mfma {np.median(d[:, 2]):.0f}  wait-out {np.median(d[:, 3]):.0f}  (median cycles; total "
           f"{np.median(d.sum(-1)):.0f})")
+
+# per-tile stamps (wave 0 of workgroups 0..63, tiles 0..15): setup, K loop, epilogue, gap
+t = np.fromfile(sys.argv[1], dtype=np.uint64)[16384:16384 + 64 * 64].reshape(64, 16, 4).astype(np.int64)
+okt = (t[..., 0] > 0) & (t[..., 3] > 0)
+sel = t[okt]
+if len(sel):
+    d = np.diff(sel, axis=-1)
+    gap = (t[:, 1:, 0] - t[:, :-1, 3])[okt[:, 1:] & okt[:, :-1]]
+    tot = np.median(d.sum(-1)) + (np.median(gap) if len(gap) else 0)
+    print(f"tiles: n={len(sel)}  setup {np.median(d[:, 0]):.0f}  K loop {np.median(d[:, 1]):.0f}  "
+          f"epilogue {np.median(d[:, 2]):.0f}  gap to next {np.median(gap) if len(gap) else 0:.0f}  "
+          f"(median s_memtime ticks; K loop share {np.median(d[:, 1]) / tot:.3f})")
