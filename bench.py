@@ -18,7 +18,8 @@ scaling).  Preset c4 (BASELINE configs[3]): 10M x 1024, 100k queries per step sp
 over the ranks by `sharded_query` (strong scaling).  No collective in the timed loop.
 
 Also reported: `per_call` (the reference harness's one-query-per-call mode at nq = 1, 8,
-64) and `cpu_baseline` (the reference op sequence in torch-CPU, all threads + 1 thread).
+64, plus the wrapper's numpy-query Fast and Basic calls: harness_call_nq1,
+harness_basic_nq1) and `cpu_baseline` (the reference op sequence in torch-CPU, all threads + 1 thread).
 """
 import argparse
 import json
@@ -221,22 +222,26 @@ class _Names:
         return f"s{i}"
 
 
-def per_call_harness(pkg, index, Q, k, reps=200):
+def per_call_harness(pkg, index, Q, k, reps=200, basic=False, node_of_sentence=None):
     """The reference harness's own timed call (benchmark_utils.py:576-579, 801-805):
     `latency = time.time()` around `cobweb.cobweb_predict_fast(query_emb, k)` with a numpy
     query and sentence strings out -- the drop-in CobwebWrapper over this index, so the
     host->device copy of the query, the result sync and the id -> sentence mapping
-    (wrapper.cobweb_predict_indexed) are inside the time."""
-    w = pkg.CobwebWrapper.from_index(index, _Names(index.n_sent))
+    (wrapper.cobweb_predict_indexed) are inside the time.  basic=True times "Cobweb Basic"
+    instead (benchmark_utils.py:580-581: `cobweb.cobweb_predict(query_emb, k)`, best-first
+    categorize, wrapper.cobweb_predict) over the same tree."""
+    w = pkg.CobwebWrapper.from_index(index, _Names(index.n_sent), node_of_sentence=node_of_sentence)
+    fn = w.cobweb_predict if basic else w.cobweb_predict_fast
     Qh = Q[:reps].cpu().numpy()
-    w.cobweb_predict_fast(Qh[0], k)
+    fn(Qh[0], k)
     ts = []
     for i in range(reps):
         t = time.perf_counter()
-        w.cobweb_predict_fast(Qh[i], k)
+        fn(Qh[i], k)
         ts.append(time.perf_counter() - t)
     ts.sort()
-    return {"call": "CobwebWrapper.cobweb_predict_fast(numpy_query, k) -> list of sentences",
+    name = "cobweb_predict" if basic else "cobweb_predict_fast"
+    return {"call": f"CobwebWrapper.{name}(numpy_query, k) -> list of sentences",
             "queries": reps, "us_per_call_median": round(ts[reps // 2] * 1e6, 1),
             "us_per_call_p10": round(ts[reps // 10] * 1e6, 1), "us_per_call_mean": round(float(np.mean(ts)) * 1e6, 1),
             "queries_per_s": round(reps / float(np.sum(ts)), 1)}
@@ -420,6 +425,13 @@ def main():
     if rank == 0 and not args.no_per_call:
         pc = per_call(index, Ql, k)
         pc["harness_call_nq1"] = per_call_harness(pkg, index, Ql, k)
+        try:
+            pc["harness_basic_nq1"] = per_call_harness(pkg, index, Ql, k, reps=50, basic=True,
+                                                       node_of_sentence=nos)
+            pc["harness_basic_nq1"]["tree"] = "the bench's flat-synth tree (root -> leaves): Basic pops the root, " \
+                                              "scores every leaf, retrieves the k best"
+        except Exception as e:            # recorded, never hides the Fast legs
+            pc["harness_basic_nq1"] = {"error": repr(e)}
         torch.cuda.empty_cache()
         mem["device_used_after_per_call"] = dev_used()
         mem["peak_sampled"] = max(mem["peak_sampled"], mem["device_used_after_per_call"])

@@ -427,10 +427,10 @@ __device__ __forceinline__ void fd_insert_mv(float c, float m, float m2, float x
 #pragma clang fp contract(off)
   const float cnt = c + 1.0f;
   const float delta = x - m;
-  const float mm = m + delta / cnt;
+  const float mm = m + CWQ_KDIV(delta, cnt);
   const float mm2 = m2 + delta * (x - mm);
   mo = mm;
-  vo = mm2 / cnt + pv;
+  vo = CWQ_KDIV(mm2, cnt) + pv;
 }
 
 // KL(cand || ref) of one wave from its two sums: (Sa + Sb - D) / 2 in float32 --
@@ -459,13 +459,13 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
     const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
     const float xd = sh.x[d];
     const float delta = xd - m;
-    const float mm = m + delta / cnt;
+    const float mm = m + CWQ_KDIV(delta, cnt);
     const float mu1 = h ? m : mm;
     const float num = h ? m2 : m2 + delta * (xd - mm);
-    const float v1 = num / (h ? cc : cnt) + pv;
+    const float v1 = CWQ_KDIV(num, (h ? cc : cnt)) + pv;
     a = sh.lv2[d] - ref_logf(v1);
     const float df = mu1 - sh.mu2[d];
-    b = (v1 + df * df) / sh.v2[d];
+    b = CWQ_KDIV((v1 + df * df), sh.v2[d]);
   }, sa, sb);
   const float k = fd_kl_score(sa, sb, D);
   U = __shfl(k, 0, 64);
@@ -479,10 +479,10 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, con
   const float cc = f.count[c];
   float sa, sb;
   torch_sum2(D, lane, [&](int d, float& a, float& b) {
-    const float mu1 = f.mean[(size_t)c * D + d], v1 = f.meanSq[(size_t)c * D + d] / cc + f.pv;
+    const float mu1 = f.mean[(size_t)c * D + d], v1 = CWQ_KDIV(f.meanSq[(size_t)c * D + d], cc) + f.pv;
     a = lv[d] - ref_logf(v1);
     const float df = mu1 - mu[d];
-    b = (v1 + df * df) / v[d];
+    b = CWQ_KDIV((v1 + df * df), v[d]);
   }, sa, sb);
   return fd_kl_score(sa, sb, D);
 }
@@ -495,10 +495,10 @@ __device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const float* mu, con
   float sa, sb;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     const size_t o = (size_t)(h ? c1 : c0) * D + d;
-    const float mu1 = f.mean[o], v1 = f.meanSq[o] / (h ? cc1 : cc0) + f.pv;
+    const float mu1 = f.mean[o], v1 = CWQ_KDIV(f.meanSq[o], (h ? cc1 : cc0)) + f.pv;
     a = lv[d] - ref_logf(v1);
     const float df = mu1 - mu[d];
-    b = (v1 + df * df) / v[d];
+    b = CWQ_KDIV((v1 + df * df), v[d]);
   }, sa, sb);
   const float k = fd_kl_score(sa, sb, D);
   K0 = __shfl(k, 0, 64);
@@ -513,7 +513,7 @@ __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, 
   torch_sum2(f.D, lane, [&](int d, float& a, float& b) {
     a = sh.lv2[d] - lv1;
     const float df = sh.x[d] - sh.mu2[d];
-    b = (v1 + df * df) / sh.v2[d];
+    b = CWQ_KDIV((v1 + df * df), sh.v2[d]);
   }, sa, sb);
   return fd_kl_score(sa, sb, f.D);
 }
@@ -1093,16 +1093,16 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float delta = mb - ma;
           const float tot = c1 + c2;
           float m2 = (sa2 + sb2) + (delta * delta) * ((c1 * c2) / tot);
-          float m = (c1 * ma + c2 * mb) / tot;
+          float m = CWQ_KDIV((c1 * ma + c2 * mb), tot);
           const float cnt = tot + 1.0f;
           const float xd = sh.x[d];
           const float dl = xd - m;
-          m = m + dl / cnt;
+          m = m + CWQ_KDIV(dl, cnt);
           m2 = m2 + dl * (xd - m);
-          const float v1 = m2 / cnt + pv;
+          const float v1 = CWQ_KDIV(m2, cnt) + pv;
           a = sh.lv2[d] - ref_logf(v1);
           const float df = m - sh.mu2[d];
-          bb = (v1 + df * df) / sh.v2[d];
+          bb = CWQ_KDIV((v1 + df * df), sh.v2[d]);
         }, sa, sb);
         const float K = fd_kl_score(sa, sb, D);
         if (lane == 0) sh.cf[3] = K;

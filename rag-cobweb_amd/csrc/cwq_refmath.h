@@ -9,6 +9,15 @@
 
 namespace cwq {
 
+// The KL terms' float32 divisions.  FIT_PROBE_DIV (a timing-only variant build, never the
+// product: scripts/build_variant.py) swaps them for the hardware reciprocal to bound what
+// faster division could save.
+#ifdef FIT_PROBE_DIV
+#define CWQ_KDIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
+#else
+#define CWQ_KDIV(a, b) ((a) / (b))
+#endif
+
 // log: torch's float32 log (Sleef, 1-ulp) is the correctly rounded value for 99.96% of
 // inputs; a log computed to a few double ulps and rounded once is that value.  The library's
 // fp64 log was most of a clustered ifit's insert time, so: a 128-entry table on the top 7
@@ -86,6 +95,9 @@ static constexpr double kRefLogL[128] = {
     -0x1.c3177b4c75deep-7, -0x1.4192bb96832bfp-7, -0x1.8121bb458686fp-8, 0x0.0p+0};
 
 __host__ __device__ __forceinline__ float ref_logf(float v) {
+#if defined(FIT_PROBE_LOG) && defined(__HIP_DEVICE_COMPILE__)
+  return __logf(v);   // timing-only variant build (see CWQ_KDIV)
+#endif
   const uint32_t u = __builtin_bit_cast(uint32_t, v);
   if (u - 0x00800000u >= 0x7f000000u) return (float)log((double)v);   // not a positive normal
   const int i = (int)((u >> 16) & 127);
