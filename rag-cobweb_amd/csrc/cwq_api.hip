@@ -1823,6 +1823,18 @@ int stream_wgs(const cwq_index* ix) {
   return ix->cus * m;
 }
 
+// Workgroups per query of the per-call path's rerank tail (FwExpand::split): a few queries'
+// candidate lists (~1k rows per query after the int8 pass) reranked by one workgroup each
+// leave the chip idle, so up to kFwSplitMax per query, about one per CU in total.
+// CWQ_FW_SPLIT = n caps it (1: one workgroup per query).
+constexpr int kFwSplitMax = 32;
+int fw_split(const cwq_index* ix, int nq) {
+  int S = std::max(1, std::min(kFwSplitMax, ix->cus / std::max(nq, 1)));
+  if (const char* e = getenv("CWQ_FW_SPLIT"))
+    if (atoi(e) > 0) S = std::min(S, atoi(e));
+  return S;
+}
+
 int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                      hipStream_t s) {
   const int K = k, kl = k <= 16 ? 16 : 64;
@@ -1836,7 +1848,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                 (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)64 * nqc * 4 + (size_t)nqc * 4 +
                 (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
                 (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256 +
-                int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512;
+                int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512 +
+                (size_t)nqc * kFwSplitMax * 64 * 12 + 3 * 256;
   const bool ib = use_int_bounds(ix);
   // int8 pass on flat trees only: with bounded internal prefixes the ~9x exact reranks pay
   // the exact parent chains too (b4/L9 one query per call 692 -> 1166 us,
@@ -1872,6 +1885,10 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
+  const int fws = fw_split(ix, nqc);
+  float* fsk = b.take<float>((size_t)nqc * fws * 64);
+  float* fsa = b.take<float>((size_t)nqc * fws * 64);
+  int* fsr = b.take<int>((size_t)nqc * fws * 64);
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[0], s));
   // one fused prep launch when the exact internal pass is small (flat trees: the root)
   bool fused = !ib && ix->NI <= kSbMaxNI && (int)ix->levels.size() <= kSbMaxNI &&
@@ -2056,7 +2073,9 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   // one candidate list per query (no anisotropic rows): final_wide expands the top-K to
   // sentence ids and writes the host flags itself (no merge launch, no flag copy)
   const bool ftail = nst == 1 && final_wide_rows(ix->DP, capq) > 0 && !getenv("CWQ_FW_UNFUSED");
-  const FwExpand fx{ix->sent_ptr, ix->sent_ids, ids, scores, k, ix->hflags};
+  // okf / nex: the split tail's arrival count and exact-rerank sum (zeroed with the counters;
+  // the fused tail reports through hflags, not these)
+  const FwExpand fx{ix->sent_ptr, ix->sent_ids, ids, scores, k, ix->hflags, fws, fsk, fsa, fsr};
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, K, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta,
                       ix->row_par, c.P ? c.P : ix->dummy, c.pT ? 1 : c.ldP, 0, pkey, paux, prow, (int64_t)nst * K, okf,
                       nex, lkb, lrb, done, ib ? &chain : nullptr, 0, 0.f, s, ftail ? &fx : nullptr));

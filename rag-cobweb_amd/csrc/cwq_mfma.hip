@@ -2063,7 +2063,8 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   __shared__ float s_T2;
   __shared__ FwChainLds s_chain;   // exact parent chains (fw_chain_prefixes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = blockIdx.x;
+  const int S = fx.ids && fx.split > 1 ? fx.split : 1;   // workgroups per query (FwExpand::split)
+  const int q = blockIdx.x / S, sidx = blockIdx.x - q * S;
   const size_t base = (size_t)q * capq;
   // ---- one round trip: counters + the first window of the candidate lists ----
   const int n = qcnt[q];
@@ -2145,10 +2146,12 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     }
     const float T2 = s_T2;
     // survivors u >= T2, compacted by all waves (their order does not matter: the top-K
-    // list below is ordered by (key, row))
-    for (int j0 = wave * 64; j0 < n; j0 += kFwThreads) {
+    // list below is ordered by (key, row)); a split workgroup takes its slice of the list
+    const int per = S > 1 ? (n + S * 64 - 1) / (S * 64) * 64 : n;
+    const int jlo = min(n, sidx * per), jhi = min(n, jlo + per);
+    for (int j0 = jlo + wave * 64; j0 < jhi; j0 += kFwThreads) {
       const int j = j0 + lane;
-      const bool c = j < n && (j < kFwCand ? s_wu[j] : cu[base + j]) >= T2;
+      const bool c = j < jhi && (j < kFwCand ? s_wu[j] : cu[base + j]) >= T2;
       const uint64_t bm = __ballot(c);
       int o = 0;
       if (lane == 0 && bm) o = atomicAdd(&s_ns, __popcll(bm));
@@ -2311,6 +2314,39 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   __syncthreads();
   if (wave != 0) return;
   nx = s_nx;
+  if (S > 1) {
+    // split: this workgroup's list out; the last of the query's S workgroups (release /
+    // acquire at agent scope around the arrival count) merges the others' into its own
+    const size_t so = ((size_t)q * S + sidx) * 64 + lane;
+    fx.sk[so] = lk;
+    fx.sa[so] = la;
+    fx.sr[so] = lr;
+    if (lane == 0 && nx) atomicAdd(&n_exact[q], nx);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    int last = 0;
+    if (lane == 0) last = atomicAdd(&ok_flag[q], 1) == S - 1;
+    last = __shfl(last, 0, 64);
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (ok) {
+      for (int w = 0; w < S; ++w) {
+        if (w == sidx) continue;
+        const size_t o = ((size_t)q * S + w) * 64 + lane;
+        const float key = lane < K ? __builtin_nontemporal_load(&fx.sk[o]) : -CWQ_INF;
+        const float lp = __builtin_nontemporal_load(&fx.sa[o]);
+        const int rid = lane < K ? __builtin_nontemporal_load(&fx.sr[o]) : 0x7fffffff;
+        const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
+        const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+        uint64_t mask = __ballot(rid != 0x7fffffff && entry_before(key, lp, rid, tk, ta, tr, cat));
+        while (mask) {
+          const int b = __builtin_ctzll(mask);
+          mask &= mask - 1;
+          list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K, cat);
+        }
+      }
+    }
+    nx = __hip_atomic_load(&n_exact[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (fx.ids) {
     // merge_expand_kernel's expansion of the (already sorted) top-K rows, in place
     if (!ok) {
@@ -2385,7 +2421,9 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
   const int wide_max = we && *we ? atoi(we) : kFinalWideMaxQ;
   const size_t lds = final_wide_lds(DP, capq);
   if ((fx || nq <= wide_max) && lds <= (size_t)kFwDynMax) {
-    hipLaunchKernelGGL(final_wide_kernel, dim3((unsigned)nq), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
+    if (fe.split > 1 && (!fe.sk || !fe.sa || !fe.sr || !ok_flag || !n_exact)) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)nq * (unsigned)(fe.ids && fe.split > 1 ? fe.split : 1);
+    hipLaunchKernelGGL(final_wide_kernel, dim3(grid), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
                        qover, crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag,
                        n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst, fe,
                        getenv("CWQ_FW_ROWS") ? std::min(final_wide_rows(DP, capq), atoi(getenv("CWQ_FW_ROWS")))
