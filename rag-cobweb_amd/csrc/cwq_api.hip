@@ -139,7 +139,8 @@ struct cwq_index {
   // per-group bound constants.  prune_ctr: the last call's stage-B pair count (diagnostics).
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
-  int prn_max_chunks = 1;
+  int prn_gmax = 1;   // the most internal nodes of one pruning group
+  int* blk_grp = nullptr;   // per 16-row block of isotropic rows: the pruning group of all its rows (-1: mixed)
   int *gs_ptr = nullptr, *gs_rows = nullptr;   // per group: up to 64 usable isotropic rows (the seed threshold)
   GroupBound* gbound = nullptr;
   int* prune_ctr = nullptr;     // device [8]: per chunk pair count + claim counters, [4] the call's pair total
@@ -745,8 +746,8 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   std::vector<int> fillp(gptr.begin(), gptr.end() - 1);
   for (int i = 1; i < NI; ++i)
     if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
-  ix->prn_max_chunks = 1;
-  for (int g = 0; g < G; ++g) ix->prn_max_chunks = std::max(ix->prn_max_chunks, (gptr[g + 1] - gptr[g] + 63) / 64);
+  ix->prn_gmax = 1;
+  for (int g = 0; g < G; ++g) ix->prn_gmax = std::max(ix->prn_gmax, gptr[g + 1] - gptr[g]);
   // the seed threshold's rows: up to 64 usable isotropic rows of each group, spread over it
   std::vector<std::vector<int>> grows(G);
   for (int r = 0; r < ix->NL_iso; ++r)
@@ -759,6 +760,16 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   }
   if (srows2.empty()) srows2.push_back(0);
   if ((rc = ix->upload(&ix->gs_ptr, sptr2, s)) || (rc = ix->upload(&ix->gs_rows, srows2, s))) return rc;
+  // the per-call filter's blocks: a block is left out when its rows' one group is pruned
+  std::vector<int> bg((size_t)std::max<int64_t>(1, ((int64_t)ix->NL_iso + 15) / 16), -1);
+  for (int64_t b = 0; b * 16 < ix->NL_iso; ++b) {
+    const int r0 = (int)(b * 16), r1 = (int)std::min<int64_t>(ix->NL_iso, b * 16 + 16);
+    int g = rgrp[r0];
+    for (int r = r0 + 1; r < r1 && g >= 0; ++r)
+      if (rgrp[r] != g) g = -1;
+    bg[b] = g;
+  }
+  if ((rc = ix->upload(&ix->blk_grp, bg, s))) return rc;
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
       (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)) ||
       (rc = ix->alloc(&ix->prune_ctr, 8)))
@@ -1186,12 +1197,12 @@ bool use_prune(const cwq_index* ix) {
 size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 28 + 16 : 0; }
 
 // The pruned Fast chunk's internal pass, in place of run_internal + group_tables (four
-// launches, cwq_prune.hip): the group shifts and the bound terms; the root, KUB, g* and g*'s
-// exact pass and tables (stage A); the seed threshold from g*'s sample rows, the stage-B
-// pairs and the sentinel fill; stage B.  K: the call's top-K.  T0 (optional): the seed is
+// launches, cwq_prune.hip): the group shifts, the bound terms, the root, KUB and g* (head);
+// g*'s exact pass over many workgroups; g*'s tables, the seed threshold from its sample rows,
+// the stage-B pairs and the sentinel fill; stage B.  K: the call's top-K.  T0 (optional): the seed is
 // also written there (the per-call filter's threshold: no probe pass).
 int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipStream_t s, float* T0 = nullptr,
-                   int64_t ldT0 = 0) {
+                   int64_t ldT0 = 0, int* live = nullptr) {
   const int nq = c.nq, G = ix->G;
   PruneArgs pa;
   memset(&pa, 0, sizeof(pa));
@@ -1237,6 +1248,12 @@ int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipS
   pa.Tseed = c.Tseed;
   pa.T0 = T0;
   pa.ldT0 = ldT0;
+  pa.gnodes_max = ix->prn_gmax;
+  if (live) {   // the per-call filter's live block list (count in ctr[5])
+    pa.blk_grp = ix->blk_grp;
+    pa.nblk = ((int64_t)ix->NL_iso + 15) / 16;
+    pa.live = live;
+  }
   HIPCHK(launch_prune(pa, ix->cus, ix->prune_nq == 0, s));   // the call's first pruned chunk resets the total
   if (getenv("CWQ_PRUNE_DEBUG")) {   // diagnostics: the first queries' bounds and thresholds
     const int n = std::min(nq, 3);
@@ -1849,7 +1866,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                 (size_t)5 * nqc * 4 + (size_t)nqc * capq * 12 + (size_t)nqc * 64 * 16 +
                 (size_t)nqc * 4 * (round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024) + 32 * 256 +
                 int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512 +
-                (size_t)nqc * kFwSplitMax * 64 * 12 + 3 * 256;
+                (size_t)nqc * kFwSplitMax * 64 * 12 + 3 * 256 + (size_t)((ix->NL_iso + 15) / 16) * 4 + 256;
   const bool ib = use_int_bounds(ix);
   // int8 pass on flat trees only: with bounded internal prefixes the ~9x exact reranks pay
   // the exact parent chains too (b4/L9 one query per call 692 -> 1166 us,
@@ -1896,6 +1913,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                !getenv("CWQ_SB_UNFUSED");
   SbPrepArgs sp;
   const bool prn = !ib && use_prune(ix);
+  int* live = nullptr;   // group pruning: the filter's 16-row blocks
   if (prn) fused = false;
   if (fused) {
     memset(&sp, 0, sizeof(sp));
@@ -1953,8 +1971,10 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     if (ib) {
       if ((rc = run_internal_bounds(ix, c, q, kFgTile, b, s))) return rc;
     } else if (prn) {
-      // the seed threshold goes straight to the filter's T0: no probe pass
-      if ((rc = prune_internal(ix, c, q, K, b, s, tl + (K - 1), 64))) return rc;
+      // the seed threshold goes straight to the filter's T0: no probe pass; the filter pass
+      // covers the live blocks only
+      live = b.take<int>((size_t)std::max<int64_t>(1, (ix->NL_iso + 15) / 16));
+      if ((rc = prune_internal(ix, c, q, K, b, s, tl + (K - 1), 64, live))) return rc;
     } else if ((rc = run_internal(ix, c, s, false, q, 0))) {
       return rc;
     }
@@ -2016,6 +2036,8 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   a.T0 = tl;
   a.ldT0 = 64;
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[4], s));
+  const char* lve = getenv("CWQ_PRUNE_LIVE");   // 0: the pass over every block (A/B)
+  const bool use_live = live && !(lve && *lve && atoi(lve) == 0);
   // the select runs in the probe launch's last workgroup (one launch less per call);
   // CWQ_SELECT_UNFUSED=1 keeps select_kernel (same thresholds: both run select_wave)
   const bool fsel = !sel_unfused();
@@ -2062,7 +2084,12 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
     a8.rf = ix->iso_rf8;
     HIPCHK(launch_stream(a8, 0, stream_wgs(ix), s));
   } else {
-    HIPCHK(launch_stream(a, 0, stream_wgs(ix), s));
+    StreamArgs a0 = a;
+    if (use_live) {
+      a0.live = live;
+      a0.live_n = ix->prune_ctr + 5;
+    }
+    HIPCHK(launch_stream(a0, 0, stream_wgs(ix), s));
   }
   if (ix->timing) HIPCHK(hipEventRecord(ix->ev[6], s));
   int nst = 0;
@@ -2722,6 +2749,21 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta, ix->row_par,
                       BFk ? BFk : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, lstride, okf, nex, lkb, lrb,
                       done, nullptr, 1, dfull, s));
+  if (getenv("CWQ_CAT_DEBUG")) {   // diagnostics: per query candidates, overflow, threshold, certified
+    std::vector<int> hc(nqc), ho(nqc), hk(nqc), hx(nqc);
+    std::vector<float> ht(nqc), hl(64);
+    HIPCHK(hipMemcpyAsync(hc.data(), qcnt, nqc * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ho.data(), qover, nqc * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hk.data(), okf, nqc * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hx.data(), nex, nqc * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ht.data(), T, nqc * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hl.data(), tl, 64 * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < std::min(nqc, 4); ++i)
+      fprintf(stderr, "[cat stream] q %d R %d cand %d over %d T %.6g ok %d exact %d probe T0 %.6g | tl[R-2..R] %.6g %.6g\n",
+              i, R, hc[i], ho[i], ht[i], hk[i], hx[i], i == 0 ? hl[R - 1] : 0.f, i == 0 ? hl[R - 2] : 0.f,
+              i == 0 && R < 64 ? hl[R] : 0.f);
+  }
   return CWQ_OK;
 }
 

@@ -220,9 +220,17 @@ struct PruneArgs {
   const int* gs_ptr; const int* gs_rows; const float* Mf; const RowMeta* meta; const int* row_par;
   float* Tseed;                 // [nq]
   float* T0; int64_t ldT0;      // optional: also written (the per-call filter's threshold, no probe)
+  int gnodes_max;               // the most internal nodes of one group (g*'s pass: workgroups per query)
+  int zero_total;               // the head kernel also zeroes ctr[4] (the call's first pruned chunk)
+  // optional (the per-call filter): the 16-row blocks of the isotropic rows it must pass over
+  // -- blk_grp[b] the pruning group of all the block's rows (-1: mixed, or rows outside every
+  // group), kept when some query of the call keeps that group -- appended to live, count ctr[5]
+  const int* blk_grp; int64_t nblk;
+  int* live;
 };
-// launches: front (shifts + the P0-free bound terms), stage A (root, KUB, g*, g*'s exact pass
-// and prefixes), seed (T, stage-B pairs, sentinel fill), stage B (the pairs' exact passes)
+// launches: head (shifts, the bound terms, the root, KUB, g*; the counters zeroed), g*'s exact
+// pass (many workgroups per query), seed (g*'s prefixes and tables, T, stage-B pairs, sentinel
+// fill), stage B (the pairs' exact passes)
 hipError_t launch_prune(const PruneArgs& a, int cus, bool first, hipStream_t s);
 hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s);
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
@@ -634,6 +642,11 @@ struct StreamArgs {
   // then the categorize RowF (cat_rf) and P / Phi its group-term tables
   const float* BFk;
   int64_t ldBF;
+  // filter pass (MODE 0) over a list of 16-row blocks instead of all of them: live[0..*live_n)
+  // (group pruning: the blocks whose rows are all in groups pruned for every query of the call
+  // are left out, prune_stage_b_kernel)
+  const int* live;
+  const int* live_n;
   // probe with the query prep fused (flat trees, nq <= 16, bf16; fprep set): every workgroup
   // forms the bf16 query fragments, the {|x'|^2, |x_hi|, |x_lo|} terms and the root's exact
   // prefix itself (sb_prep_kernel's arithmetic), and workgroup 0 also writes them to Xb /

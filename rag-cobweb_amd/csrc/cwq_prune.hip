@@ -16,14 +16,14 @@
 //   evaluation of the exact keys (every bound below is on the fp32 values the exact pass and
 //   the rerank compute, not on real arithmetic).
 //
-// Stage A (before the filter's threshold exists): for each query only its best group g* =
-// argmax_g KUB gets the exact internal pass (prune_scan_kernel: the scan's arithmetic, bit
-// for bit) and exact prefixes; every other (query, node) gets the sentinel prefix kPruneSent
-// in the filters' tables, so its rows are never candidates and their lower bounds never
-// raise a threshold.  The filter's first threshold T[q] (the sample / probe pass: the K-th
-// largest lower bound over distinct rows, <= tau_K) then decides stage B: the groups with
-// KUB[q][g] >= T[q] get the exact pass too.  Every group left has KUB < T <= tau_K: none of
-// its rows can be in the top-K, so the result is the exact scan's bit for bit.
+// First (before the filter's threshold exists): for each query only its best group g* =
+// argmax_g KUB gets the exact internal pass (the scan's arithmetic, bit for bit) and exact
+// prefixes; every other (query, node) gets the sentinel prefix kPruneSent in the filters'
+// tables, so its rows are never candidates and their lower bounds never raise a threshold.
+// The seed threshold T[q] (the K-th largest exact key over up to 64 rows of g*, <= tau_K)
+// then decides stage B: the groups with KUB[q][g] >= T[q] get the exact pass too.  Every
+// group left has KUB < T <= tau_K: none of its rows can be in the top-K, so the result is the
+// exact scan's bit for bit.  Launches: head (bounds, root, g*), g*'s pass, seed, stage B.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -122,19 +122,14 @@ __device__ __forceinline__ void prune_write_prefix(const PruneArgs& a, int q, in
   a.Phi[o] = __double2float_ru(tt + e);
 }
 
-// Front: per (query, group), one wave: the group shift -2 x'.d_g and its error bound (as
-// group_shift_kernel), |x - c_g|^2, and the bound terms of KUB that do not depend on the
-// root's prefix P0: kpart[0] = max(Cmin UB, Cmax UB), kpart[1] = Cmax mag (the margin's).
+// The bound terms of one (query, group) pair, by one wave: the group shift -2 x'.d_g and its
+// error bound (as group_shift_kernel), |x - c_g|^2, and the terms of KUB that do not depend
+// on the root's prefix P0: kpart[0] = max(Cmin UB, Cmax UB), kpart[1] = Cmax mag (the margin's).
 //   every member a of g: S_a >= wmin (|x - c_g| - r_g)_+^2 in real arithmetic; the fp32 S
 //   >= (1 - 2^-16) (sqrt(wmin) dlo - 2^-23 sqrt(wmax) mmax)_+^2 (t = x A - B with B = fl(mu
 //   A), the partial sums' relative error < 64 * 2^-24); lp'_fp32 = fl(-0.5 fl(logdet + S))
 //   <= -logdet/2 + 2^-22 |logdet| - (1/2 - 2^-22) S_fp32 = UB; |lp'| <= mag.
-__global__ void prune_front_kernel(const PruneArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
-  if (w >= (int64_t)a.nq * a.G) return;
-  const int64_t qi = w / a.G;
-  const int g = (int)(w % a.G);
+__device__ __forceinline__ void prune_group_terms(const PruneArgs& a, int64_t qi, int g, int lane) {
   double d1 = 0.0, ab = 0.0, e2 = 0.0;
   for (int d = lane; d < a.D; d += 64) {
     const float x = a.q[qi * a.D + d];
@@ -175,75 +170,86 @@ __global__ void prune_front_kernel(const PruneArgs a) {
   a.kpart[(size_t)a.nq * a.G + o] = m2;
 }
 
-// The exact internal pass of one (query, group) pair by one workgroup: the query's slices in
-// LDS; per chunk of kPrChunk of the group's nodes every (node, 16-dim slice) partial in
-// parallel -- exact_aniso_S's fma chain -- and one thread per node adding them in slice
-// order (the scan kernel's raw sums bit for bit); then the nodes' prefixes and tables.
-constexpr int kPrThreads = 512, kPrChunk = 128;
-__device__ void prune_pair(const PruneArgs& a, int q, int g, float* s_x, float* s_part) {
+// S of cnt nodes of a group's list from position c0, for query q (its slices in s_x): every
+// (node, 16-dim slice) partial in parallel -- exact_aniso_S's fma chain -- and one thread per
+// node adding them in slice order (the scan kernel's raw sums bit for bit).  NT threads.
+template <int NT>
+__device__ __forceinline__ void prune_nodes_S(const PruneArgs& a, int q, int c0, int cnt, const float* s_x,
+                                              float* s_part) {
   const int tid = threadIdx.x;
   const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  for (int it = tid; it < cnt * NV16; it += NT) {
+    const int e = it / NV16, v = it - e * NV16;
+    const int node = a.gi_nodes[c0 + e];
+    const float* __restrict__ ar = a.Ar + (size_t)node * a.DP + v * 16;
+    const float* __restrict__ br = a.Br + (size_t)node * a.DP + v * 16;
+    float4 a4[4], b4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
+      b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
+    }
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 ta = a4[j >> 2], tb = b4[j >> 2];
+      const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
+      const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
+      const float tt = fmaf(s_x[v * 16 + j], aj, -bj);
+      part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+    }
+    s_part[e * LDP + v] = part;
+  }
+  __syncthreads();
+  if (tid < cnt) {
+    float acc = 0.f;
+    for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+    a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
+  }
+  __syncthreads();
+}
+
+// The query's padded slices into LDS.
+__device__ __forceinline__ void prune_load_query(const PruneArgs& a, int q, float* s_x, int nt) {
+  const int NV16 = a.DP / 16;
   const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
-  for (int d = tid; d < a.DP; d += kPrThreads) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+  for (int d = threadIdx.x; d < a.DP; d += nt) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+}
+
+// The exact internal pass of one (query, group) pair by one workgroup (stage B): the nodes'
+// raw sums in chunks of kPrChunk, then their prefixes and tables.
+constexpr int kPrThreads = 512, kPrChunk = 128;
+__device__ void prune_pair(const PruneArgs& a, int q, int g, float* s_x, float* s_part) {
+  prune_load_query(a, q, s_x, kPrThreads);
   __syncthreads();
   const int b0 = a.gi_ptr[g], b1 = a.gi_ptr[g + 1];
-  for (int c0 = b0; c0 < b1; c0 += kPrChunk) {
-    const int cnt = min(kPrChunk, b1 - c0);
-    for (int it = tid; it < cnt * NV16; it += kPrThreads) {
-      const int e = it / NV16, v = it - e * NV16;
-      const int node = a.gi_nodes[c0 + e];
-      const float* __restrict__ ar = a.Ar + (size_t)node * a.DP + v * 16;
-      const float* __restrict__ br = a.Br + (size_t)node * a.DP + v * 16;
-      float4 a4[4], b4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
-        b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
-      }
-      float part;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float4 ta = a4[j >> 2], tb = b4[j >> 2];
-        const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
-        const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
-        const float tt = fmaf(s_x[v * 16 + j], aj, -bj);
-        part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
-      }
-      s_part[e * LDP + v] = part;
-    }
-    __syncthreads();
-    if (tid < cnt) {
-      float acc = 0.f;
-      for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
-      a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
-    }
-    __syncthreads();
-  }
+  for (int c0 = b0; c0 < b1; c0 += kPrChunk) prune_nodes_S<kPrThreads>(a, q, c0, min(kPrChunk, b1 - c0), s_x, s_part);
   // the raw sums complete and visible before the chain walks read them back
   __threadfence();
   __syncthreads();
-  for (int j = b0 + tid; j < b1; j += kPrThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
+  for (int j = b0 + (int)threadIdx.x; j < b1; j += kPrThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
   __syncthreads();   // s_x reused by the next pair
 }
 
 size_t prune_pair_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
 
-// Stage A, one workgroup per query: the root's raw sum (exact_aniso_S's arithmetic, bit for
-// bit), its prefix P0 and the root's tables; KUB[q][g] = max(iLmin P0, iLmax P0) + kpart +
-// 2^-16 (iLmax |P0| + Cmax mag) (the exact key's fp32 chain: <= 64 fmaf steps and the final
-// fmaf, < 2^-17 of its terms), rounded up; g* = argmax (ties: the smaller g); then g*'s
-// exact pass and prefixes (prune_pair).
-__global__ __launch_bounds__(kPrThreads) void prune_stage_a_kernel(const PruneArgs a) {
-  extern __shared__ float s_dyn[];
-  float* s_x = s_dyn;
-  float* s_part = s_dyn + a.DP;
+// Head, one workgroup per query: every group's bound terms (one wave per group,
+// prune_group_terms); the root's raw sum (exact_aniso_S's arithmetic, bit for bit), its
+// prefix P0 and the root's tables; KUB[q][g] = max(iLmin P0, iLmax P0) + kpart + 2^-16 (iLmax
+// |P0| + Cmax mag) (the exact key's fp32 chain: <= 64 fmaf steps and the final fmaf, < 2^-17
+// of its terms), rounded up; g* = argmax (ties: the smaller g).  Block 0 zeroes the pair and
+// claim counters (and the call's total on its first pruned chunk).
+constexpr int kHdThreads = 512;
+__global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs a) {
+  __shared__ float s_root[128];   // DP <= 2048
   __shared__ float s_p0;
-  __shared__ double s_best[kPrThreads / 64];
-  __shared__ int s_bg[kPrThreads / 64];
+  __shared__ double s_best[kHdThreads / 64];
+  __shared__ int s_bg[kHdThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
   const int NV16 = a.DP / 16;
-  // the root: 16-dim partials in parallel, added in slice order by thread 0
+  if (q == 0 && tid < 6 && (tid != 4 || a.zero_total)) a.ctr[tid] = 0;
+  // the root: 16-dim partials in parallel (added in slice order by thread 0 below)
   const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
   if (tid < NV16) {
     const int v = tid;
@@ -253,12 +259,13 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_a_kernel(const PruneAr
       const float tt = fmaf(xq[(size_t)v * kXQ * 16 + j], a.Ar[v * 16 + j], -a.Br[v * 16 + j]);
       part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
     }
-    s_dyn[v] = part;
+    s_root[v] = part;
   }
+  for (int g = wave; g < a.G; g += kHdThreads / 64) prune_group_terms(a, q, g, lane);
   __syncthreads();
   if (tid == 0) {
     float acc = 0.f;
-    for (int v = 0; v < NV16; ++v) acc += s_dyn[v];
+    for (int v = 0; v < NV16; ++v) acc += s_root[v];
     a.S[(size_t)q * a.ldS] = acc;
     const float lp = -0.5f * (a.logdet_int[0] + acc);
     const float P0 = a.w_int[0] * lp;
@@ -268,11 +275,12 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_a_kernel(const PruneAr
     a.Plo[o] = P0;
     a.Phi[o] = P0;
   }
+  __threadfence();   // the waves' kpart stores, read back by other waves below
   __syncthreads();
   const double P0 = (double)s_p0;
   double best = -INFINITY;
   int bg = 0x7fffffff;
-  for (int g = tid; g < a.G; g += kPrThreads) {
+  for (int g = tid; g < a.G; g += kHdThreads) {
     const GroupBound b = a.gb[g];
     const size_t o = (size_t)q * a.G + g;
     double kub = -INFINITY;
@@ -300,22 +308,36 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_a_kernel(const PruneAr
   }
   __syncthreads();
   if (tid == 0) {
-    for (int w = 1; w < kPrThreads / 64; ++w)
+    for (int w = 1; w < kHdThreads / 64; ++w)
       if (s_best[w] > best || (s_best[w] == best && s_bg[w] < bg)) {
         best = s_best[w];
         bg = s_bg[w];
       }
-    s_bg[0] = bg == 0x7fffffff ? -1 : bg;
-    a.gstar[q] = s_bg[0];
+    a.gstar[q] = bg == 0x7fffffff ? -1 : bg;
   }
+}
+
+// g*'s exact pass: kGsNodes of its nodes per workgroup, nb workgroups per query (the
+// workgroups past g*'s list leave at once) -- the per-call path's one query then reads its
+// best group's ~100s of node rows with a few dozen CUs instead of one.
+constexpr int kGsNodes = 16, kGsThreads = 256;
+__global__ __launch_bounds__(kGsThreads) void prune_gstar_kernel(const PruneArgs a, int nb) {
+  extern __shared__ float s_dyn[];
+  float* s_x = s_dyn;
+  float* s_part = s_dyn + a.DP;
+  const int q = blockIdx.x / nb, blk = blockIdx.x - q * nb;
+  const int g = a.gstar[q];
+  if (g < 0) return;
+  const int c0 = a.gi_ptr[g] + blk * kGsNodes, b1 = a.gi_ptr[g + 1];
+  if (c0 >= b1) return;
+  prune_load_query(a, q, s_x, kGsThreads);
   __syncthreads();
-  const int g = s_bg[0];
-  if (g >= 0) prune_pair(a, q, g, s_x, s_part);
+  prune_nodes_S<kGsThreads>(a, q, c0, min(kGsNodes, b1 - c0), s_x, s_part);
 }
 
 // Seed threshold and stage-B pairs, one workgroup per query (blocks >= nq: the sentinel fill
 // of every (query, node) outside the root and g*).  The exact keys of up to 64 sample rows of
-// g* (their parents' prefixes are stage A's): every (row, slice) partial in parallel, summed
+// g* (their parents' prefixes: written first, from prune_gstar_kernel's raw sums): every (row, slice) partial in parallel, summed
 // in slice order and finished by iso_key_tail -- the rerank's keys bit for bit -- so T = the
 // K-th largest over distinct rows is <= tau_K (fewer than K rows: -inf).  Then the groups
 // g != g* with KUB >= T go to the pair list.
@@ -339,6 +361,13 @@ __global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArg
   const int q = blockIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NV16 = a.DP / 16, LDP = NV16 + 1;
   const int g = a.gstar[q];
+  // g*'s prefixes and tables (its raw sums: prune_gstar_kernel), read back below by the
+  // sample rows whose parents they are
+  if (g >= 0) {
+    for (int j = a.gi_ptr[g] + tid; j < a.gi_ptr[g + 1]; j += kSeedThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
+    __threadfence();
+  }
+  __syncthreads();
   const int n = g >= 0 ? min(64, a.gs_ptr[g + 1] - a.gs_ptr[g]) : 0;
   const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
   for (int it = tid; it < n * NV16; it += kSeedThreads) {
@@ -395,13 +424,41 @@ __global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArg
   }
 }
 
+// Group g kept for query q: g*, or a valid group whose KUB reaches the seed threshold (the
+// seed kernel's pair test).
+__device__ __forceinline__ bool prune_kept(const PruneArgs& a, int q, int g) {
+  if (g == a.gstar[q]) return true;
+  if (!a.gb[g].valid) return false;
+  const float T = a.Tseed[q];
+  return a.kub[(size_t)q * a.G + g] >= T || !(T == T);
+}
+
 // Stage B: persistent workgroups claim the pairs; every workgroup leaves when the claim
-// counter passes the pair count.
+// counter passes the pair count.  First (blk_grp set) the live list of 16-row blocks for the
+// filter pass: one thread per block, appended in any order (the candidate lists' order does
+// not reach the results: the rerank orders by key and row).
 __global__ __launch_bounds__(kPrThreads) void prune_stage_b_kernel(const PruneArgs a) {
   extern __shared__ float s_dyn[];
   float* s_x = s_dyn;
   float* s_part = s_dyn + a.DP;
   __shared__ int s_p;
+  if (a.blk_grp) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t b0 = (int64_t)blockIdx.x * kPrThreads; b0 < a.nblk; b0 += (int64_t)gridDim.x * kPrThreads) {
+      const int64_t b = b0 + threadIdx.x;
+      bool keep = false;
+      if (b < a.nblk) {
+        const int g = a.blk_grp[b];
+        keep = g < 0;
+        for (int q = 0; q < a.nq && !keep; ++q) keep = prune_kept(a, q, g);
+      }
+      const uint64_t m = __ballot(keep);
+      int base = 0;
+      if (lane == 0 && m) base = atomicAdd(&a.ctr[5], __popcll(m));
+      base = __shfl(base, 0, 64);
+      if (keep) a.live[base + __popcll(m & ((1ull << lane) - 1))] = (int)b;
+    }
+  }
   const int npairs = a.ctr[0];
   for (;;) {
     if (threadIdx.x == 0) s_p = atomicAdd(&a.ctr[3], 1);
@@ -414,18 +471,22 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_b_kernel(const PruneAr
   }
 }
 
-// The whole pruned internal pass of a chunk: front, stage A, seed (+ fill), stage B.
-// ctr[0..3] zeroed here, and ctr[4] (the call's stage-B pair total) on its first pruned chunk.
-hipError_t launch_prune(const PruneArgs& a, int cus, bool first, hipStream_t s) {
-  if (a.nq <= 0) return hipSuccess;
-  if (a.DP % 16 || a.DP / 16 > kPrThreads) return hipErrorInvalidValue;
-  if (hipError_t e = hipMemsetAsync(a.ctr, 0, (first ? 5 : 4) * sizeof(int), s)) return e;
-  const int64_t nw = (int64_t)a.nq * a.G;
-  hipLaunchKernelGGL(prune_front_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(prune_stage_a_kernel, dim3((unsigned)a.nq), dim3(kPrThreads), prune_pair_lds(a.DP), s, a);
+// The whole pruned internal pass of a chunk: head, g*'s pass, seed (+ fill), stage B.
+// ctr[0..3] zeroed by the head, and ctr[4] (the call's stage-B pair total) on its first
+// pruned chunk.
+hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s) {
+  if (a0.nq <= 0) return hipSuccess;
+  if (a0.DP % 16 || a0.DP / 16 > 128 || a0.gnodes_max < 1) return hipErrorInvalidValue;
+  PruneArgs a = a0;
+  a.zero_total = first ? 1 : 0;
+  hipLaunchKernelGGL(prune_head_kernel, dim3((unsigned)a.nq), dim3(kHdThreads), 0, s, a);
+  const int nb = (a.gnodes_max + kGsNodes - 1) / kGsNodes;
+  hipLaunchKernelGGL(prune_gstar_kernel, dim3((unsigned)((int64_t)a.nq * nb)), dim3(kGsThreads),
+                     ((size_t)a.DP + (size_t)kGsNodes * (a.DP / 16 + 1)) * 4, s, a, nb);
   const int64_t nfill = ((int64_t)a.nq * a.NI + kSeedThreads - 1) / kSeedThreads;
   hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads),
                      (size_t)64 * (a.DP / 16 + 1) * 4, s, a);
+  const int64_t nw = (int64_t)a.nq * a.G;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(nw, cus));
   hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_pair_lds(a.DP), s, a);
   return hipGetLastError();

@@ -209,7 +209,10 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
   for (int qb = 0; qb < MQB; ++qb)
     proot[qb] = (MODE == 2 && qok[qb]) ? a.root_w * (-0.5f * (a.root_ld + a.Sroot[qb * 16 + (lane & 15)])) : 0.f;
-  const int64_t ngroups = MODE == 1 ? a.n_probe : (int64_t)((a.nrows + 15) >> 4);
+  // groups of the pass: the probe's sampled groups, the live block list (group pruning), or
+  // every 16-row block
+  const bool lst = MODE == 0 && a.live;
+  const int64_t ngroups = MODE == 1 ? a.n_probe : lst ? (int64_t)*a.live_n : (int64_t)((a.nrows + 15) >> 4);
   const int64_t gstride = (int64_t)gridDim.x * SK_WAVES;
   const int c16 = lane >> 4, r16 = lane & 15;
   // probe: max of the lower bounds per query over the current group
@@ -224,13 +227,16 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
   for (int qb = 0; qb < MQB; ++qb) cP[qb] = cPh[qb] = 0.f, cB[qb] = CWQ_INF;
   const float* Pu = a.Phi ? a.Phi : a.P;
-  auto panel = [&](int64_t gi) {
-    const int64_t grp = MODE == 1 ? gi * a.probe_stride : gi;
-    return reinterpret_cast<const char*>(a.Mb) + (size_t)(grp * 16 + r16) * a.DPB * ES + 16 * c16;
+  // the wave's groups are numbered gi; a group's 16-row block (its rows blk * 16 ..): the probe's
+  // every probe_stride-th, or the live list's entry (a wave-uniform scalar load, issued one
+  // group ahead so the next group's first loads never wait for it)
+  auto bmap = [&](int64_t g) -> int64_t { return MODE == 1 ? g * a.probe_stride : lst ? (int64_t)a.live[g] : g; };
+  auto panel = [&](int64_t blk) {
+    return reinterpret_cast<const char*>(a.Mb) + (size_t)(blk * 16 + r16) * a.DPB * ES + 16 * c16;
   };
   // row terms of the rows this lane's accumulator columns hold (r0 + 4*c16 + j)
-  auto load_rf = [&](RowF (&dst)[4], int64_t g) {
-    const int64_t r0n = (MODE == 1 ? g * a.probe_stride : g) * 16;
+  auto load_rf = [&](RowF (&dst)[4], int64_t blk) {
+    const int64_t r0n = blk * 16;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t r = r0n + 4 * c16 + j;
@@ -240,6 +246,8 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   int64_t gi = (int64_t)blockIdx.x * SK_WAVES + wave;
   const bool idle = gi >= ngroups;   // no group for this wave (the filter's flush barrier follows)
   if (idle) gi = 0;
+  int64_t bcur = idle ? 0 : bmap(gi);
+  int64_t bnxt = (!idle && gi + gstride < ngroups) ? bmap(gi + gstride) : 0;
   // K runs in chunks of CH fragments (16 B per lane each: row r0 + (lane & 15),
   // k = ks*32 + 8*(lane >> 4)) over the wave's whole (group, chunk) sequence.  Two
   // register buffers alternate chunk by chunk: the loads of the next chunk (after a
@@ -275,11 +283,11 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       }
     }
   };
-  issue(bA, panel(gi), min(CH, nk));
+  issue(bA, panel(bcur), min(CH, nk));
   // the group's row terms are loaded at its start and used at its end (in flight with
   // its chunks)
   RowF rf[4];
-  load_rf(rf, gi);
+  load_rf(rf, bcur);
   int tlive[MQB];
   bool live = false;
   auto load_live = [&](int it) {
@@ -304,7 +312,8 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       cn = 0;
     }
     const bool more = gn < ngroups;
-    issue(oth, more ? panel(gn) + cn * 64 : panel(gi) + c0 * 64, more ? min(CH, nk - cn) : min(CH, nk - c0));
+    issue(oth, more ? panel(cn == 0 ? bnxt : bcur) + cn * 64 : panel(bcur) + c0 * 64,
+          more ? min(CH, nk - cn) : min(CH, nk - c0));
     mma(cur, c0);
     if (cn != 0) {
       c0 = cn;
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
     // ---- group gi done.  Epilogue: rigorous bounds per (row, query); acc[qb][j] = dot
     // of row r0 + 4*c16 + j with query qb*16 + (lane & 15)
-    const int64_t r0 = (MODE == 1 ? gi * a.probe_stride : gi) * 16;
+    const int64_t r0 = bcur * 16;
     if (live) {
 #pragma unroll
       for (int qb = 0; qb < MQB; ++qb) Tq[qb] = fmaxf(Tq[qb], ord2f(tlive[qb]));
@@ -418,7 +427,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     if (!more) return false;
     gi = gn;
     c0 = 0;
-    load_rf(rf, gi);
+    bcur = bnxt;
+    bnxt = gi + gstride < ngroups ? bmap(gi + gstride) : 0;
+    load_rf(rf, bcur);
     load_live(++it);
 #pragma unroll
     for (int qb = 0; qb < MQB; ++qb) acc[qb] = acc_t{0, 0, 0, 0};

@@ -58,6 +58,9 @@ def main():
                     help="run the Fast legs with group pruning off (CWQ_GROUP_PRUNE=0) and on, in one process")
     ap.add_argument("--legs", default="all",
                     help="list (comma or +) of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
+    ap.add_argument("--env-ab", default=None,
+                    help="';'-separated variants of '&'-separated KEY=VAL (read per call): Fast one query per call "
+                         "(nq = 1, 64) under each, interleaved over 3 rounds, after the other legs")
     ap.add_argument("--save-struct", default=None,
                     help="write the ifit tree's structure (BFS parent, node of each row) to this .npz")
     ap.add_argument("--load-struct", default=None,
@@ -117,7 +120,37 @@ def main():
             fast_legs(args, w, ix, Q, Qn, pick, k)
     if not args.fast_only:
         basic_legs(args, w, ix, Q, Qn, k)
+    if args.env_ab:
+        env_ab(args, w, ix, Q, Qn, k)
     print("done", flush=True)
+
+
+def env_ab(args, w, ix, Q, Qn, k):
+    variants = []
+    for v in args.env_ab.split(";"):
+        variants.append(dict(kv.split("=", 1) for kv in v.split("&") if kv.strip()))
+    keys = sorted({key for v in variants for key in v})
+    ix.set_filter(0)
+    ids0, _ = ix.score_topk(Q, k)
+    ix.set_filter(-1)
+    for r in range(3):
+        for v in variants:
+            for key in keys:
+                os.environ.pop(key, None)
+            os.environ.update(v)
+            print(f"-- round {r} env {v or 'default'}", flush=True)
+            for nq in (1, 64):
+                fast_percall(args, ix, Q, k, ids0, nq)
+            if "bpc" in args.legs.replace("+", ","):
+                ts = []
+                for i in range(100):
+                    t0 = time.perf_counter()
+                    w.cobweb_predict(Qn[i % args.nq], k)
+                    ts.append(time.perf_counter() - t0)
+                ts.sort()
+                print(f"Basic per call cobweb_predict(numpy, {k}): median {ts[50] * 1e6:.1f} us", flush=True)
+    for key in keys:
+        os.environ.pop(key, None)
 
 
 def want(args, leg):

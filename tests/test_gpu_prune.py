@@ -159,3 +159,34 @@ def test_no_prune_with_negative_level_weight(gpu):
     assert not ix.last_prune_stats()["available"]
     assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
     ix.close()
+
+
+def test_live_block_list_equals_full_pass(gpu, monkeypatch):
+    """The per-call filter passes over the live 16-row blocks only (blocks whose rows all lie
+    in groups pruned for every query of the call are left out, prune_stage_b_kernel): same
+    ids and scores as the pass over every block (CWQ_PRUNE_LIVE=0) and as the exact scan,
+    for 1 / 8 / 64 queries per call, queries inside and between clusters."""
+    X, lab, Q, C = clustered(50_000, 96, 120, 58, nq=128)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(59)
+    a = torch.randint(0, 120, (64,), generator=g, device="cuda:0")
+    mid = (0.5 * C[a] + 0.5 * C[(a + 7) % 120]).contiguous()
+    Q = torch.cat([Q, mid]).contiguous()
+    t = gpu.synth.two_level_synth(X, lab)
+    ix = gpu.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], device="cuda:0")
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, 10)
+    ix.set_filter(-1)
+    for nq in (1, 8, 64):
+        for a0 in range(0, Q.shape[0], max(nq, 16)):
+            q = Q[a0:a0 + nq].contiguous()
+            out = {}
+            for v in ("0", "1"):
+                monkeypatch.setenv("CWQ_PRUNE_LIVE", v)
+                ids, sc = ix.score_topk(q, 10)
+                assert ix.last_stats()["path"] == "stream" and ix.last_prune_stats()["queries"] == q.shape[0]
+                out[v] = (ids, sc)
+            m = q.shape[0]
+            assert torch.equal(out["0"][0], ids0[a0:a0 + m]) and torch.equal(out["0"][1], s0[a0:a0 + m]), (nq, a0)
+            assert torch.equal(out["1"][0], ids0[a0:a0 + m]) and torch.equal(out["1"][1], s0[a0:a0 + m]), (nq, a0)
+    ix.close()
