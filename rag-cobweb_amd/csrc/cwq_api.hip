@@ -1840,13 +1840,14 @@ int stream_wgs(const cwq_index* ix) {
   return ix->cus * m;
 }
 
-// Workgroups per query of the per-call path's rerank tail (FwExpand::split): a few queries'
-// candidate lists (~1k rows per query after the int8 pass) reranked by one workgroup each
-// leave the chip idle, so up to kFwSplitMax per query, about one per CU in total.
-// CWQ_FW_SPLIT = n caps it (1: one workgroup per query).
+// Workgroups per query of the per-call path's rerank tail (FwExpand::split): after the int8
+// pass a query's ~1k-row candidate list reranked by one workgroup leaves the chip idle, so
+// up to kFwSplitMax per query, about one per CU in total (C3 one query per call 267 -> 262
+// us); the bf16 pass's lists are short and the split's merge costs more than it saves (C2:
+// 142 -> 154 us, profiles/r05_c2_probe_envab_v1.log), so one there.  CWQ_FW_SPLIT = n caps it.
 constexpr int kFwSplitMax = 32;
-int fw_split(const cwq_index* ix, int nq) {
-  int S = std::max(1, std::min(kFwSplitMax, ix->cus / std::max(nq, 1)));
+int fw_split(const cwq_index* ix, int nq, bool i8) {
+  int S = i8 ? std::max(1, std::min(kFwSplitMax, ix->cus / std::max(nq, 1))) : 1;
   if (const char* e = getenv("CWQ_FW_SPLIT"))
     if (atoi(e) > 0) S = std::min(S, atoi(e));
   return S;
@@ -1902,7 +1903,7 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
-  const int fws = fw_split(ix, nqc);
+  const int fws = fw_split(ix, nqc, i8);
   float* fsk = b.take<float>((size_t)nqc * fws * 64);
   float* fsa = b.take<float>((size_t)nqc * fws * 64);
   int* fsr = b.take<int>((size_t)nqc * fws * 64);
@@ -2670,9 +2671,15 @@ namespace {
 // list_before<true> in final_wide.  BFk: the chunk's BF (list 1) or the second-level T2
 // (the two-level replay's list 2).  The list goes to slot 0 of pkey/paux/prow (stride lstride),
 // the per-query certified flags to okf (a query whose candidates overflow: 0).
+// the probe's 16-row groups for a list of R and the per-row bound lines they fill
+int64_t cat_n_probe(const cwq_index* ix, int R) {
+  const int64_t ngroups = (ix->NL_iso + 15) / 16;
+  return std::min<int64_t>(std::max<int64_t>((int64_t)3 * R * ngroups / 1024, (int64_t)8 * R), ngroups);
+}
+int64_t cat_ldlb(const cwq_index* ix, int R) { return round_up(cat_n_probe(ix, R) * 16 + 1, 1024) + 1024; }
 size_t stream_cat_bytes(const cwq_index* ix, int nqc) {
   const int nq16 = (nqc + 15) / 16 * 16;
-  const int64_t ldlb = round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024;
+  const int64_t ldlb = cat_ldlb(ix, 64);
   return (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)nqc * 4 + (size_t)(5 * nqc + 1) * 4 +
          (size_t)nqc * kFgCapQ * 12 + (size_t)nqc * 64 * 16 + (size_t)nqc * ldlb * 4 + 16 * 256;
 }
@@ -2698,7 +2705,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   float* cl = b.take<float>((size_t)nqc * capq);
   float* lkb = b.take<float>((size_t)nqc * 64);
   int* lrb = b.take<int>((size_t)nqc * 64);
-  const int64_t ldlb = round_up((ix->NL_iso + 15) / 16 + 1, 1024) + 1024;
+  const int64_t ldlb = cat_ldlb(ix, R);   // every probed row's bound (probe_rows)
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
@@ -2733,9 +2740,10 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   a.cu = cu;
   a.cl = cl;
   const int64_t ngroups = (ix->NL_iso + 15) / 16;
-  int64_t n_probe = std::min<int64_t>(std::max<int64_t>((int64_t)3 * R * ngroups / 1024, (int64_t)8 * R), ngroups);
+  const int64_t n_probe = cat_n_probe(ix, R);
   a.probe_stride = std::max<int64_t>(1, ngroups / std::max<int64_t>(n_probe, 1));
   a.n_probe = std::min<int64_t>(n_probe, (ngroups + a.probe_stride - 1) / a.probe_stride);
+  a.probe_rows = getenv("CWQ_CAT_PROBE_MAX") ? 0 : 1;   // 1: group maxima (A/B)
   a.lb = lb;
   a.ldlb = ldlb;
   a.T0 = tl;
@@ -2745,6 +2753,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   a.sel_lr = tr;
   HIPCHK(launch_stream(a, 1, (int)std::max<int64_t>(1, std::min<int64_t>(ix->cus, (a.n_probe + 7) / 8)), s));
   a.sel_ctr = nullptr;
+  a.probe_rows = 0;
   HIPCHK(launch_stream(a, 0, stream_wgs(ix), s));
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta, ix->row_par,
                       BFk ? BFk : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, lstride, okf, nex, lkb, lrb,

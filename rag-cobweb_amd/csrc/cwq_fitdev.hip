@@ -209,8 +209,11 @@ struct FdShared {
   float tg[kFdWaves][2], tn[kFdWaves][2];
   double tr[kFdWaves][2];
   int ti[kFdWaves][2];
+  double logl[128];   // ref_logf's tables (kRefLogL, kRefLogC), copied in at launch
+  float logc[128];
 };
 static_assert(sizeof(FdShared) <= 160 * 1024, "the fit workgroup's LDS");
+__device__ __forceinline__ float fd_logf(const FdShared& sh, float v) { return ref_logf_tab(v, sh.logc, sh.logl); }
 
 
 __device__ __forceinline__ int ld_agent(const int* p) {
@@ -463,7 +466,7 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
     const float mu1 = h ? m : mm;
     const float num = h ? m2 : m2 + delta * (xd - mm);
     const float v1 = CWQ_KDIV(num, (h ? cc : cnt)) + pv;
-    a = sh.lv2[d] - ref_logf(v1);
+    a = sh.lv2[d] - fd_logf(sh, v1);
     const float df = mu1 - sh.mu2[d];
     b = CWQ_KDIV((v1 + df * df), sh.v2[d]);
   }, sa, sb);
@@ -472,7 +475,7 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
   T = __shfl(k, 32, 64);
 }
 // KL(c || ref) with the reference vectors (mu, v, log v) given
-__device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, const float* v, const float* lv, int c,
+__device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, const float* mu, const float* v, const float* lv, int c,
                                            int lane) {
 #pragma clang fp contract(off)
   const int D = f.D;
@@ -480,14 +483,14 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const float* mu, con
   float sa, sb;
   torch_sum2(D, lane, [&](int d, float& a, float& b) {
     const float mu1 = f.mean[(size_t)c * D + d], v1 = CWQ_KDIV(f.meanSq[(size_t)c * D + d], cc) + f.pv;
-    a = lv[d] - ref_logf(v1);
+    a = lv[d] - fd_logf(sh, v1);
     const float df = mu1 - mu[d];
     b = CWQ_KDIV((v1 + df * df), v[d]);
   }, sa, sb);
   return fd_kl_score(sa, sb, D);
 }
 // KL(c0 || ref) and KL(c1 || ref) in one wave (c0 on lanes 0-31, c1 on lanes 32-63)
-__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const float* mu, const float* v, const float* lv, int c0,
+__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const FdShared& sh, const float* mu, const float* v, const float* lv, int c0,
                                            int c1, int lane, float& K0, float& K1) {
 #pragma clang fp contract(off)
   const int D = f.D;
@@ -496,7 +499,7 @@ __device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const float* mu, con
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     const size_t o = (size_t)(h ? c1 : c0) * D + d;
     const float mu1 = f.mean[o], v1 = CWQ_KDIV(f.meanSq[o], (h ? cc1 : cc0)) + f.pv;
-    a = lv[d] - ref_logf(v1);
+    a = lv[d] - fd_logf(sh, v1);
     const float df = mu1 - mu[d];
     b = CWQ_KDIV((v1 + df * df), v[d]);
   }, sa, sb);
@@ -509,7 +512,7 @@ __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, 
 #pragma clang fp contract(off)
   float sa, sb;
   const float v1 = 0.f + f.pv;
-  const float lv1 = ref_logf(v1);
+  const float lv1 = fd_logf(sh, v1);
   torch_sum2(f.D, lane, [&](int d, float& a, float& b) {
     a = sh.lv2[d] - lv1;
     const float df = sh.x[d] - sh.mu2[d];
@@ -529,7 +532,7 @@ __device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh
     st_agent_f(&f.kres[2 * j], U);
     st_agent_f(&f.kres[2 * j + 1], T);
   } else {
-    const float K = fd_kl_ref(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
+    const float K = fd_kl_ref(f, sh, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
     st_agent_f(&f.kres[kofs + j], K);
   }
 }
@@ -801,6 +804,11 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
 #pragma clang fp contract(off)
   extern __shared__ char fd_smem[];
   FdShared& sh = *reinterpret_cast<FdShared*>(fd_smem);
+  for (int i = threadIdx.x; i < 128; i += kFdThreads) {
+    sh.logc[i] = kRefLogC[i];
+    sh.logl[i] = kRefLogL[i];
+  }
+  __syncthreads();
   if (blockIdx.x > 0) {   // a helper of the chip-wide KL passes
     fd_helper(f, sh, X);
     return;
@@ -877,7 +885,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         fd_insert_mv(cP, f.mean[(size_t)cur * D + d], f.meanSq[(size_t)cur * D + d], sh.x[d], pv, m, v);
         sh.mu2[d] = m;
         sh.v2[d] = v;
-        sh.lv2[d] = ref_logf(v);
+        sh.lv2[d] = fd_logf(sh, v);
       }
       __syncthreads();
       stamp(5);   // P + x (into dbg[13])
@@ -1070,7 +1078,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float m = f.mean[(size_t)cur * D + d], v = f.meanSq[(size_t)cur * D + d] / cP + pv;
           sh.muP[d] = m;
           sh.vP[d] = v;
-          sh.lvP[d] = ref_logf(v);
+          sh.lvP[d] = fd_logf(sh, v);
         }
         // the split's nodes: cur's children except b1, then b1's children (list order)
         const int nb1 = f.ccnt[b1];
@@ -1100,7 +1108,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           m = m + CWQ_KDIV(dl, cnt);
           m2 = m2 + dl * (xd - m);
           const float v1 = CWQ_KDIV(m2, cnt) + pv;
-          a = sh.lv2[d] - ref_logf(v1);
+          a = sh.lv2[d] - fd_logf(sh, v1);
           const float df = m - sh.mu2[d];
           bb = CWQ_KDIV((v1 + df * df), sh.v2[d]);
         }, sa, sb);
@@ -1120,7 +1128,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           for (int j = 2 * wave; wave < nsw && j < n_split; j += 2 * nsw) {
             const int j1 = j + 1 < n_split ? j + 1 : j;
             float K0, K1;
-            fd_kl_ref2(f, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
+            fd_kl_ref2(f, sh, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
             if (lane == 0) {
               f.kres[2 * b + 1 + j] = K0;
               f.kres[2 * b + 1 + j1] = K1;

@@ -506,6 +506,38 @@ __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float
   }
 }
 
+// One wave: the top-Kp list (lk, lr) of the values uq[lo, hi) one by one (rows = indices);
+// 8 chunks of 64 values in flight per round trip.
+__device__ __forceinline__ void select_values_wave(const float* __restrict__ uq, int lo, int hi, int Kp, int lane,
+                                                   float& lk, int& lr) {
+  lk = -__builtin_inff();
+  lr = 0x7fffffff;
+  bool first = true;
+  for (int r0 = lo; r0 < hi; r0 += 512) {
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int r = r0 + c * 64 + lane;
+      v[c] = r < hi ? uq[r] : -__builtin_inff();
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int r = r0 + c * 64 + lane;
+      if (r0 + c * 64 >= hi) break;
+      const float x = v[c] == v[c] ? v[c] : -__builtin_inff();
+      if (first) {
+        lk = x;
+        lr = x == -__builtin_inff() ? 0x7fffffff : r;
+        float dummy = 0.f;
+        wave_sort64<false>(lk, lr, dummy, lane);
+        first = false;
+      } else {
+        list64_offer(lk, lr, lane, x, r, Kp);
+      }
+    }
+  }
+}
+
 // One wave: the top-Kp list (lk, lr: lane i holds the i-th) of the per-lane maxima of up to
 // 16 values of uq[0, nrows) -- the K-th largest of maxima over distinct rows is still a
 // lower bound of the K-th largest value.  Reads whole 1024-value steps (the buffer carries
@@ -642,6 +674,11 @@ struct StreamArgs {
   // then the categorize RowF (cat_rf) and P / Phi its group-term tables
   const float* BFk;
   int64_t ldBF;
+  // probe (MODE 1): every probed row's lower bound to lb[q][g * 16 + row] instead of the
+  // group's maximum, and the fused select takes them one by one (all waves of the last
+  // workgroup per query): categorize's lists (R = 64) cluster in a few 16-row blocks, where
+  // group maxima leave the threshold far below the R-th key
+  int probe_rows;
   // filter pass (MODE 0) over a list of 16-row blocks instead of all of them: live[0..*live_n)
   // (group pruning: the blocks whose rows are all in groups pruned for every query of the call
   // are left out, prune_stage_b_kernel)

@@ -94,7 +94,10 @@ static constexpr double kRefLogL[128] = {
     -0x1.e72bccc13cd9fp-6, -0x1.a55f624c5c427p-6, -0x1.63d615c690bd6p-6, -0x1.228f827ea2d0ep-6,
     -0x1.c3177b4c75deep-7, -0x1.4192bb96832bfp-7, -0x1.8121bb458686fp-8, 0x0.0p+0};
 
-__host__ __device__ __forceinline__ float ref_logf(float v) {
+// ref_logf with the tables given (the device fitter keeps copies in LDS: a lane-indexed
+// table read from global memory is a vector-memory round trip per log)
+__host__ __device__ __forceinline__ float ref_logf_tab(float v, const float* __restrict__ tabC,
+                                                       const double* __restrict__ tabL) {
 #if defined(FIT_PROBE_LOG) && defined(__HIP_DEVICE_COMPILE__)
   return __logf(v);   // timing-only variant build (see CWQ_KDIV)
 #endif
@@ -103,7 +106,7 @@ __host__ __device__ __forceinline__ float ref_logf(float v) {
   const int i = (int)((u >> 16) & 127);
   const int e = (int)(u >> 23) - 127 + (i >> 6);
   const double m = (double)__builtin_bit_cast(float, (u & 0x007fffffu) | 0x3f800000u);
-  const double r = fma(m, (double)kRefLogC[i], -1.0);
+  const double r = fma(m, (double)tabC[i], -1.0);
   double p = 1.0 / 7.0;
   p = fma(p, r, -1.0 / 6.0);
   p = fma(p, r, 1.0 / 5.0);
@@ -112,9 +115,10 @@ __host__ __device__ __forceinline__ float ref_logf(float v) {
   p = fma(p, r, -0.5);
   p = fma(p, r * r, r);   // r + r^2 (-1/2 + r (1/3 - ...))
   const double ed = (double)e;
-  const double y = fma(ed, 0x1.62e42fefa39efp-1, kRefLogL[i] + fma(ed, 0x1.abc9e3b39803fp-56, p));
+  const double y = fma(ed, 0x1.62e42fefa39efp-1, tabL[i] + fma(ed, 0x1.abc9e3b39803fp-56, p));
   return (float)y;
 }
+__host__ __device__ __forceinline__ float ref_logf(float v) { return ref_logf_tab(v, kRefLogC, kRefLogL); }
 
 // torch's CPU float32 sum of a contiguous vector, bit for bit (ATen's cascade sum as this
 // build runs it -- 8-wide vectors: 4 vector accumulators, cascade levels of 16 rows, the

@@ -368,6 +368,8 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 #pragma unroll
       for (int qb = 0; qb < MQB; ++qb) {
         if (qb >= nqb) break;
+        if (MODE == 1 && a.probe_rows && qok[qb] && !rok)
+          a.lb[(size_t)(qb * 16 + r16) * a.ldlb + gi * 16 + 4 * c16 + j] = -CWQ_INF;
         if (!rok || !qok[qb]) continue;
         float u, l;
         // int8: the int32 acc is exact (|acc| <= 127^2 * DPB); up to three fp32 roundings
@@ -383,7 +385,8 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
           l = fminf(l, cB[qb]);
         }
         if (MODE == 1) {
-          pmax[qb] = fmaxf(pmax[qb], l);
+          if (a.probe_rows) a.lb[(size_t)(qb * 16 + r16) * a.ldlb + gi * 16 + 4 * c16 + j] = l;
+          else pmax[qb] = fmaxf(pmax[qb], l);
         } else if (u >= Tq[qb] && u > -CWQ_INF) {   // (a -inf bound: a -inf key, never listed)
           const int q = qb * 16 + r16;
           // live threshold: fold l into its row block, then publish min over the blocks
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
         }
       }
     }
-    if (MODE == 1) {   // the group's max lower bound per query -> lb[q][gi]
+    if (MODE == 1 && !a.probe_rows) {   // the group's max lower bound per query -> lb[q][gi]
 #pragma unroll
       for (int qb = 0; qb < MQB; ++qb) {
         float m = fmaxf(pmax[qb], __shfl_xor(pmax[qb], 16, 64));
@@ -455,7 +458,35 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
-    if (s_last) {
+    if (s_last && a.probe_rows) {
+      // per-row bounds: each query's values split over the waves, the waves' lists merged by
+      // wave 0 (LDS past the flag word: the query image is no longer read)
+      float* s_lk = reinterpret_cast<float*>(sq) + 16;
+      int* s_lr = reinterpret_cast<int*>(sq) + 16 + SK_WAVES * 64;
+      const int n = (int)(a.n_probe * 16);
+      const int per = (n + SK_WAVES * 64 - 1) / (SK_WAVES * 64) * 64;
+      for (int q = 0; q < a.nq; ++q) {
+        float lk;
+        int lr;
+        const int lo = min(n, wave * per);
+        select_values_wave(a.lb + (size_t)q * a.ldlb, lo, min(n, lo + per), a.K, lane, lk, lr);
+        s_lk[wave * 64 + lane] = lk;
+        s_lr[wave * 64 + lane] = lr;
+        __syncthreads();
+        if (wave == 0) {
+          for (int w = 1; w < SK_WAVES; ++w) {
+            const float x = s_lk[w * 64 + lane];
+            const int r = s_lr[w * 64 + lane];
+            list64_offer(lk, lr, lane, lane < a.K && r != 0x7fffffff ? x : -CWQ_INF, r, a.K);
+          }
+          if (a.sel_floor && lane == a.K - 1) lk = fmaxf(lk, a.sel_floor[q]);
+          a.sel_lk[(size_t)q * 64 + lane] = lk;
+          a.sel_lr[(size_t)q * 64 + lane] = lr;
+        }
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(a.sel_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (s_last) {
       for (int q = wave; q < a.nq; q += SK_WAVES) {
         float lk;
         int lr;

@@ -302,10 +302,10 @@ def test_stream_near_duplicate_rows(gpu, N, monkeypatch):
 @pytest.mark.parametrize("N,D,nq,k", [(60000, 768, 1, 10), (60000, 768, 3, 64), (4000, 64, 2, 10),
                                       (600, 384, 1, 10), (30000, 200, 64, 5)])
 def test_stream_tail_split_equals_one_workgroup(gpu, N, D, nq, k, monkeypatch):
-    """The per-call rerank tail split over several workgroups per query (FwExpand::split:
-    each reranks a slice of the candidate list, the last merges) returns what one workgroup
-    per query returns, and both equal the exact scan: many candidates (near-duplicate rows
-    at N = 4000), fewer candidates than workgroups (N = 600), k = 64."""
+    """The per-call rerank tail split over several workgroups per query (FwExpand::split, the
+    int8 pass: each reranks a slice of the candidate list, the last merges) returns what one
+    workgroup per query returns, and both equal the exact scan: many candidates
+    (near-duplicate rows at N = 4000), fewer candidates than workgroups (N = 600), k = 64."""
     if N == 4000:
         g = torch.Generator(device="cuda:0").manual_seed(N)
         base = torch.randn(D, device="cuda:0", generator=g)
@@ -314,11 +314,12 @@ def test_stream_tail_split_equals_one_workgroup(gpu, N, D, nq, k, monkeypatch):
         X = gpu.synth.synthetic_corpus(N, D, seed=N + D + 9)
     ix = flat_index(gpu, X)
     Q, _ = gpu.synth.synthetic_queries(X, nq, seed=nq + 9)
+    monkeypatch.setenv("CWQ_STREAM_I8", "1")   # the split serves the int8 pass's long lists
     out = {}
     for v in ("1", "32"):
         monkeypatch.setenv("CWQ_FW_SPLIT", v)
         ids0, s0, ids1, s1, st = both(ix, Q, k)
-        assert st["path"] == "stream" and st["fallback_queries"] == 0, st
+        assert st["path"] == "stream" and st["int8_pass"] and st["fallback_queries"] == 0, st
         assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
         out[v] = (ids1, s1, st["exact_reranks"])
     assert torch.equal(out["1"][0], out["32"][0]) and torch.equal(out["1"][1], out["32"][1])
