@@ -2681,7 +2681,8 @@ size_t stream_cat_bytes(const cwq_index* ix, int nqc) {
   const int nq16 = (nqc + 15) / 16 * 16;
   const int64_t ldlb = cat_ldlb(ix, 64);
   return (size_t)nq16 * ix->DPB * 2 + (size_t)nq16 * 16 + (size_t)nqc * 4 + (size_t)(5 * nqc + 1) * 4 +
-         (size_t)nqc * kFgCapQ * 12 + (size_t)nqc * 64 * 16 + (size_t)nqc * ldlb * 4 + 16 * 256;
+         (size_t)nqc * kFgCapQ * 12 + (size_t)nqc * 64 * 16 + (size_t)nqc * ldlb * 4 + 16 * 256 +
+         (size_t)nqc * kFwSplitMax * 64 * 12 + 3 * 256;
 }
 bool stream_cat_ok(const cwq_index* ix, int nqc, int R) {
   return ix->iso_Mb && ix->NL_iso >= kStreamMinRows && nqc <= kStreamMaxQ && R <= kFiltMaxK &&
@@ -2709,6 +2710,11 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   float* lb = b.take<float>((size_t)nqc * ldlb);
   float* tl = b.take<float>((size_t)nqc * 64);
   int* tr = b.take<int>((size_t)nqc * 64);
+  // the rerank split over workgroups (categorize lists: ~1k candidates, most reranked --
+  // their keys tie at the parents' bottlenecks); arrivals counted in the zeroed ok slot
+  const int fws = fw_split(ix, nqc, true);
+  FwExpand fx{nullptr, nullptr, nullptr, nullptr, 0, nullptr, fws, b.take<float>((size_t)nqc * fws * 64),
+              b.take<float>((size_t)nqc * fws * 64), b.take<int>((size_t)nqc * fws * 64), qcnt + nqc};
   // the counters (qcnt, qover, done, the fused select's) zeroed by the prep's block 0
   HIPCHK(launch_query_prep(q, nqc, ix->D, ix->iso_c, ix->DPB, nq16, Xb, qinfo, s, qcnt, (int)(5 * nqc + 1)));
   const FiltConsts fc = filt_consts(ix->DPB);
@@ -2757,7 +2763,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   HIPCHK(launch_stream(a, 0, stream_wgs(ix), s));
   HIPCHK(launch_final(c.X, ix->iso_Mf, ix->DP, nqc, R, capq, qcnt, qover, crow, cu, cl, T, 1, ix->row_meta, ix->row_par,
                       BFk ? BFk : ix->dummy, std::max(ix->NI, 1), 0, pkey, paux, prow, lstride, okf, nex, lkb, lrb,
-                      done, nullptr, 1, dfull, s));
+                      done, nullptr, 1, dfull, s, fws > 1 ? &fx : nullptr));
   if (getenv("CWQ_CAT_DEBUG")) {   // diagnostics: per query candidates, overflow, threshold, certified
     std::vector<int> hc(nqc), ho(nqc), hk(nqc), hx(nqc);
     std::vector<float> ht(nqc), hl(64);

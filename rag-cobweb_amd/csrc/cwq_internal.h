@@ -780,11 +780,13 @@ struct FwExpand {
   int* hflags;
   // split > 1: `split` workgroups per query, each reranking its own slice of the candidate
   // list into a top-K list in sk/sa/sr ([nq][split][64]); the last to finish (arrival count
-  // in the call's zeroed ok_flag[q], exact reranks summed in n_exact[q]) merges and expands
+  // in sctr[q], or with sctr null the call's zeroed ok_flag[q]; exact reranks summed in the
+  // zeroed n_exact[q]) merges, then expands (ids) or writes the list (no ids)
   int split;
   float* sk;
   float* sa;
   int* sr;
+  int* sctr;
 };
 size_t final_wide_lds(int DP, int capq);   // dynamic LDS of final_wide_kernel (SIZE_MAX: cannot run)
 int final_wide_rows(int DP, int capq);     // survivors per rerank round

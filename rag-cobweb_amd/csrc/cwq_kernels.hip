@@ -1385,19 +1385,84 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // ---------------------------------------------------------------------------
 // The heap lives in LDS (kTwoHeapLds entries, one wave per workgroup): a two-level replay
 // pushes ~1.5k entries on C2's tree, and its pops / pushes are dependent round trips --
-// ~100 cycles in LDS instead of ~1-2 us in global memory.  A heap that outgrows it
-// ends the replay uncertified (the query goes DENSE).
+// ~100 cycles in LDS instead of ~1-2 us in global memory.  A heap that outgrows it ends the
+// replay uncertified (the query goes DENSE).  Each entry carries what its pop needs (a side
+// record moved with it): the bottleneck b (BF[node], or min(BF[parent], lp) of a row), the
+// second-level b2 (T2[node] / min(T2[parent], lp), cat_t2_kernel's values: the chain minimum
+// below the group root, formed down the path as the children are pushed), the parent's
+// bottleneck and has_sent -- all known when the entry is pushed (a child's BF is
+// min(BF[parent], LPF), run_internal's own recurrence), so a pop reads no global memory but
+// an internal node's child range, and the children's LPF / BFS index / has_sent come in one
+// round trip.
 constexpr int kTwoHeapLds = 4096;
+struct TwoRec {
+  float b, b2, pb;
+  int hs;
+};
+
+__device__ void xheap_push(HeapEnt* h, TwoRec* hx, int64_t& n, const HeapEnt& e, const TwoRec& x, int lane) {
+  if (lane == 0) {
+    int64_t i = n;
+    while (i > 0) {
+      const int64_t p = (i - 1) >> 6;
+      const HeapEnt hp = h[p];
+      if (!wheap_before(e.score, e.pscore, e.tb, hp.score, hp.pscore, hp.tb)) break;
+      h[i] = hp;
+      hx[i] = hx[p];
+      i = p;
+    }
+    h[i] = e;
+    hx[i] = x;
+  }
+  ++n;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ HeapEnt xheap_pop(HeapEnt* h, TwoRec* hx, int64_t& n, int lane, TwoRec& xtop) {
+  const HeapEnt top = h[0];
+  xtop = hx[0];
+  --n;
+  const HeapEnt last = h[n];
+  const TwoRec xlast = hx[n];
+  int64_t i = 0;
+  for (;;) {
+    const int64_t c0 = (i << 6) + 1;
+    if (c0 >= n) break;
+    const int64_t c = c0 + lane;
+    const bool ok = c < n;
+    HeapEnt ce = ok ? h[c] : HeapEnt{-CWQ_INF, 0.f, 0x7fffffff, 0};
+    const int b = wave_best(ok, ce.score, ce.pscore, ce.tb);
+    const float bs = __shfl(ce.score, b, 64), bp = __shfl(ce.pscore, b, 64);
+    const int bt = __shfl(ce.tb, b, 64), bn = __shfl(ce.node, b, 64);
+    if (!wheap_before(bs, bp, bt, last.score, last.pscore, last.tb)) break;
+    if (lane == 0) {
+      h[i] = HeapEnt{bs, bp, bt, bn};
+      hx[i] = hx[c0 + b];
+    }
+    i = c0 + b;
+  }
+  if (n > 0 && lane == 0) {
+    h[i] = last;
+    hx[i] = xlast;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return top;
+}
+
 __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   extern __shared__ HeapEnt s_heap[];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x;
   if (q >= a.nq) return;
   HeapEnt* h = s_heap;
+  TwoRec* hx = reinterpret_cast<TwoRec*>(s_heap + kTwoHeapLds);
   const int64_t hcap = kTwoHeapLds;
   int64_t hn = 0;
   const float* BF = a.BF + (size_t)q * a.ldI;
-  const float* T2 = a.T2 + (size_t)q * a.ldI;
   const int R = a.R;
   const size_t lo = (size_t)q * R;
   const float k1 = lane < R ? a.lkey[lo + lane] : -CWQ_INF;
@@ -1416,48 +1481,68 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   const bool full2 = __popcll(__ballot(v2)) == (uint64_t)R;
   const float tau2 = fmaxf(rl_f(k2, R - 1), G);
   const int p1 = v1 ? pe1 : -3, p2 = v2 ? a.row_par[w2] : -3;
+  // the list rows' BFS index and has_sent, per lane (read when a row is pushed)
+  const int tb1 = v1 ? a.row_bfs[w1] : 0, tb2 = v2 ? a.row_bfs[w2] : 0;
+  const int hs1 = v1 ? ((a.row_flags[w1] & FLAG_HAS_SENT) != 0) : 0;
+  const int hs2 = v2 ? ((a.row_flags[w2] & FLAG_HAS_SENT) != 0) : 0;
   int status = 0, found = 0, gpops = 0;
   int64_t calls = 1, visited = 0;
   // list 1 must be full, end inside the tie at G, and hold every group root among the rows
   if (!(G > -CWQ_INF) || wG == 0x7fffffff || !(xG > G) || a.NI <= 0) status = 1;
 
-  if (!status) wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0}, lane);
+  if (!status) {
+    const float b0 = BF[0];   // the root: BF = its own lp; T2 = +inf when at G (it is the group root)
+    xheap_push(h, hx, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0},
+               TwoRec{b0, b0 == G ? CWQ_INF : -CWQ_INF, CWQ_INF, a.int_has_sent[0] != 0 ? 1 : 0}, lane);
+  }
   while (hn > 0) {
-    const HeapEnt e = wheap_pop(h, hn, lane);
+    TwoRec x;
+    const HeapEnt e = xheap_pop(h, hx, hn, lane, x);
     ++visited;
     const bool is_int = e.node >= 0;
-    const int row = is_int ? -1 : -e.node - 1;
-    const int pr = is_int ? a.par_int[e.node] : a.row_par[row];
-    const float b = is_int ? BF[e.node] : (pr >= 0 ? fminf(BF[pr], e.score) : e.score);
+    const float b = x.b;
     if (!(b >= G)) {   // below the group (or NaN)
       status = 1;
       break;
     }
     if (b == G) {
-      const bool root = pr < 0 || BF[pr] > G;
-      const float b2 = is_int ? T2[e.node] : (pr >= 0 ? fminf(T2[pr], e.score) : CWQ_INF);
-      if (full2 && (root ? gpops > 0 : !(b2 > tau2))) {
+      const bool root = x.pb > G;
+      if (full2 && (root ? gpops > 0 : !(x.b2 > tau2))) {
         status = 1;
         break;
       }
       ++gpops;
     }
     if (visited >= a.max_nodes) break;
-    const bool has_sent = is_int ? a.int_has_sent[e.node] != 0 : (a.row_flags[row] & FLAG_HAS_SENT) != 0;
-    if (has_sent) {
+    if (x.hs) {
       if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
       ++found;
     }
     if (found == a.k) break;
     if (is_int) {
       const int u = e.node;
+      const int cb = a.int_child_begin[u], ce = a.int_child_end[u];
       calls += a.int_nchild[u];
       // room for every push of this pop (internal children + at most 2R list rows)
-      if (hn + (a.int_child_end[u] - a.int_child_begin[u]) + 2 * R > hcap) {
+      if (hn + (ce - cb) + 2 * R > hcap) {
         status = 1;
         break;
       }
-      wheap_push_children(h, hn, a, q, u, e.score, lane);
+      for (int c0 = cb; c0 < ce; c0 += 64) {   // the children: one load round trip per 64
+        const int c = c0 + lane;
+        const bool ok = c < ce;
+        const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
+        const int tb = ok ? a.int_bfs[c] : 0;
+        const int hs = ok ? (a.int_has_sent[c] != 0 ? 1 : 0) : 0;
+        const int m = min(64, ce - c0);
+        for (int j = 0; j < m; ++j) {
+          const float lj = __shfl(lpf, j, 64);
+          const float bj = fminf(b, lj);   // BF[child] = min(BF[u], LPF[child])
+          const float t2 = bj != G ? -CWQ_INF : (b > G ? CWQ_INF : fminf(lj, x.b2));
+          xheap_push(h, hx, hn, HeapEnt{lj, e.score, __shfl(tb, j, 64), c0 + j}, TwoRec{bj, t2, b, __shfl(hs, j, 64)},
+                     lane);
+        }
+      }
       for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint)
         uint64_t bm = __ballot(l == 0 ? p1 == u : p2 == u);
         while (bm) {
@@ -1465,7 +1550,10 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
           bm &= bm - 1;
           const int r = l == 0 ? rl_i(w1, j) : rl_i(w2, j);
           const float sc = l == 0 ? rl_f(x1, j) : rl_f(x2, j);
-          wheap_push(h, hn, HeapEnt{sc, e.score, a.row_bfs[r], -(r + 1)}, lane);
+          const int tbr = l == 0 ? rl_i(tb1, j) : rl_i(tb2, j);
+          const int hsr = l == 0 ? rl_i(hs1, j) : rl_i(hs2, j);
+          xheap_push(h, hx, hn, HeapEnt{sc, e.score, tbr, -(r + 1)}, TwoRec{fminf(b, sc), fminf(x.b2, sc), b, hsr},
+                     lane);
         }
       }
     }
@@ -1508,7 +1596,15 @@ hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hip
 
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
   if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(simulate_two_kernel, dim3((unsigned)a.nq), dim3(64), kTwoHeapLds * sizeof(HeapEnt), s, a);
+  static bool attr = false;   // dynamic LDS above the 64 KiB default
+  const size_t lds = (size_t)kTwoHeapLds * (sizeof(HeapEnt) + sizeof(TwoRec));
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&simulate_two_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(simulate_two_kernel, dim3((unsigned)a.nq), dim3(64), lds, s, a);
   return hipGetLastError();
 }
 

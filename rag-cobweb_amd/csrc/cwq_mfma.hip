@@ -2063,7 +2063,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   __shared__ float s_T2;
   __shared__ FwChainLds s_chain;   // exact parent chains (fw_chain_prefixes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int S = fx.ids && fx.split > 1 ? fx.split : 1;   // workgroups per query (FwExpand::split)
+  const int S = fx.split > 1 ? fx.split : 1;   // workgroups per query (FwExpand::split)
   const int q = blockIdx.x / S, sidx = blockIdx.x - q * S;
   const size_t base = (size_t)q * capq;
   // ---- one round trip: counters + the first window of the candidate lists ----
@@ -2324,7 +2324,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     if (lane == 0 && nx) atomicAdd(&n_exact[q], nx);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     int last = 0;
-    if (lane == 0) last = atomicAdd(&ok_flag[q], 1) == S - 1;
+    if (lane == 0) last = atomicAdd(fx.sctr ? &fx.sctr[q] : &ok_flag[q], 1) == S - 1;
     last = __shfl(last, 0, 64);
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2421,8 +2421,8 @@ hipError_t launch_final(const float* X, const float* Mf, int DP, int nq, int K, 
   const int wide_max = we && *we ? atoi(we) : kFinalWideMaxQ;
   const size_t lds = final_wide_lds(DP, capq);
   if ((fx || nq <= wide_max) && lds <= (size_t)kFwDynMax) {
-    if (fe.split > 1 && (!fe.sk || !fe.sa || !fe.sr || !ok_flag || !n_exact)) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)nq * (unsigned)(fe.ids && fe.split > 1 ? fe.split : 1);
+    if (fe.split > 1 && (!fe.sk || !fe.sa || !fe.sr || !(fe.sctr || ok_flag) || !n_exact)) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)nq * (unsigned)(fe.split > 1 ? fe.split : 1);
     hipLaunchKernelGGL(final_wide_kernel, dim3(grid), dim3(kFwThreads), lds, s, X, Mf, DP, nq, K, capq, qcnt,
                        qover, crow, cu, cl, T, ldT, meta, par, P, ldP, seg_base, pkey, paux, prow, lstride, ok_flag,
                        n_exact, lkb, lrb, done, ch, chain ? 1 : 0, cat, dconst, fe,

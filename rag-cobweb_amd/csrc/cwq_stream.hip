@@ -458,42 +458,43 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
       if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
-    if (s_last && a.probe_rows) {
-      // per-row bounds: each query's values split over the waves, the waves' lists merged by
-      // wave 0 (LDS past the flag word: the query image is no longer read)
+    if (s_last) {
+      // the K-th largest of the probe's values (group maxima, or every probed row's bound
+      // with probe_rows) one by one: wpq waves per query on its value range, the first of
+      // them merging the others' lists (LDS past the flag word: the query image is no
+      // longer read); all waves run the same rounds, so the barriers are uniform
       float* s_lk = reinterpret_cast<float*>(sq) + 16;
       int* s_lr = reinterpret_cast<int*>(sq) + 16 + SK_WAVES * 64;
-      const int n = (int)(a.n_probe * 16);
-      const int per = (n + SK_WAVES * 64 - 1) / (SK_WAVES * 64) * 64;
-      for (int q = 0; q < a.nq; ++q) {
-        float lk;
-        int lr;
-        const int lo = min(n, wave * per);
-        select_values_wave(a.lb + (size_t)q * a.ldlb, lo, min(n, lo + per), a.K, lane, lk, lr);
-        s_lk[wave * 64 + lane] = lk;
-        s_lr[wave * 64 + lane] = lr;
-        __syncthreads();
-        if (wave == 0) {
-          for (int w = 1; w < SK_WAVES; ++w) {
-            const float x = s_lk[w * 64 + lane];
-            const int r = s_lr[w * 64 + lane];
-            list64_offer(lk, lr, lane, lane < a.K && r != 0x7fffffff ? x : -CWQ_INF, r, a.K);
-          }
+      const int n = (int)(a.probe_rows ? a.n_probe * 16 : a.n_probe);
+      const int wpq = a.nq >= SK_WAVES ? 1 : SK_WAVES / a.nq;
+      const int qpr = SK_WAVES / wpq;   // queries per round
+      const int sub = wave % wpq;
+      const int per = (n + wpq * 64 - 1) / (wpq * 64) * 64;
+      for (int q0 = 0; q0 < a.nq; q0 += qpr) {
+        const int q = q0 + wave / wpq;
+        const bool act = wave / wpq < qpr && q < a.nq;
+        float lk = -CWQ_INF;
+        int lr = 0x7fffffff;
+        if (act) {
+          const int lo = min(n, sub * per);
+          select_values_wave(a.lb + (size_t)q * a.ldlb, lo, min(n, lo + per), a.K, lane, lk, lr);
+        }
+        if (wpq > 1) {
+          s_lk[wave * 64 + lane] = lk;
+          s_lr[wave * 64 + lane] = lr;
+          __syncthreads();
+          if (act && sub == 0)
+            for (int w = wave + 1; w < wave + wpq; ++w) {
+              const int r = s_lr[w * 64 + lane];
+              list64_offer(lk, lr, lane, lane < a.K && r != 0x7fffffff ? s_lk[w * 64 + lane] : -CWQ_INF, r, a.K);
+            }
+        }
+        if (act && sub == 0) {
           if (a.sel_floor && lane == a.K - 1) lk = fmaxf(lk, a.sel_floor[q]);
           a.sel_lk[(size_t)q * 64 + lane] = lk;
           a.sel_lr[(size_t)q * 64 + lane] = lr;
         }
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) __hip_atomic_store(a.sel_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (s_last) {
-      for (int q = wave; q < a.nq; q += SK_WAVES) {
-        float lk;
-        int lr;
-        select_wave(a.lb + (size_t)q * a.ldlb, (int)a.n_probe, a.K, lane, lk, lr);
-        if (a.sel_floor && lane == a.K - 1) lk = fmaxf(lk, a.sel_floor[q]);
-        a.sel_lk[(size_t)q * 64 + lane] = lk;
-        a.sel_lr[(size_t)q * 64 + lane] = lr;
+        if (wpq > 1) __syncthreads();
       }
       if (threadIdx.x == 0) __hip_atomic_store(a.sel_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
