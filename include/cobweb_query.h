@@ -215,6 +215,15 @@ int cwq_set_filter(cwq_index* idx, int mode);
  */
 int cwq_score_topk_host(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_t* ids, float* scores,
                         void* stream);
+/*
+ * cwq_categorize with host memory on both sides: q (host [nq*dim]) in; nodes (host
+ * [nq*k]), n_found (host [nq]) and n_calls (host [nq] or NULL) out; returns synchronized.
+ * The reference harness's Basic call shape (benchmark_utils.py:580-581: cobweb_predict on a
+ * numpy embedding, CobwebWrapper.py:435-461 -> CobwebTorchTree.py:235-289).  Same results
+ * as cwq_categorize.
+ */
+int cwq_categorize_host(cwq_index* idx, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
+                        int32_t* n_found, int64_t* n_calls, void* stream);
 
 int cwq_last_stats(cwq_index* idx, int64_t* out6);
 

@@ -43,6 +43,7 @@ SIGNATURES = {
     "cwq_last_stats": (_c.c_int, [_P, _P]),
     "cwq_last_prune_stats": (_c.c_int, [_P, _P]),
     "cwq_score_topk_host": (_c.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
+    "cwq_categorize_host": (_c.c_int, [_P, _P, _I64, _I32, _I64, _P, _P, _P, _P]),
     "cwq_whiten": (_c.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _I32, _P, _P, _P]),
     "cwq_fit_kl": (_c.c_int, [_P, _P, _P, _I32, _P, _c.c_float, _I32, _P, _I32, _P, _P]),
     "cwq_fit_node_op": (_c.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),

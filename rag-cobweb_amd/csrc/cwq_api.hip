@@ -3204,6 +3204,42 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   return CWQ_OK;
 }
 
+// Basic in the harness's shape (benchmark_utils.py:580-581: cobweb_predict(numpy_query, k)):
+// the query through pinned staging, the pop-order node ids / found counts / call counts
+// written by the kernels straight into mapped host memory, the call returning synchronized.
+extern "C" int cwq_categorize_host(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes,
+                                   int64_t* nodes, int32_t* n_found, int64_t* n_calls, void* stream) {
+  if (!ix || (!q && nq > 0) || (nq > 0 && (!nodes || !n_found))) return fail(CWQ_ERR_ARG, "NULL argument");
+  if (k <= 0) return fail(CWQ_ERR_ARG, "k must be >= 1");
+  if (nq == 0) return CWQ_OK;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DevGuard dg(ix->device);
+  for (int64_t& t : ix->stats) t = 0;
+  hipStream_t s = (hipStream_t)stream;
+  WsUse wu(ix, s);
+  ScanCfgScope scs(nq);
+  if (wu.rc) return wu.rc;
+  const size_t qb = (size_t)nq * ix->D * 4, nb = (size_t)round_up(nq * k * 8, 256), cb = (size_t)round_up(nq * 8, 256),
+               fb = (size_t)nq * 4;
+  int rc;
+  if ((rc = ix->host_io(qb, nb + cb + fb))) return rc;
+  memcpy(ix->hq, q, qb);
+  HIPCHK(hipMemcpyAsync(ix->dq, ix->hq, qb, hipMemcpyHostToDevice, s));
+  int64_t* hn = (int64_t*)ix->hout;
+  int64_t* hc = (int64_t*)((char*)ix->hout + nb);
+  int32_t* hf = (int32_t*)((char*)ix->hout + nb + cb);
+  rc = categorize_impl(ix, (const float*)ix->dq, nq, k, max_nodes, hn, hf, hc, s, true);
+  ix->stats[0] = nq;
+  if (rc) return rc;
+  HIPCHK(launch_clear_tail(hn, hf, nq, k, s));
+  HIPCHK(sync_spin(s));
+  ix->ws_idle = true;   // synchronized
+  memcpy(nodes, hn, (size_t)nq * k * 8);
+  memcpy(n_found, hf, fb);
+  if (n_calls) memcpy(n_calls, hc, (size_t)nq * 8);
+  return CWQ_OK;
+}
+
 extern "C" int cwq_welford_groups(const float* X, int64_t n_rows, int32_t dim, const int64_t* order,
                                   const int64_t* group_ptr, int64_t n_groups, float* count, float* mean,
                                   float* meanSq, void* stream) {

@@ -196,6 +196,7 @@ struct FdJob {
 struct FdShared {
   float x[kFdMaxD], mu2[kFdMaxD], v2[kFdMaxD], lv2[kFdMaxD];
   float muP[kFdMaxD], vP[kFdMaxD], lvP[kFdMaxD];
+  float rv2[kFdMaxD], rvP[kFdMaxD];   // div_recip of v2 / vP (the KL terms' divisor per dimension)
   uint32_t mt[kMtN];
   uint32_t mtn[kMtN];   // the parallel twist's new words
   alignas(16) float cg[kFdChunk];
@@ -214,6 +215,13 @@ struct FdShared {
 };
 static_assert(sizeof(FdShared) <= 160 * 1024, "the fit workgroup's LDS");
 __device__ __forceinline__ float fd_logf(const FdShared& sh, float v) { return ref_logf_tab(v, sh.logc, sh.logl); }
+// the KL terms' divisions: IEEE's by div_rn (y = div_recip(b)); the timing-only probe build
+// (FIT_PROBE_DIV) takes the bare hardware reciprocal instead
+#ifdef FIT_PROBE_DIV
+#define KDIV(a, b, y) ((a) * __builtin_amdgcn_rcpf(b))
+#else
+#define KDIV(a, b, y) div_rn((a), (b), (y))
+#endif
 
 
 __device__ __forceinline__ int ld_agent(const int* p) {
@@ -456,52 +464,57 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
   float sa, sb;
   // U on lanes 0-31, T on lanes 32-63 (the same instructions: only (mu1, v1) differ)
   const float cnt = cc + 1.0f;
+  // the divisions are IEEE's, by a reciprocal and two corrections (div_rn)
+  const float ycnt = div_recip(cnt), yvar = (lane >> 5) ? div_recip(cc) : ycnt;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     // U: c + x (fd_insert_mv's ops); T: c as is (m2 / cc + pv) -- one variance division per
     // lane, the operands selected per half
     const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
     const float xd = sh.x[d];
     const float delta = xd - m;
-    const float mm = m + CWQ_KDIV(delta, cnt);
+    const float mm = m + KDIV(delta, cnt, ycnt);
     const float mu1 = h ? m : mm;
     const float num = h ? m2 : m2 + delta * (xd - mm);
-    const float v1 = CWQ_KDIV(num, (h ? cc : cnt)) + pv;
+    const float v1 = KDIV(num, (h ? cc : cnt), yvar) + pv;
     a = sh.lv2[d] - fd_logf(sh, v1);
     const float df = mu1 - sh.mu2[d];
-    b = CWQ_KDIV((v1 + df * df), sh.v2[d]);
+    b = KDIV((v1 + df * df), sh.v2[d], sh.rv2[d]);
   }, sa, sb);
   const float k = fd_kl_score(sa, sb, D);
   U = __shfl(k, 0, 64);
   T = __shfl(k, 32, 64);
 }
 // KL(c || ref) with the reference vectors (mu, v, log v) given
-__device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, const float* mu, const float* v, const float* lv, int c,
-                                           int lane) {
+__device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, const float* mu, const float* v,
+                                           const float* rv, const float* lv, int c, int lane) {
 #pragma clang fp contract(off)
   const int D = f.D;
   const float cc = f.count[c];
+  const float ycc = div_recip(cc);
   float sa, sb;
   torch_sum2(D, lane, [&](int d, float& a, float& b) {
-    const float mu1 = f.mean[(size_t)c * D + d], v1 = CWQ_KDIV(f.meanSq[(size_t)c * D + d], cc) + f.pv;
+    const float mu1 = f.mean[(size_t)c * D + d], v1 = KDIV(f.meanSq[(size_t)c * D + d], cc, ycc) + f.pv;
     a = lv[d] - fd_logf(sh, v1);
     const float df = mu1 - mu[d];
-    b = CWQ_KDIV((v1 + df * df), v[d]);
+    b = KDIV((v1 + df * df), v[d], rv[d]);
   }, sa, sb);
   return fd_kl_score(sa, sb, D);
 }
 // KL(c0 || ref) and KL(c1 || ref) in one wave (c0 on lanes 0-31, c1 on lanes 32-63)
-__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const FdShared& sh, const float* mu, const float* v, const float* lv, int c0,
-                                           int c1, int lane, float& K0, float& K1) {
+__device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const FdShared& sh, const float* mu, const float* v,
+                                           const float* rv, const float* lv, int c0, int c1, int lane, float& K0,
+                                           float& K1) {
 #pragma clang fp contract(off)
   const int D = f.D;
   const float cc0 = f.count[c0], cc1 = f.count[c1];
+  const float ycc = div_recip((lane >> 5) ? cc1 : cc0);
   float sa, sb;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     const size_t o = (size_t)(h ? c1 : c0) * D + d;
-    const float mu1 = f.mean[o], v1 = CWQ_KDIV(f.meanSq[o], (h ? cc1 : cc0)) + f.pv;
+    const float mu1 = f.mean[o], v1 = KDIV(f.meanSq[o], (h ? cc1 : cc0), ycc) + f.pv;
     a = lv[d] - fd_logf(sh, v1);
     const float df = mu1 - mu[d];
-    b = CWQ_KDIV((v1 + df * df), v[d]);
+    b = KDIV((v1 + df * df), v[d], rv[d]);
   }, sa, sb);
   const float k = fd_kl_score(sa, sb, D);
   K0 = __shfl(k, 0, 64);
@@ -516,7 +529,7 @@ __device__ __forceinline__ float fd_kl_new(const FitDev& f, const FdShared& sh, 
   torch_sum2(f.D, lane, [&](int d, float& a, float& b) {
     a = sh.lv2[d] - lv1;
     const float df = sh.x[d] - sh.mu2[d];
-    b = CWQ_KDIV((v1 + df * df), sh.v2[d]);
+    b = KDIV((v1 + df * df), sh.v2[d], sh.rv2[d]);
   }, sa, sb);
   return fd_kl_score(sa, sb, f.D);
 }
@@ -532,7 +545,7 @@ __device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh
     st_agent_f(&f.kres[2 * j], U);
     st_agent_f(&f.kres[2 * j + 1], T);
   } else {
-    const float K = fd_kl_ref(f, sh, sh.muP, sh.vP, sh.lvP, f.jobs[j], lane);
+    const float K = fd_kl_ref(f, sh, sh.muP, sh.vP, sh.rvP, sh.lvP, f.jobs[j], lane);
     st_agent_f(&f.kres[kofs + j], K);
   }
 }
@@ -566,10 +579,12 @@ __device__ __forceinline__ void fd_help_job(const FitDev& f, FdShared& sh, const
   if (n <= 0 || n > 3 * f.cap || base < 0 || row < 0) return;   // never: a descriptor not (yet) seen
   float* mu = type ? sh.muP : sh.mu2;
   float* v = type ? sh.vP : sh.v2;
+  float* rv = type ? sh.rvP : sh.rv2;
   float* lv = type ? sh.lvP : sh.lv2;
   for (int d = tid; d < D; d += kFdThreads) {
     mu[d] = f.pvec[d];
     v[d] = f.pvec[D + d];
+    rv[d] = div_recip(v[d]);
     lv[d] = f.pvec[2 * D + d];
     if (type == 0) sh.x[d] = X[row * D + d];
   }
@@ -885,6 +900,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         fd_insert_mv(cP, f.mean[(size_t)cur * D + d], f.meanSq[(size_t)cur * D + d], sh.x[d], pv, m, v);
         sh.mu2[d] = m;
         sh.v2[d] = v;
+        sh.rv2[d] = div_recip(v);
         sh.lv2[d] = fd_logf(sh, v);
       }
       __syncthreads();
@@ -1078,6 +1094,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float m = f.mean[(size_t)cur * D + d], v = f.meanSq[(size_t)cur * D + d] / cP + pv;
           sh.muP[d] = m;
           sh.vP[d] = v;
+          sh.rvP[d] = div_recip(v);
           sh.lvP[d] = fd_logf(sh, v);
         }
         // the split's nodes: cur's children except b1, then b1's children (list order)
@@ -1093,6 +1110,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       __syncthreads();
       if (do_merge && wave == kFdWaves - 1) {   // mean_var_merge(b1, b2) with x vs P + x
         const float c1 = f.count[b1], c2 = f.count[b2];
+        const float ytot = div_recip(c1 + c2), ycn = div_recip((c1 + c2) + 1.0f);
         float sa, sb;
         torch_sum2(D, lane, [&](int d, float& a, float& bb) {
 #pragma clang fp contract(off)
@@ -1101,16 +1119,16 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float delta = mb - ma;
           const float tot = c1 + c2;
           float m2 = (sa2 + sb2) + (delta * delta) * ((c1 * c2) / tot);
-          float m = CWQ_KDIV((c1 * ma + c2 * mb), tot);
+          float m = KDIV((c1 * ma + c2 * mb), tot, ytot);
           const float cnt = tot + 1.0f;
           const float xd = sh.x[d];
           const float dl = xd - m;
-          m = m + CWQ_KDIV(dl, cnt);
+          m = m + KDIV(dl, cnt, ycn);
           m2 = m2 + dl * (xd - m);
-          const float v1 = CWQ_KDIV(m2, cnt) + pv;
+          const float v1 = KDIV(m2, cnt, ycn) + pv;
           a = sh.lv2[d] - fd_logf(sh, v1);
           const float df = m - sh.mu2[d];
-          bb = CWQ_KDIV((v1 + df * df), sh.v2[d]);
+          bb = KDIV((v1 + df * df), sh.v2[d], sh.rv2[d]);
         }, sa, sb);
         const float K = fd_kl_score(sa, sb, D);
         if (lane == 0) sh.cf[3] = K;
@@ -1128,7 +1146,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           for (int j = 2 * wave; wave < nsw && j < n_split; j += 2 * nsw) {
             const int j1 = j + 1 < n_split ? j + 1 : j;
             float K0, K1;
-            fd_kl_ref2(f, sh, sh.muP, sh.vP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
+            fd_kl_ref2(f, sh, sh.muP, sh.vP, sh.rvP, sh.lvP, f.jobs[j], f.jobs[j1], lane, K0, K1);
             if (lane == 0) {
               f.kres[2 * b + 1 + j] = K0;
               f.kres[2 * b + 1 + j1] = K1;

@@ -18,6 +18,36 @@ namespace cwq {
 #define CWQ_KDIV(a, b) ((a) / (b))
 #endif
 
+// a / b rounded to nearest, from y = div_recip(b) (computed once per divisor): q = fl(a y),
+// then two Markstein corrections q <- fl(q + r y) with r = a - b q (exact by fma).  One
+// correction leaves q within (1/2 + 2^-23) ulp of a/b; with y = RN(1/b) the second returns
+// RN(a/b): |fl-free q + r y - a/b| <= |a/b - q| |1 - b y| < (1/2 + 2^-23) u B 2^-48 (u the ulp of
+// a/b, B the divisor's 24-bit integer significand), while a/b is never a midpoint and any
+// midpoint is at least u / (2B) away (|a - b m| is a nonzero multiple of b's and m's joint
+// grain), and (1 + 2^-22) B^2 < 2^48 for B <= 2^24 - 2.  So: a divisor with an all-ones
+// significand (B = 2^24 - 1), or outside [2^-60, 2^60], gets y = NaN and every quotient by it
+// the IEEE division; so does a dividend outside [2^-60, 2^60] (0 excepted: 0 / b = 0 with
+// a's sign, which the sequence keeps).  Checked against IEEE division on host
+// (scripts/check_div_rn.hip: every dividend for a set of divisors, random and near-midpoint
+// pairs; tests/test_div_rn.py).
+__host__ __device__ __forceinline__ float div_recip(float b) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, b) & 0x7fffffffu;
+  const bool ok = (u & 0x007fffffu) != 0x007fffffu && u - 0x21800000u < 0x5d800000u - 0x21800000u;
+  return ok ? 1.0f / b : __builtin_nanf("");
+}
+__host__ __device__ __forceinline__ float div_rn(float a, float b, float y) {
+#pragma clang fp contract(off)
+  const uint32_t ua = __builtin_bit_cast(uint32_t, a) & 0x7fffffffu;
+  const bool ok = y == y && (ua == 0u || ua - 0x21800000u < 0x5d800000u - 0x21800000u);
+  if (!ok) return a / b;
+  float q = a * y;
+  float r = fmaf(b, q, -a);   // -(a - b q), exact
+  q = fmaf(-r, y, q);
+  r = fmaf(b, q, -a);
+  q = fmaf(-r, y, q);
+  return q;
+}
+
 // log: torch's float32 log (Sleef, 1-ulp) is the correctly rounded value for 99.96% of
 // inputs; a log computed to a few double ulps and rounded once is that value.  The library's
 // fp64 log was most of a clustered ifit's insert time, so: a 128-entry table on the top 7

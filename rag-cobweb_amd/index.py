@@ -247,6 +247,24 @@ class CobwebIndex:
                                           _stream_raw(self.device.index)))
         return ids, scores
 
+    def categorize_host(self, q, k, max_nodes=100000):
+        """categorize for a host (numpy) query batch -> numpy (nodes [nq, k] int64, found [nq]
+        int32, calls [nq] int64): cwq_categorize_host, the harness's Basic call shape (pinned
+        staging in, the kernels write the results into mapped host memory)."""
+        q = np.ascontiguousarray(np.asarray(q, dtype=np.float32))
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be [nq, {self.dim}]")
+        nq, k = q.shape[0], int(k)
+        nodes = np.empty((nq, k), np.int64)
+        found = np.empty(nq, np.int32)
+        calls = np.empty(nq, np.int64)
+        mx = int(min(max_nodes, 2 ** 62)) if max_nodes != float("inf") else 2 ** 62
+        check(self._L.cwq_categorize_host(self._h, q.ctypes.data, nq, k, mx, nodes.ctypes.data, found.ctypes.data,
+                                          calls.ctypes.data, _stream_raw(self.device.index)))
+        return nodes, found, calls
+
     def rank_scores(self, q):
         """All sentence scores (A8), [nq, n_sent]."""
         q = self._queries(q)

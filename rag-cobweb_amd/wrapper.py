@@ -284,8 +284,14 @@ class CobwebWrapper:
         retrieve_k=k and max_nodes=max_init_search; IndexError when fewer than k
         nodes with sentences are retrieved (CobwebTorchTree.py:289)."""
         self.build_prediction_index()
-        x = self._embed(input, is_embedding)
-        nodes, found, calls = self._index.categorize(x[None, :], k, self.max_init_search)
+        emb = input if is_embedding else self.encode_func([input])[0]
+        if torch.is_tensor(emb):
+            x = emb.detach().to(self._index.device, torch.float32).reshape(1, -1)
+            nodes, found, calls = self._index.categorize(x, k, self.max_init_search)
+            nodes, found, calls = nodes.cpu().numpy(), found.cpu().numpy(), calls.cpu().numpy()
+        else:   # a host embedding (the harness's numpy query): host memory in and out, one call
+            nodes, found, calls = self._index.categorize_host(np.asarray(emb, np.float32).reshape(1, -1), k,
+                                                              self.max_init_search)
         nf = int(found[0])
         # the reference's search draws one random() per heap push (one per log_prob call)
         # and one per retrieval (CobwebTorchTree.py:243,268,285) from the global stream
