@@ -219,6 +219,8 @@ __device__ __forceinline__ float fd_logf(const FdShared& sh, float v) { return r
 // (FIT_PROBE_DIV) takes the bare hardware reciprocal instead
 #ifdef FIT_PROBE_DIV
 #define KDIV(a, b, y) ((a) * __builtin_amdgcn_rcpf(b))
+#elif defined(FIT_DIV_IEEE)
+#define KDIV(a, b, y) ((a) / (b))   // A/B build: the plain IEEE division
 #else
 #define KDIV(a, b, y) div_rn((a), (b), (y))
 #endif

@@ -39,12 +39,19 @@ __host__ __device__ __forceinline__ float div_rn(float a, float b, float y) {
 #pragma clang fp contract(off)
   const uint32_t ua = __builtin_bit_cast(uint32_t, a) & 0x7fffffffu;
   const bool ok = y == y && (ua == 0u || ua - 0x21800000u < 0x5d800000u - 0x21800000u);
-  if (!ok) return a / b;
   float q = a * y;
   float r = fmaf(b, q, -a);   // -(a - b q), exact
   q = fmaf(-r, y, q);
   r = fmaf(b, q, -a);
   q = fmaf(-r, y, q);
+#ifdef __HIP_DEVICE_COMPILE__
+  // the IEEE division only in a wave that has a lane outside the range (never on the data
+  // the fitters see): a uniform branch, so the division's code is not run for every term
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0, 0))
+    if (!ok) q = a / b;
+#else
+  if (!ok) q = a / b;
+#endif
   return q;
 }
 

@@ -58,6 +58,7 @@ def main():
                     help="run the Fast legs with group pruning off (CWQ_GROUP_PRUNE=0) and on, in one process")
     ap.add_argument("--legs", default="all",
                     help="list (comma or +) of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
+    ap.add_argument("--chunk", type=int, default=0, help="device ifit in add_sentences calls of this many rows")
     ap.add_argument("--env-ab", default=None,
                     help="';'-separated variants of '&'-separated KEY=VAL (read per call): Fast one query per call "
                          "(nq = 1, 64) under each, interleaved over 3 rounds, after the other legs")
@@ -83,6 +84,19 @@ def main():
         ix = pkg.index.CobwebIndex(t["mean"], t["var"], t["parent"], t["node_of_sentence"], [1.0] * 6, device="cuda:0")
         w = pkg.CobwebWrapper.from_index(ix, [f"p{i}" for i in range(args.n)], node_of_sentence=t["node_of_sentence"])
         del t
+    elif args.chunk:
+        # the same device ifit in add_sentences calls of --chunk rows, progress per chunk (a
+        # long build keeps printing; inserts/s against the tree size)
+        w = pkg.CobwebWrapper(corpus=None, corpus_embeddings=None)
+        for a0 in range(0, args.n, args.chunk):
+            a1 = min(args.n, a0 + args.chunk)
+            tc = time.perf_counter()
+            w.add_sentences([f"p{i}" for i in range(a0, a1)], X[a0:a1])
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - tc
+            print(f"  ifit rows {a0}..{a1}: {(a1 - a0) / dt:.0f} inserts/s ({dt:.1f} s), total "
+                  f"{time.perf_counter() - t0:.1f} s", flush=True)
+        t_fit = time.perf_counter() - t0
     else:
         w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(args.n)], corpus_embeddings=X)
         torch.cuda.synchronize()
