@@ -215,14 +215,22 @@ struct FdShared {
 };
 static_assert(sizeof(FdShared) <= 160 * 1024, "the fit workgroup's LDS");
 __device__ __forceinline__ float fd_logf(const FdShared& sh, float v) { return ref_logf_tab(v, sh.logc, sh.logl); }
-// the KL terms' divisions: IEEE's by div_rn (y = div_recip(b)); the timing-only probe build
-// (FIT_PROBE_DIV) takes the bare hardware reciprocal instead
+// the KL terms' divisions: the compiler's IEEE division.  A/B builds: FIT_DIV_RN=1 takes
+// div_rn (a reciprocal per divisor and two Markstein corrections, equal to IEEE division:
+// scripts/check_div_rn.hip) -- measured slower on gfx950 (clustered 20k x 768: 9.51 vs 8.19
+// s, profiles/r05_fit_divrn_ab.log): the hardware sequence (v_div_scale, v_rcp, four fma,
+// v_div_fmas, v_div_fixup) is cheaper than the guarded corrections plus the per-dimension
+// reciprocal reads; FIT_PROBE_DIV (timing only) the bare reciprocal.
 #ifdef FIT_PROBE_DIV
 #define KDIV(a, b, y) ((a) * __builtin_amdgcn_rcpf(b))
-#elif defined(FIT_DIV_IEEE)
-#define KDIV(a, b, y) ((a) / (b))   // A/B build: the plain IEEE division
-#else
+#elif defined(FIT_DIV_RN)
 #define KDIV(a, b, y) div_rn((a), (b), (y))
+#define FIT_RECIP(b) div_recip(b)
+#else
+#define KDIV(a, b, y) ((a) / (b))
+#endif
+#ifndef FIT_RECIP
+#define FIT_RECIP(b) 0.f   // the reciprocals are read by div_rn only
 #endif
 
 
@@ -466,8 +474,8 @@ __device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, in
   float sa, sb;
   // U on lanes 0-31, T on lanes 32-63 (the same instructions: only (mu1, v1) differ)
   const float cnt = cc + 1.0f;
-  // the divisions are IEEE's, by a reciprocal and two corrections (div_rn)
-  const float ycnt = div_recip(cnt), yvar = (lane >> 5) ? div_recip(cc) : ycnt;
+  // the divisors' reciprocals (read by div_rn in the FIT_DIV_RN build only)
+  const float ycnt = FIT_RECIP(cnt), yvar = (lane >> 5) ? FIT_RECIP(cc) : ycnt;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     // U: c + x (fd_insert_mv's ops); T: c as is (m2 / cc + pv) -- one variance division per
     // lane, the operands selected per half
@@ -492,7 +500,7 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, 
 #pragma clang fp contract(off)
   const int D = f.D;
   const float cc = f.count[c];
-  const float ycc = div_recip(cc);
+  const float ycc = FIT_RECIP(cc);
   float sa, sb;
   torch_sum2(D, lane, [&](int d, float& a, float& b) {
     const float mu1 = f.mean[(size_t)c * D + d], v1 = KDIV(f.meanSq[(size_t)c * D + d], cc, ycc) + f.pv;
@@ -509,7 +517,7 @@ __device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const FdShared& sh, 
 #pragma clang fp contract(off)
   const int D = f.D;
   const float cc0 = f.count[c0], cc1 = f.count[c1];
-  const float ycc = div_recip((lane >> 5) ? cc1 : cc0);
+  const float ycc = FIT_RECIP((lane >> 5) ? cc1 : cc0);
   float sa, sb;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     const size_t o = (size_t)(h ? c1 : c0) * D + d;
@@ -586,7 +594,7 @@ __device__ __forceinline__ void fd_help_job(const FitDev& f, FdShared& sh, const
   for (int d = tid; d < D; d += kFdThreads) {
     mu[d] = f.pvec[d];
     v[d] = f.pvec[D + d];
-    rv[d] = div_recip(v[d]);
+    rv[d] = FIT_RECIP(v[d]);
     lv[d] = f.pvec[2 * D + d];
     if (type == 0) sh.x[d] = X[row * D + d];
   }
@@ -902,7 +910,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
         fd_insert_mv(cP, f.mean[(size_t)cur * D + d], f.meanSq[(size_t)cur * D + d], sh.x[d], pv, m, v);
         sh.mu2[d] = m;
         sh.v2[d] = v;
-        sh.rv2[d] = div_recip(v);
+        sh.rv2[d] = FIT_RECIP(v);
         sh.lv2[d] = fd_logf(sh, v);
       }
       __syncthreads();
@@ -1096,7 +1104,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           const float m = f.mean[(size_t)cur * D + d], v = f.meanSq[(size_t)cur * D + d] / cP + pv;
           sh.muP[d] = m;
           sh.vP[d] = v;
-          sh.rvP[d] = div_recip(v);
+          sh.rvP[d] = FIT_RECIP(v);
           sh.lvP[d] = fd_logf(sh, v);
         }
         // the split's nodes: cur's children except b1, then b1's children (list order)
@@ -1112,7 +1120,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       __syncthreads();
       if (do_merge && wave == kFdWaves - 1) {   // mean_var_merge(b1, b2) with x vs P + x
         const float c1 = f.count[b1], c2 = f.count[b2];
-        const float ytot = div_recip(c1 + c2), ycn = div_recip((c1 + c2) + 1.0f);
+        const float ytot = FIT_RECIP(c1 + c2), ycn = FIT_RECIP((c1 + c2) + 1.0f);
         float sa, sb;
         torch_sum2(D, lane, [&](int d, float& a, float& bb) {
 #pragma clang fp contract(off)

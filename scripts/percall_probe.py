@@ -27,13 +27,13 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--modes", default="0,-1,1")
     ap.add_argument("--wrapper", action="store_true", help="also time the drop-in cobweb_predict_fast(q, k)")
-    ap.add_argument("--balanced", default=None, help="B,L: a depth-L tree of branching B (synth.balanced_synth)")
+    ap.add_argument("--balanced", default=None, help="B,L (or BxL): a depth-L tree of branching B (synth.balanced_synth)")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
     if args.balanced:
-        b, L = (int(v) for v in args.balanced.split(","))
+        b, L = (int(v) for v in args.balanced.replace("x", ",").split(","))   # "4,9" or "4x9"
         fs = pkg.synth.balanced_synth(X, b, L, seed=1)
     else:
         fs = pkg.synth.flat_synth(X)
