@@ -140,6 +140,8 @@ struct cwq_index {
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
   int prn_gmax = 1;   // the most internal nodes of one pruning group
+  int prn_maxdep = 0;   // deepest internal node of any group
+  int *gi_dep = nullptr, *gi_ppos = nullptr;   // per group-list entry: depth, the parent's list position
   int* blk_grp = nullptr;   // per 16-row block of isotropic rows: the pruning group of all its rows (-1: mixed)
   int *gs_ptr = nullptr, *gs_rows = nullptr;   // per group: up to 64 usable isotropic rows (the seed threshold)
   GroupBound* gbound = nullptr;
@@ -748,6 +750,24 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
   ix->prn_gmax = 1;
   for (int g = 0; g < G; ++g) ix->prn_gmax = std::max(ix->prn_gmax, gptr[g + 1] - gptr[g]);
+  if ((size_t)ix->prn_gmax * 4 + (size_t)64 * (ix->DP / 16 + 1) * 4 > (size_t)144 * 1024) return CWQ_OK;   // LDS
+  // per list entry: depth (root 0) and the parent's position in the same list (the lists are
+  // BFS-ordered, so a level is finished before the next starts)
+  std::vector<int> idep(NI, 0), lpos(NI, -1), gdep(gnodes.size()), gpp(gnodes.size());
+  for (int i = 1; i < NI; ++i) idep[i] = par_int[i] >= 0 ? idep[par_int[i]] + 1 : 0;
+  for (size_t j = 0; j < gnodes.size(); ++j) lpos[gnodes[j]] = (int)j;
+  ix->prn_maxdep = 0;
+  for (size_t j = 0; j < gnodes.size(); ++j) {
+    const int i = gnodes[j], p = par_int[i];
+    gdep[j] = idep[i];
+    gpp[j] = p > 0 ? lpos[p] : -1;
+    ix->prn_maxdep = std::max(ix->prn_maxdep, idep[i]);
+    if (p > 0 && (gint[p] != gint[i] || lpos[p] >= (int)j)) return CWQ_OK;   // never: a group is a subtree in BFS order
+  }
+  if (gdep.empty()) {
+    gdep.push_back(0);
+    gpp.push_back(-1);
+  }
   // the seed threshold's rows: up to 64 usable isotropic rows of each group, spread over it
   std::vector<std::vector<int>> grows(G);
   for (int r = 0; r < ix->NL_iso; ++r)
@@ -770,6 +790,7 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     bg[b] = g;
   }
   if ((rc = ix->upload(&ix->blk_grp, bg, s))) return rc;
+  if ((rc = ix->upload(&ix->gi_dep, gdep, s)) || (rc = ix->upload(&ix->gi_ppos, gpp, s))) return rc;
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
       (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)) ||
       (rc = ix->alloc(&ix->prune_ctr, 8)))
@@ -1249,6 +1270,9 @@ int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipS
   pa.T0 = T0;
   pa.ldT0 = ldT0;
   pa.gnodes_max = ix->prn_gmax;
+  pa.gi_dep = ix->gi_dep;
+  pa.gi_ppos = ix->gi_ppos;
+  pa.gmaxdep = ix->prn_maxdep;
   if (live) {   // the per-call filter's live block list (count in ctr[5])
     pa.blk_grp = ix->blk_grp;
     pa.nblk = ((int64_t)ix->NL_iso + 15) / 16;

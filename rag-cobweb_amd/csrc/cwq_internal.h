@@ -206,7 +206,9 @@ struct PruneArgs {
   const float* Ar; const float* Br;   // row-major fp32 A, B of the internal nodes [NI][DP]
   const int* par_int; const float* w_int; const float* logdet_int;
   const int* gint;              // pruning group of each internal node (-1: the root)
-  const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists
+  const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists (BFS order)
+  const int* gi_dep; const int* gi_ppos;    // per list entry: tree depth, the parent's list position (-1: the root)
+  int gmaxdep;                              // deepest internal node of any group
   const GroupBound* gb;
   double* kpart;                // [2][nq][G]: P0-free part of KUB, and the margin's magnitude term
   float* S; float* P;           // [nq][ldS]

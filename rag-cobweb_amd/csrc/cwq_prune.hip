@@ -84,27 +84,10 @@ hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, con
   return hipGetLastError();
 }
 
-// Exact prefix of internal node i for query q from the raw sums S (the node's ancestors all
-// computed): internal_chain_kernel's arithmetic, top-down, bit for bit.
-__device__ __forceinline__ float prune_chain_prefix(const PruneArgs& a, int q, int i) {
-  const size_t ro = (size_t)q * a.ldS;
-  int d = 0;
-  for (int j = i; a.par_int[j] >= 0 && d < kMaxChain; j = a.par_int[j]) ++d;
-  float P = 0.f;
-  for (int l = d; l >= 0; --l) {
-    int j = i;
-    for (int u = 0; u < l; ++u) j = a.par_int[j];
-    const float lp = -0.5f * (a.logdet_int[j] + a.S[ro + j]);
-    P = (l == d) ? a.w_int[j] * lp : fmaf(a.w_int[j], lp, P);
-  }
-  return P;
-}
-
 // P, and the filters' tables [Plo, Phi] of node i (internal_chain_kernel's tail: the
 // group-centred rows' shifted prefix, outward-rounded).
-__device__ __forceinline__ void prune_write_prefix(const PruneArgs& a, int q, int i) {
+__device__ __forceinline__ void prune_write_tables(const PruneArgs& a, int q, int i, float P) {
   const size_t o = (size_t)q * a.ldS + i;
-  const float P = prune_chain_prefix(a, q, i);
   a.P[o] = P;
   const int g = a.grp[i];
   if (g < 0) {
@@ -122,6 +105,27 @@ __device__ __forceinline__ void prune_write_prefix(const PruneArgs& a, int q, in
   a.Phi[o] = __double2float_ru(tt + e);
 }
 
+// The prefixes and tables of group g's internal nodes for query q, level by level down the
+// group's BFS-ordered list: P(i) = fmaf(w_i, lp'(i), P(parent)) with the parent's P from LDS
+// (s_P[position - gi_ptr[g]]; the root's P0 from P[q][0]) -- internal_chain_kernel's
+// top-down chain, the same values, without walking every node's chain from the root.  nt threads; the raw
+// sums S of the group's nodes must be complete and visible.
+__device__ __forceinline__ void prune_group_prefixes(const PruneArgs& a, int q, int g, float* s_P, int nt) {
+  const int b0 = a.gi_ptr[g], b1 = a.gi_ptr[g + 1];
+  const float P0 = a.P[(size_t)q * a.ldS];
+  for (int L = 1; L <= a.gmaxdep; ++L) {
+    for (int j = b0 + (int)threadIdx.x; j < b1; j += nt) {
+      if (a.gi_dep[j] != L) continue;
+      const int node = a.gi_nodes[j], pp = a.gi_ppos[j];
+      const float lp = -0.5f * (a.logdet_int[node] + a.S[(size_t)q * a.ldS + node]);
+      const float P = fmaf(a.w_int[node], lp, pp < 0 ? P0 : s_P[pp - b0]);
+      s_P[j - b0] = P;
+      prune_write_tables(a, q, node, P);
+    }
+    __syncthreads();
+  }
+}
+
 // The bound terms of one (query, group) pair, by one wave: the group shift -2 x'.d_g and its
 // error bound (as group_shift_kernel), |x - c_g|^2, and the terms of KUB that do not depend
 // on the root's prefix P0: kpart[0] = max(Cmin UB, Cmax UB), kpart[1] = Cmax mag (the margin's).
@@ -129,13 +133,16 @@ __device__ __forceinline__ void prune_write_prefix(const PruneArgs& a, int q, in
 //   >= (1 - 2^-16) (sqrt(wmin) dlo - 2^-23 sqrt(wmax) mmax)_+^2 (t = x A - B with B = fl(mu
 //   A), the partial sums' relative error < 64 * 2^-24); lp'_fp32 = fl(-0.5 fl(logdet + S))
 //   <= -logdet/2 + 2^-22 |logdet| - (1/2 - 2^-22) S_fp32 = UB; |lp'| <= mag.
-__device__ __forceinline__ void prune_group_terms(const PruneArgs& a, int64_t qi, int g, int lane) {
+// xs / c0s: the query and the root centre (LDS copies in the head kernel).
+__device__ __forceinline__ void prune_group_terms(const PruneArgs& a, const float* xs, const float* c0s, int64_t qi, int g,
+                                                  int lane) {
   double d1 = 0.0, ab = 0.0, e2 = 0.0;
+#pragma unroll 4
   for (int d = lane; d < a.D; d += 64) {
-    const float x = a.q[qi * a.D + d];
-    const float xc = x - a.c0[d];
+    const float x = xs[d];
+    const float xc = x - c0s[d];
     const float cg = a.cent[(int64_t)g * a.D + d];
-    const double dd = (double)cg - (double)a.c0[d];
+    const double dd = (double)cg - (double)c0s[d];
     const double t = (double)xc * dd;
     d1 += t;
     ab += fabs(t);
@@ -227,11 +234,13 @@ __device__ void prune_pair(const PruneArgs& a, int q, int g, float* s_x, float* 
   // the raw sums complete and visible before the chain walks read them back
   __threadfence();
   __syncthreads();
-  for (int j = b0 + (int)threadIdx.x; j < b1; j += kPrThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
-  __syncthreads();   // s_x reused by the next pair
+  prune_group_prefixes(a, q, g, s_part + kPrChunk * (a.DP / 16 + 1), kPrThreads);   // ends with a barrier
 }
 
-size_t prune_pair_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1)) * 4; }
+// s_x [DP], s_part [kPrChunk][DP/16 + 1], then the group prefixes [gnodes_max]
+size_t prune_pair_lds(int DP, int gmax) {
+  return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1) + (size_t)gmax) * 4;
+}
 
 // Head, one workgroup per query: every group's bound terms (one wave per group,
 // prune_group_terms); the root's raw sum (exact_aniso_S's arithmetic, bit for bit), its
@@ -242,6 +251,7 @@ size_t prune_pair_lds(int DP) { return ((size_t)DP + (size_t)kPrChunk * (DP / 16
 constexpr int kHdThreads = 512;
 __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs a) {
   __shared__ float s_root[128];   // DP <= 2048
+  __shared__ float s_xq[2048], s_c0[2048];   // the query and the root centre (D <= DP <= 2048)
   __shared__ float s_p0;
   __shared__ double s_best[kHdThreads / 64];
   __shared__ int s_bg[kHdThreads / 64];
@@ -261,7 +271,12 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
     }
     s_root[v] = part;
   }
-  for (int g = wave; g < a.G; g += kHdThreads / 64) prune_group_terms(a, q, g, lane);
+  for (int d = tid; d < a.D; d += kHdThreads) {
+    s_xq[d] = a.q[(int64_t)q * a.D + d];
+    s_c0[d] = a.c0[d];
+  }
+  __syncthreads();
+  for (int g = wave; g < a.G; g += kHdThreads / 64) prune_group_terms(a, s_xq, s_c0, q, g, lane);
   __syncthreads();
   if (tid == 0) {
     float acc = 0.f;
@@ -335,6 +350,78 @@ __global__ __launch_bounds__(kGsThreads) void prune_gstar_kernel(const PruneArgs
   prune_nodes_S<kGsThreads>(a, q, c0, min(kGsNodes, b1 - c0), s_x, s_part);
 }
 
+// g*'s exact pass for a batch: one workgroup per (group, kGgNodes of its nodes) serving every
+// query whose g* is that group -- the nodes' A / B rows staged in LDS once and reused by the
+// group's queries (a 1,000-query C2 chunk: ~10 queries per group; per query the same
+// arithmetic as prune_nodes_S, bit for bit).  The group's queries are found by a scan of g*
+// (windows of kGgWin queries; their order does not matter: each query's sums are its own).
+constexpr int kGgNodes = 8, kGgThreads = 256, kGgWin = 1024;
+constexpr int kGgMinQ = 96;   // chunks of at least this many queries take the grouped pass (CWQ_PRUNE_GROUPED_MIN)
+__global__ __launch_bounds__(kGgThreads) void prune_gstar_grouped_kernel(const PruneArgs a, int nb) {
+  extern __shared__ float s_dyn[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  float* s_a = s_dyn;                           // [kGgNodes][DP]
+  float* s_b = s_a + (size_t)kGgNodes * a.DP;   // [kGgNodes][DP]
+  float* s_x = s_b + (size_t)kGgNodes * a.DP;   // [DP]
+  float* s_part = s_x + a.DP;                   // [kGgNodes][LDP]
+  int* s_q = reinterpret_cast<int*>(s_part + kGgNodes * LDP);   // [kGgWin]
+  __shared__ int s_n;
+  const int g = blockIdx.x / nb, blk = blockIdx.x - g * nb;
+  const int c0 = a.gi_ptr[g] + blk * kGgNodes, b1 = a.gi_ptr[g + 1];
+  if (c0 >= b1) return;
+  const int cnt = min(kGgNodes, b1 - c0);
+  bool staged = false;
+  for (int w0 = 0; w0 < a.nq; w0 += kGgWin) {
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    for (int q = w0 + tid; q < min(a.nq, w0 + kGgWin); q += kGgThreads) {
+      const bool m = a.gstar[q] == g;
+      const uint64_t bm = __ballot(m);
+      int base = 0;
+      if (lane == 0 && bm) base = atomicAdd(&s_n, __popcll(bm));
+      base = __shfl(base, 0, 64);
+      if (m) s_q[base + __popcll(bm & ((1ull << lane) - 1))] = q;
+    }
+    __syncthreads();
+    const int n = s_n;
+    if (n == 0) continue;   // uniform
+    if (!staged) {
+      for (int it = tid; it < cnt * a.DP; it += kGgThreads) {
+        const int e = it / a.DP, d = it - e * a.DP;
+        const size_t o = (size_t)a.gi_nodes[c0 + e] * a.DP + d;
+        s_a[it] = a.Ar[o];
+        s_b[it] = a.Br[o];
+      }
+      staged = true;
+    }
+    for (int i = 0; i < n; ++i) {
+      const int q = s_q[i];
+      prune_load_query(a, q, s_x, kGgThreads);
+      __syncthreads();
+      for (int it = tid; it < cnt * NV16; it += kGgThreads) {
+        const int e = it / NV16, v = it - e * NV16;
+        const float* ar = s_a + (size_t)e * a.DP + v * 16;
+        const float* br = s_b + (size_t)e * a.DP + v * 16;
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float tt = fmaf(s_x[v * 16 + j], ar[j], -br[j]);
+          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+        }
+        s_part[e * LDP + v] = part;
+      }
+      __syncthreads();
+      if (tid < cnt) {
+        float acc = 0.f;
+        for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+        a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
+      }
+      __syncthreads();   // s_x and s_part reused by the next query
+    }
+  }
+}
+
 // Seed threshold and stage-B pairs, one workgroup per query (blocks >= nq: the sentinel fill
 // of every (query, node) outside the root and g*).  The exact keys of up to 64 sample rows of
 // g* (their parents' prefixes: written first, from prune_gstar_kernel's raw sums): every (row, slice) partial in parallel, summed
@@ -363,10 +450,8 @@ __global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArg
   const int g = a.gstar[q];
   // g*'s prefixes and tables (its raw sums: prune_gstar_kernel), read back below by the
   // sample rows whose parents they are
-  if (g >= 0) {
-    for (int j = a.gi_ptr[g] + tid; j < a.gi_ptr[g + 1]; j += kSeedThreads) prune_write_prefix(a, q, a.gi_nodes[j]);
-    __threadfence();
-  }
+  if (g >= 0) prune_group_prefixes(a, q, g, s_part + 64 * LDP, kSeedThreads);   // ends with a barrier
+  __threadfence();   // the P stores, read back below by other waves
   __syncthreads();
   const int n = g >= 0 ? min(64, a.gs_ptr[g + 1] - a.gs_ptr[g]) : 0;
   const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
@@ -480,15 +565,42 @@ hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s)
   PruneArgs a = a0;
   a.zero_total = first ? 1 : 0;
   hipLaunchKernelGGL(prune_head_kernel, dim3((unsigned)a.nq), dim3(kHdThreads), 0, s, a);
-  const int nb = (a.gnodes_max + kGsNodes - 1) / kGsNodes;
-  hipLaunchKernelGGL(prune_gstar_kernel, dim3((unsigned)((int64_t)a.nq * nb)), dim3(kGsThreads),
-                     ((size_t)a.DP + (size_t)kGsNodes * (a.DP / 16 + 1)) * 4, s, a, nb);
+  int gmin = kGgMinQ;
+  if (const char* e = getenv("CWQ_PRUNE_GROUPED_MIN")) gmin = atoi(e) > 0 ? atoi(e) : kGgMinQ;
+  if (a.nq >= gmin) {   // a batch: per (group, node chunk), the group's queries together
+    const int nbg = (a.gnodes_max + kGgNodes - 1) / kGgNodes;
+    const size_t lds = ((size_t)(2 * kGgNodes + 1) * a.DP + (size_t)kGgNodes * (a.DP / 16 + 1) + kGgWin) * 4;
+    static bool attr = false;   // dynamic LDS above the 64 KiB default (DP > 768)
+    if (!attr) {
+      if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_gstar_grouped_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
+        return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(prune_gstar_grouped_kernel, dim3((unsigned)((int64_t)a.G * nbg)), dim3(kGgThreads), lds, s, a,
+                       nbg);
+  } else {   // a few queries: per (query, node chunk)
+    const int nb = (a.gnodes_max + kGsNodes - 1) / kGsNodes;
+    hipLaunchKernelGGL(prune_gstar_kernel, dim3((unsigned)((int64_t)a.nq * nb)), dim3(kGsThreads),
+                       ((size_t)a.DP + (size_t)kGsNodes * (a.DP / 16 + 1)) * 4, s, a, nb);
+  }
+  static bool attr = false;   // the group-prefix LDS of a large group can pass the 64 KiB default
+  if (!attr) {
+    if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_seed_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
+      return e;
+    if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_stage_b_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
+      return e;
+    attr = true;
+  }
   const int64_t nfill = ((int64_t)a.nq * a.NI + kSeedThreads - 1) / kSeedThreads;
   hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads),
-                     (size_t)64 * (a.DP / 16 + 1) * 4, s, a);
+                     ((size_t)64 * (a.DP / 16 + 1) + (size_t)a.gnodes_max) * 4, s, a);
   const int64_t nw = (int64_t)a.nq * a.G;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(nw, cus));
-  hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_pair_lds(a.DP), s, a);
+  hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_pair_lds(a.DP, a.gnodes_max), s,
+                     a);
   return hipGetLastError();
 }
 
