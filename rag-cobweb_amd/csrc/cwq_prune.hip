@@ -556,6 +556,17 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_b_kernel(const PruneAr
   }
 }
 
+// A kernel's dynamic-LDS limit raised to `bytes` when that passes the 64 KiB default (and
+// what was set before): the attribute is only ever set to a size the launch requests, which
+// with the kernel's static LDS stays within the 160 KiB of a CU.
+static hipError_t lds_attr(const void* fn, size_t bytes, size_t& cur) {
+  if (bytes <= (size_t)64 * 1024 || bytes <= cur) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) cur = bytes;
+  else (void)hipGetLastError();   // not left as the runtime's sticky error for the next caller
+  return e;
+}
+
 // The whole pruned internal pass of a chunk: head, g*'s pass, seed (+ fill), stage B.
 // ctr[0..3] zeroed by the head, and ctr[4] (the call's stage-B pair total) on its first
 // pruned chunk.
@@ -570,13 +581,8 @@ hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s)
   if (a.nq >= gmin) {   // a batch: per (group, node chunk), the group's queries together
     const int nbg = (a.gnodes_max + kGgNodes - 1) / kGgNodes;
     const size_t lds = ((size_t)(2 * kGgNodes + 1) * a.DP + (size_t)kGgNodes * (a.DP / 16 + 1) + kGgWin) * 4;
-    static bool attr = false;   // dynamic LDS above the 64 KiB default (DP > 768)
-    if (!attr) {
-      if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_gstar_grouped_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
-        return e;
-      attr = true;
-    }
+    static size_t attr = 0;   // dynamic LDS above the 64 KiB default (DP > 768)
+    if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_gstar_grouped_kernel), lds, attr)) return e;
     hipLaunchKernelGGL(prune_gstar_grouped_kernel, dim3((unsigned)((int64_t)a.G * nbg)), dim3(kGgThreads), lds, s, a,
                        nbg);
   } else {   // a few queries: per (query, node chunk)
@@ -584,23 +590,17 @@ hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s)
     hipLaunchKernelGGL(prune_gstar_kernel, dim3((unsigned)((int64_t)a.nq * nb)), dim3(kGsThreads),
                        ((size_t)a.DP + (size_t)kGsNodes * (a.DP / 16 + 1)) * 4, s, a, nb);
   }
-  static bool attr = false;   // the group-prefix LDS of a large group can pass the 64 KiB default
-  if (!attr) {
-    if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_seed_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
-      return e;
-    if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&prune_stage_b_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
-      return e;
-    attr = true;
-  }
+  // the group-prefix LDS of a large group can pass the 64 KiB default
+  static size_t attr_seed = 0, attr_b = 0;
+  const size_t lds_seed = ((size_t)64 * (a.DP / 16 + 1) + (size_t)a.gnodes_max) * 4;
+  const size_t lds_b = prune_pair_lds(a.DP, a.gnodes_max);
+  if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_seed_kernel), lds_seed, attr_seed)) return e;
+  if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_stage_b_kernel), lds_b, attr_b)) return e;
   const int64_t nfill = ((int64_t)a.nq * a.NI + kSeedThreads - 1) / kSeedThreads;
-  hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads),
-                     ((size_t)64 * (a.DP / 16 + 1) + (size_t)a.gnodes_max) * 4, s, a);
+  hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads), lds_seed, s, a);
   const int64_t nw = (int64_t)a.nq * a.G;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(nw, cus));
-  hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), prune_pair_lds(a.DP, a.gnodes_max), s,
-                     a);
+  hipLaunchKernelGGL(prune_stage_b_kernel, dim3((unsigned)wgs), dim3(kPrThreads), lds_b, s, a);
   return hipGetLastError();
 }
 
