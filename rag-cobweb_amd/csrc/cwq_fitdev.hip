@@ -131,6 +131,8 @@ struct FitDev {
   float pv;
   int cap;                      // node slots
   float *count, *mean, *meanSq; // [cap], [cap][D]
+  float* lvar;                  // [cap][D] ref_logf(meanSq / count + pv): a node's log-variances, kept
+                                // current by fd_increment / fd_combine and set for every loaded node
   int *parent, *ccnt, *ccap;    // [cap]
   int64_t* coff;                // [cap] child slab offset in the arena
   int* arena;
@@ -314,8 +316,10 @@ __device__ __forceinline__ void fd_increment(const FitDev& f, int s, const float
     const float cnt = cd + 1.0f;
     const float delta = x[d] - f.mean[o];
     const float m = f.mean[o] + delta / cnt;
-    f.meanSq[o] = f.meanSq[o] + delta * (x[d] - m);
+    const float m2 = f.meanSq[o] + delta * (x[d] - m);
+    f.meanSq[o] = m2;
     f.mean[o] = m;
+    f.lvar[o] = ref_logf(m2 / cnt + f.pv);   // the T / split terms' log (count = cnt below)
   }
   __syncthreads();
   if (threadIdx.x == 0) f.count[s] = cd + 1.0f;
@@ -330,8 +334,10 @@ __device__ __forceinline__ void fd_combine(const FitDev& f, int dst, int src) {
     const size_t o = (size_t)dst * f.D + d, os = (size_t)src * f.D + d;
     const float delta = f.mean[os] - f.mean[o];
     const float tot = cd + cs;
-    f.meanSq[o] = (f.meanSq[o] + f.meanSq[os]) + (delta * delta) * ((cd * cs) / tot);
+    const float m2 = (f.meanSq[o] + f.meanSq[os]) + (delta * delta) * ((cd * cs) / tot);
+    f.meanSq[o] = m2;
     f.mean[o] = (cd * f.mean[o] + cs * f.mean[os]) / tot;
+    f.lvar[o] = ref_logf(m2 / tot + f.pv);
   }
   __syncthreads();
   if (threadIdx.x == 0) f.count[dst] = cd + cs;
@@ -464,35 +470,55 @@ __device__ __forceinline__ float fd_kl_score(float sa, float sb, int D) {
   score = score / 2.0f;
   return score;
 }
-// The per-child KL terms of one wave, summed in torch's order (torch_sum2): U = KL(c + x ||
-// P + x) and T = KL(c || P + x) for child c (two sums each)
-__device__ __forceinline__ void fd_kl_UT(const FitDev& f, const FdShared& sh, int c, int lane, float& U, float& T) {
+// The per-child KL terms, summed in torch's order (torch_sum2), two children per wave (c0 on
+// lanes 0-31, c1 on 32-63).  U = KL(c + x || P + x): mean_var_insert's ops, a log per term
+// (x enters the variance)
+__device__ __forceinline__ void fd_kl_U2(const FitDev& f, const FdShared& sh, int c0, int c1, int lane, float& U0,
+                                        float& U1) {
 #pragma clang fp contract(off)
   const int D = f.D;
   const float pv = f.pv;
-  const float cc = f.count[c];
+  const int c = (lane >> 5) ? c1 : c0;
+  const float cnt = f.count[c] + 1.0f;
+  const float ycnt = FIT_RECIP(cnt);
   float sa, sb;
-  // U on lanes 0-31, T on lanes 32-63 (the same instructions: only (mu1, v1) differ)
-  const float cnt = cc + 1.0f;
-  // the divisors' reciprocals (read by div_rn in the FIT_DIV_RN build only)
-  const float ycnt = FIT_RECIP(cnt), yvar = (lane >> 5) ? FIT_RECIP(cc) : ycnt;
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
-    // U: c + x (fd_insert_mv's ops); T: c as is (m2 / cc + pv) -- one variance division per
-    // lane, the operands selected per half
-    const float m = f.mean[(size_t)c * D + d], m2 = f.meanSq[(size_t)c * D + d];
+    const size_t o = (size_t)(h ? c1 : c0) * D + d;
+    const float m = f.mean[o], m2 = f.meanSq[o];
     const float xd = sh.x[d];
     const float delta = xd - m;
     const float mm = m + KDIV(delta, cnt, ycnt);
-    const float mu1 = h ? m : mm;
-    const float num = h ? m2 : m2 + delta * (xd - mm);
-    const float v1 = KDIV(num, (h ? cc : cnt), yvar) + pv;
+    const float num = m2 + delta * (xd - mm);
+    const float v1 = KDIV(num, cnt, ycnt) + pv;
     a = sh.lv2[d] - fd_logf(sh, v1);
-    const float df = mu1 - sh.mu2[d];
+    const float df = mm - sh.mu2[d];
     b = KDIV((v1 + df * df), sh.v2[d], sh.rv2[d]);
   }, sa, sb);
   const float k = fd_kl_score(sa, sb, D);
-  U = __shfl(k, 0, 64);
-  T = __shfl(k, 32, 64);
+  U0 = __shfl(k, 0, 64);
+  U1 = __shfl(k, 32, 64);
+}
+// T = KL(c || P + x) of two children in one wave: the child's log-variance from its cache
+// (lvar: the same ref_logf of the same m2 / cc + pv), so no log per term
+__device__ __forceinline__ void fd_kl_T2(const FitDev& f, const FdShared& sh, int c0, int c1, int lane, float& T0,
+                                        float& T1) {
+#pragma clang fp contract(off)
+  const int D = f.D;
+  const float pv = f.pv;
+  const float cc = f.count[(lane >> 5) ? c1 : c0];
+  const float ycc = FIT_RECIP(cc);
+  float sa, sb;
+  torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
+    const size_t o = (size_t)(h ? c1 : c0) * D + d;
+    const float m = f.mean[o], m2 = f.meanSq[o];
+    const float v1 = KDIV(m2, cc, ycc) + pv;
+    a = sh.lv2[d] - f.lvar[o];
+    const float df = m - sh.mu2[d];
+    b = KDIV((v1 + df * df), sh.v2[d], sh.rv2[d]);
+  }, sa, sb);
+  const float k = fd_kl_score(sa, sb, D);
+  T0 = __shfl(k, 0, 64);
+  T1 = __shfl(k, 32, 64);
 }
 // KL(c || ref) with the reference vectors (mu, v, log v) given
 __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, const float* mu, const float* v,
@@ -504,7 +530,7 @@ __device__ __forceinline__ float fd_kl_ref(const FitDev& f, const FdShared& sh, 
   float sa, sb;
   torch_sum2(D, lane, [&](int d, float& a, float& b) {
     const float mu1 = f.mean[(size_t)c * D + d], v1 = KDIV(f.meanSq[(size_t)c * D + d], cc, ycc) + f.pv;
-    a = lv[d] - fd_logf(sh, v1);
+    a = lv[d] - f.lvar[(size_t)c * D + d];   // = fd_logf(sh, v1), cached
     const float df = mu1 - mu[d];
     b = KDIV((v1 + df * df), v[d], rv[d]);
   }, sa, sb);
@@ -522,7 +548,7 @@ __device__ __forceinline__ void fd_kl_ref2(const FitDev& f, const FdShared& sh, 
   torch_sum2_halves(D, lane, [&](int d, int h, float& a, float& b) {
     const size_t o = (size_t)(h ? c1 : c0) * D + d;
     const float mu1 = f.mean[o], v1 = KDIV(f.meanSq[o], (h ? cc1 : cc0), ycc) + f.pv;
-    a = lv[d] - fd_logf(sh, v1);
+    a = lv[d] - f.lvar[o];   // = fd_logf(sh, v1), cached
     const float df = mu1 - mu[d];
     b = KDIV((v1 + df * df), v[d], rv[d]);
   }, sa, sb);
@@ -549,11 +575,16 @@ __device__ __forceinline__ void fd_job_child(const FitDev& f, const FdShared& sh
                                              int lane) {
   // the butterfly leaves the sums in every lane: every lane stores the same words (no
   // lane-divergent region inside the claim loops -- cf. fd_fork)
-  if (type == 0) {
-    float U, T;
-    fd_kl_UT(f, sh, f.arena[base + j], lane, U, T);
-    st_agent_f(&f.kres[2 * j], U);
-    st_agent_f(&f.kres[2 * j + 1], T);
+  if (type == 0) {   // kofs = the level's children b: items 0..nP-1 U pairs, nP..2nP-1 T pairs
+    const int b = kofs, nP = (b + 1) / 2, i = j < nP ? j : j - nP;
+    const int j0 = 2 * i, j1 = 2 * i + 1 < b ? 2 * i + 1 : 2 * i;
+    const int c0 = f.arena[base + j0], c1 = f.arena[base + j1];
+    float K0, K1;
+    if (j < nP) fd_kl_U2(f, sh, c0, c1, lane, K0, K1);
+    else fd_kl_T2(f, sh, c0, c1, lane, K0, K1);
+    const int w = j < nP ? 0 : 1;
+    st_agent_f(&f.kres[2 * j0 + w], K0);
+    st_agent_f(&f.kres[2 * j1 + w], K1);
   } else {
     const float K = fd_kl_ref(f, sh, sh.muP, sh.vP, sh.rvP, sh.lvP, f.jobs[j], lane);
     st_agent_f(&f.kres[kofs + j], K);
@@ -703,9 +734,9 @@ __device__ __forceinline__ bool fd_fork(const FitDev& f, FdShared& sh, int64_t r
     mt_gen_wave(sh.mt, sh.mtn, idx, nrnd, f.rnd, lane);
     if (lane == 0) mt_idx = idx;
   }
-  if (wave == 1 && type == 0) {
+  if (wave == 1 && type == 0) {   // kofs = the level's children
     const float K = fd_kl_new(f, sh, lane);
-    if (lane == 0) f.kres[2 * n] = K;
+    if (lane == 0) f.kres[2 * kofs] = K;
   }
   for (;;) {   // per wave; every lane in every atomic (fd_help_job)
     const int v = atomicAdd(&job->next[slot][0], lane == 0 ? kFdWaveClaim : 0);
@@ -922,7 +953,7 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
       // child, the draws sequential below)
       const bool forked = f.job != nullptr && b >= f.fork_min;
       if (forked) {
-        if (!fd_fork(f, sh, row, 0, b, cbase, 0, 2 * (int64_t)b, mt_idx)) {
+        if (!fd_fork(f, sh, row, 0, 2 * ((b + 1) / 2), cbase, b, 2 * (int64_t)b, mt_idx)) {
           if (tid == 0) f.ctrl[3] = FD_HANG;
           break;
         }
@@ -934,17 +965,25 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
           if (lane == 0) mt_idx = idx;
         }
         if (b >= kFdParTop && tid == 0) drawn += b;
-        for (int j = wave; j <= b; j += kFdWaves) {
-          if (j < b) {
-            float U, T;
-            fd_kl_UT(f, sh, f.arena[cbase + j], lane, U, T);
-            if (lane == 0) {
-              f.kres[2 * j] = U;
-              f.kres[2 * j + 1] = T;
-            }
-          } else {
+        // tasks: the U pairs (a log per term) first, then the new leaf, then the T pairs
+        // (cached logs), so the heavy waves go in the first round
+        const int nP = (b + 1) / 2;
+        for (int t = wave; t < 2 * nP + 1; t += kFdWaves) {
+          if (t == nP) {
             const float K = fd_kl_new(f, sh, lane);
             if (lane == 0) f.kres[2 * b] = K;
+            continue;
+          }
+          const int i = t < nP ? t : t - nP - 1;
+          const int j0 = 2 * i, j1 = 2 * i + 1 < b ? 2 * i + 1 : 2 * i;
+          const int c0 = f.arena[cbase + j0], c1 = f.arena[cbase + j1];
+          float K0, K1;
+          if (t < nP) fd_kl_U2(f, sh, c0, c1, lane, K0, K1);
+          else fd_kl_T2(f, sh, c0, c1, lane, K0, K1);
+          const int w = t < nP ? 0 : 1;
+          if (lane == 0) {
+            f.kres[2 * j0 + w] = K0;
+            f.kres[2 * j1 + w] = K1;
           }
         }
       }
@@ -1288,6 +1327,16 @@ __global__ __launch_bounds__(kFdThreads) void fit_insert_kernel(const FitDev f, 
   }
 }
 
+// lvar[n][d] = ref_logf(meanSq / count + pv) for nodes 0..n-1 (count 0: unused slot, 0)
+__global__ void fd_lvar_kernel(const FitDev f, int n) {
+#pragma clang fp contract(off)
+  const int64_t nt = (int64_t)n * f.D;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nt; t += (int64_t)gridDim.x * blockDim.x) {
+    const float c = f.count[t / f.D];
+    f.lvar[t] = c > 0.f ? ref_logf(f.meanSq[t] / c + f.pv) : 0.f;
+  }
+}
+
 }  // namespace cwq
 
 using namespace cwq;
@@ -1327,6 +1376,7 @@ extern "C" int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t 
   };
   const size_t C = (size_t)cap_nodes;
   bool ok = al((void**)&f.count, C * 4) && al((void**)&f.mean, C * dim * 4) && al((void**)&f.meanSq, C * dim * 4) &&
+            al((void**)&f.lvar, C * dim * 4) &&
             al((void**)&f.parent, C * 4) && al((void**)&f.ccnt, C * 4) && al((void**)&f.ccap, C * 4) &&
             al((void**)&f.coff, C * 8) && al((void**)&f.arena, (size_t)f.arena_cap * 4) &&
             al((void**)&f.ctrl, 64) && al((void**)&f.ctrl64, 64) &&
@@ -1401,6 +1451,12 @@ extern "C" int cwq_fit_load(cwq_fit* h, int32_t n_nodes, int32_t root, const int
   FCPY(f.ctrl64, ctrl64.data(), ctrl64.size() * 8);
   FCPY(f.mt, mt_state, (size_t)kMtN * 4);
 #undef FCPY
+  {   // the loaded nodes' log-variances (the cache fd_increment / fd_combine keep current)
+    const int64_t nt = (int64_t)n_nodes * D;
+    hipLaunchKernelGGL(fd_lvar_kernel, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 65536)), dim3(256), 0, s, f,
+                       n_nodes);
+    if (hipGetLastError() != hipSuccess) return fit_fail(CWQ_ERR_HIP, "cwq_fit_load log-variance launch failed");
+  }
   if (hipStreamSynchronize(s) != hipSuccess) return fit_fail(CWQ_ERR_HIP, "cwq_fit_load sync failed");
   return CWQ_OK;
 }

@@ -356,7 +356,11 @@ __global__ __launch_bounds__(kGsThreads) void prune_gstar_kernel(const PruneArgs
 // arithmetic as prune_nodes_S, bit for bit).  The group's queries are found by a scan of g*
 // (windows of kGgWin queries; their order does not matter: each query's sums are its own).
 constexpr int kGgNodes = 8, kGgThreads = 256, kGgWin = 1024;
-constexpr int kGgMinQ = 96;   // chunks of at least this many queries take the grouped pass (CWQ_PRUNE_GROUPED_MIN)
+// Off by default: measured slower (C2 batch, 1,000 queries: 1,163 us against 309 us for the
+// per-query pass, profiles/r05_c2_batch_grouped_rocprof_kernel_stats.csv -- each workgroup
+// walks its group's queries one after another, a load round trip and three barriers per
+// query); CWQ_PRUNE_GROUPED_MIN = n takes it for chunks of >= n queries (A/B).
+constexpr int kGgMinQ = 0x7fffffff;
 __global__ __launch_bounds__(kGgThreads) void prune_gstar_grouped_kernel(const PruneArgs a, int nb) {
   extern __shared__ float s_dyn[];
   const int tid = threadIdx.x, lane = tid & 63;

@@ -97,6 +97,8 @@ def main():
             print(f"  ifit rows {a0}..{a1}: {(a1 - a0) / dt:.0f} inserts/s ({dt:.1f} s), total "
                   f"{time.perf_counter() - t0:.1f} s", flush=True)
         t_fit = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        w.build_prediction_index()
     else:
         w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(args.n)], corpus_embeddings=X)
         torch.cuda.synchronize()
