@@ -191,7 +191,9 @@ int cwq_last_timing(cwq_index* idx, float* out8);
  * choice; results are identical either way).
  *   mode -1: automatic (default; env CWQ_FILTER=0/1 overrides): the bf16-MFMA
  *            candidate filter + exact rerank when k <= 64 and the index holds
- *            >= 16384 isotropic rows, the exact fp32 scan otherwise
+ *            >= 16384 isotropic rows, the exact fp32 scan otherwise; an index on which
+ *            >= 9 in 10 of its first >= 256 filtered queries had to be re-run exactly (the
+ *            bounds too loose for its rows) stays on the exact scan from then on
  *   mode  0: always the exact fp32 scan      mode 1: the filter whenever k <= 64
  * Calls with nq <= 64 take the small-batch stream filter instead of the batch MFMA
  * filter (one HBM pass over the bf16 row panel; env CWQ_STREAM=0 disables it).

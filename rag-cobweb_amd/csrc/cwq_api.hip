@@ -139,6 +139,11 @@ struct cwq_index {
   // per-group bound constants.  prune_ctr: the last call's stage-B pair count (diagnostics).
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
+  // auto mode's record of the filter on this index: queries filtered / re-run exactly; when
+  // at least 9 in 10 of >= 256 queries had to be re-run (the bounds too loose for this
+  // tree's rows), auto mode takes the exact scan from then on (same results, less work)
+  int64_t filt_q = 0, filt_fb = 0;
+  bool filt_auto_off = false;
   int prn_gmax = 1;   // the most internal nodes of one pruning group
   int prn_maxdep = 0;   // deepest internal node of any group
   int *gi_dep = nullptr, *gi_ppos = nullptr;   // per group-list entry: depth, the parent's list position
@@ -1718,8 +1723,16 @@ bool use_filter(const cwq_index* ix, int k, int min_rows = kFiltMinRows) {
     const char* e = getenv("CWQ_FILTER");
     if (e && *e) mode = atoi(e) ? 1 : 0;
   }
-  if (mode < 0) return ix->NL_iso >= min_rows;
+  if (mode < 0) return ix->NL_iso >= min_rows && !ix->filt_auto_off;
   return mode == 1;
+}
+
+// After a Fast call (cwq_last_stats' record): the auto-mode filter record of the index.
+void note_filter(cwq_index* ix) {
+  if (ix->stats[2] == 0 || ix->stats[0] <= 0 || ix->filter >= 0) return;
+  ix->filt_q += ix->stats[0];
+  ix->filt_fb += ix->stats[1];
+  if (ix->filt_q >= 256 && ix->filt_fb * 10 >= ix->filt_q * 9) ix->filt_auto_off = true;
 }
 
 // fgemm launch geometry: query groups over the 8 XCDs (each keeps its query panel in
@@ -2504,7 +2517,9 @@ extern "C" int cwq_score_topk(cwq_index* ix, const float* q, int64_t nq, int32_t
   WsUse wu(ix, s);
   ScanCfgScope scs(nq);
   if (wu.rc) return wu.rc;
-  return score_topk_impl(ix, q, nq, k, ids, scores, s, true);
+  const int rc = score_topk_impl(ix, q, nq, k, ids, scores, s, true);
+  if (!rc) note_filter(ix);
+  return rc;
 }
 
 // The reference harness's call with host memory on both sides (benchmark_utils.py:801-805:
@@ -2534,6 +2549,7 @@ extern "C" int cwq_score_topk_host(cwq_index* ix, const float* q, int64_t nq, in
   int64_t* hid = (int64_t*)ix->hout;
   float* hsc = (float*)((char*)ix->hout + ib);
   if ((rc = score_topk_impl(ix, (const float*)ix->dq, nq, k, hid, hsc, s, true))) return rc;
+  note_filter(ix);
   HIPCHK(sync_spin(s));
   ix->ws_idle = true;   // synchronized
   memcpy(ids, hid, (size_t)nq * k * 8);

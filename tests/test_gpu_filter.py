@@ -111,6 +111,30 @@ def test_candidate_overflow_falls_back(gpu):
     assert torch.equal(ids0, ids1) and torch.equal(s0, s1)
 
 
+def test_auto_mode_drops_a_failing_filter(gpu):
+    """Auto mode: an index on which >= 9 in 10 of >= 256 filtered queries overflow their
+    candidate lists (every query next to 6,000 identical leaves) takes the exact scan from then
+    on -- same answers, the filter's pass no longer paid for nothing; mode 1 still forces it."""
+    X = gpu.synth.synthetic_corpus(20000, 64, seed=17)
+    X[2000:8000] = X[2000]
+    ix = flat_index(gpu, X)
+    Q = X[2000].repeat(300, 1) + 0.01 * gpu.synth.synthetic_corpus(300, 64, seed=18)
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, 10)
+    ix.set_filter(-1)
+    ids1, s1 = ix.score_topk(Q, 10)
+    st = ix.last_stats()
+    assert st["filter_used"] and st["fallback_queries"] >= 270, st
+    ids2, s2 = ix.score_topk(Q, 10)
+    assert not ix.last_stats()["filter_used"]
+    ix.set_filter(1)
+    ids3, s3 = ix.score_topk(Q, 10)
+    assert ix.last_stats()["filter_used"]
+    ix.set_filter(-1)
+    for i, s_ in ((ids1, s1), (ids2, s2), (ids3, s3)):
+        assert torch.equal(ids0, i) and torch.equal(s0, s_)
+
+
 @pytest.mark.parametrize("shift,scale", [(50.0, 1.0), (0.0, 100.0), (0.0, 0.01), (-3.0, 7.0)])
 def test_offset_and_scale(gpu, shift, scale):
     X = gpu.synth.synthetic_corpus(8000, 128, seed=21) * scale + shift
