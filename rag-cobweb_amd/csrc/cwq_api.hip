@@ -1716,14 +1716,18 @@ inline int dir_per_q(const cwq_index* ix) { return ix->grp_mode ? 4 * kFgDirPerQ
 // stream path pays no batch pipeline and wins from a few hundred rows on -- the exact
 // scan's per-call cost on a 1.5k-row tree is its scalar query-slice latency chain, 0.3 ms)
 constexpr int kStreamMinRows = 512;
-bool use_filter(const cwq_index* ix, int k, int min_rows = kFiltMinRows) {
+// fast: a Fast call (score_topk), which the auto-mode record can turn off; categorize keeps
+// its own rule (its per-call lists still pay on a tree whose Fast filter fails: 500k x 768
+// Basic one query per call 4.0 ms with the filter, 8.3 ms without,
+// profiles/r05_c500k_probe_v1.log / _v2.log)
+bool use_filter(const cwq_index* ix, int k, int min_rows = kFiltMinRows, bool fast = true) {
   if (k > kFiltMaxK || ix->NL_iso == 0 || !ix->iso_Mb) return false;
   int mode = ix->filter;
   if (mode < 0) {
     const char* e = getenv("CWQ_FILTER");
     if (e && *e) mode = atoi(e) ? 1 : 0;
   }
-  if (mode < 0) return ix->NL_iso >= min_rows && !ix->filt_auto_off;
+  if (mode < 0) return ix->NL_iso >= min_rows && !(fast && ix->filt_auto_off);
   return mode == 1;
 }
 
@@ -2831,7 +2835,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int kl = 64;
   int rc;
   const char* ce = getenv("CWQ_CAT_FILTER");
-  const bool filt = allow_filter && use_filter(ix, R) && !(ce && *ce && atoi(ce) == 0);
+  const bool filt = allow_filter && use_filter(ix, R, kFiltMinRows, false) && !(ce && *ce && atoi(ce) == 0);
   const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
   const size_t filt_q = filt ? iso_filter_bytes_per_query(ix, n_rt) : 0;
   const int nqb_est = n_qblocks_for(nq, kl);
