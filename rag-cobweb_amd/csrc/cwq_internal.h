@@ -496,6 +496,37 @@ __device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr,
   }
 }
 
+// The best 64 of this sorted list and another (lane i holds each list's i-th entry in
+// entry_before order, lanes past a list's length invalid: key -inf, row INT_MAX): the other
+// list reversed against this one keeps the better of each pair -- a bitonic sequence that
+// holds the union's best 64 -- and six half-cleaner stages sort it.  Rows are distinct
+// across the two lists, so the result's first K lanes are exactly what K serial
+// list64_insert_aux calls would leave, in ~7 shuffle rounds instead of up to 64 inserts.
+__device__ __forceinline__ void list64_merge_aux(float& lk, float& la, int& lr, int lane, float ok, float oa, int orow,
+                                                 bool cat) {
+  {
+    const int rl = 63 - lane;
+    const float rk = __shfl(ok, rl, 64), ra = __shfl(oa, rl, 64);
+    const int rr = __shfl(orow, rl, 64);
+    if (entry_before(rk, ra, rr, lk, la, lr, cat)) {
+      lk = rk;
+      la = ra;
+      lr = rr;
+    }
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    const float pk = __shfl_xor(lk, s, 64), pa = __shfl_xor(la, s, 64);
+    const int pr = __shfl_xor(lr, s, 64);
+    const bool take = (lane & s) ? entry_before(lk, la, lr, pk, pa, pr, cat) : entry_before(pk, pa, pr, lk, la, lr, cat);
+    if (take) {
+      lk = pk;
+      la = pa;
+      lr = pr;
+    }
+  }
+}
+
 __device__ __forceinline__ void list64_offer(float& lk, int& lr, int lane, float key, int row, int K) {
   const float tk = rl_f2(lk, K - 1);
   const int tr = __builtin_amdgcn_readlane(lr, K - 1);

@@ -1391,13 +1391,15 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // second-level b2 (T2[node] / min(T2[parent], lp), cat_t2_kernel's values: the chain minimum
 // below the group root, formed down the path as the children are pushed), the parent's
 // bottleneck and has_sent -- all known when the entry is pushed (a child's BF is
-// min(BF[parent], LPF), run_internal's own recurrence), so a pop reads no global memory but
-// an internal node's child range, and the children's LPF / BFS index / has_sent come in one
-// round trip.
-constexpr int kTwoHeapLds = 4096;
+// min(BF[parent], LPF), run_internal's own recurrence) -- and an internal node's child range
+// and child count, read with the node's own LPF when its parent pushes it.  So a pop of an
+// internal node is one load round trip (its children's LPF / BFS index / has_sent / child
+// ranges, 64 at a time), a row's none.  The heap holds kTwoHeapLds entries of 44 B.
+constexpr int kTwoHeapLds = 3072;
 struct TwoRec {
   float b, b2, pb;
   int hs;
+  int cb, ce, nch;   // an internal node's child range and child count (read when it is pushed)
 };
 
 __device__ void xheap_push(HeapEnt* h, TwoRec* hx, int64_t& n, const HeapEnt& e, const TwoRec& x, int lane) {
@@ -1493,7 +1495,9 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   if (!status) {
     const float b0 = BF[0];   // the root: BF = its own lp; T2 = +inf when at G (it is the group root)
     xheap_push(h, hx, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0},
-               TwoRec{b0, b0 == G ? CWQ_INF : -CWQ_INF, CWQ_INF, a.int_has_sent[0] != 0 ? 1 : 0}, lane);
+               TwoRec{b0, b0 == G ? CWQ_INF : -CWQ_INF, CWQ_INF, a.int_has_sent[0] != 0 ? 1 : 0,
+                      a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0]},
+               lane);
   }
   while (hn > 0) {
     TwoRec x;
@@ -1521,8 +1525,8 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
     if (found == a.k) break;
     if (is_int) {
       const int u = e.node;
-      const int cb = a.int_child_begin[u], ce = a.int_child_end[u];
-      calls += a.int_nchild[u];
+      const int cb = x.cb, ce = x.ce;   // from the entry: no load round trip before the children's
+      calls += x.nch;
       // room for every push of this pop (internal children + at most 2R list rows)
       if (hn + (ce - cb) + 2 * R > hcap) {
         status = 1;
@@ -1534,12 +1538,15 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
         const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
         const int tb = ok ? a.int_bfs[c] : 0;
         const int hs = ok ? (a.int_has_sent[c] != 0 ? 1 : 0) : 0;
+        const int ccb = ok ? a.int_child_begin[c] : 0, cce = ok ? a.int_child_end[c] : 0;
+        const int cnc = ok ? a.int_nchild[c] : 0;
         const int m = min(64, ce - c0);
         for (int j = 0; j < m; ++j) {
           const float lj = __shfl(lpf, j, 64);
           const float bj = fminf(b, lj);   // BF[child] = min(BF[u], LPF[child])
           const float t2 = bj != G ? -CWQ_INF : (b > G ? CWQ_INF : fminf(lj, x.b2));
-          xheap_push(h, hx, hn, HeapEnt{lj, e.score, __shfl(tb, j, 64), c0 + j}, TwoRec{bj, t2, b, __shfl(hs, j, 64)},
+          xheap_push(h, hx, hn, HeapEnt{lj, e.score, __shfl(tb, j, 64), c0 + j},
+                     TwoRec{bj, t2, b, __shfl(hs, j, 64), __shfl(ccb, j, 64), __shfl(cce, j, 64), __shfl(cnc, j, 64)},
                      lane);
         }
       }
@@ -1552,7 +1559,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
           const float sc = l == 0 ? rl_f(x1, j) : rl_f(x2, j);
           const int tbr = l == 0 ? rl_i(tb1, j) : rl_i(tb2, j);
           const int hsr = l == 0 ? rl_i(hs1, j) : rl_i(hs2, j);
-          xheap_push(h, hx, hn, HeapEnt{sc, e.score, tbr, -(r + 1)}, TwoRec{fminf(b, sc), fminf(x.b2, sc), b, hsr},
+          xheap_push(h, hx, hn, HeapEnt{sc, e.score, tbr, -(r + 1)}, TwoRec{fminf(b, sc), fminf(x.b2, sc), b, hsr, 0, 0, 0},
                      lane);
         }
       }

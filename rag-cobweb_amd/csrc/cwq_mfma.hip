@@ -2288,24 +2288,18 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       __syncthreads();
       if (wave > 0 && wave < nkw) {
         s_ml[tid] = lane < K ? lk : -CWQ_INF;
-        s_ma[tid] = la;
+        s_ma[tid] = lane < K ? la : CWQ_INF;
         s_mr[tid] = lane < K ? lr : 0x7fffffff;
       }
       __syncthreads();
       if (wave == 0) {
-        for (int w = 1; w < nkw; ++w) {
-          const float key = s_ml[w * 64 + lane], lp = s_ma[w * 64 + lane];
-          const int rid = s_mr[w * 64 + lane];
-          const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
-          const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-          uint64_t mask = __ballot(rid != 0x7fffffff && entry_before(key, lp, rid, tk, ta, tr, cat));
-          while (mask) {
-            const int b = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K,
-                              cat);
-          }
+        if (lane >= K) {
+          lk = -CWQ_INF;
+          la = CWQ_INF;
+          lr = 0x7fffffff;
         }
+        for (int w = 1; w < nkw; ++w)
+          list64_merge_aux(lk, la, lr, lane, s_ml[w * 64 + lane], s_ma[w * 64 + lane], s_mr[w * 64 + lane], cat);
       }
     }
   }
@@ -2329,20 +2323,28 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (ok) {
-      for (int w = 0; w < S; ++w) {
-        if (w == sidx) continue;
-        const size_t o = ((size_t)q * S + w) * 64 + lane;
-        const float key = lane < K ? __builtin_nontemporal_load(&fx.sk[o]) : -CWQ_INF;
-        const float lp = __builtin_nontemporal_load(&fx.sa[o]);
-        const int rid = lane < K ? __builtin_nontemporal_load(&fx.sr[o]) : 0x7fffffff;
-        const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
-        const int tr = __builtin_amdgcn_readlane(lr, K - 1);
-        uint64_t mask = __ballot(rid != 0x7fffffff && entry_before(key, lp, rid, tk, ta, tr, cat));
-        while (mask) {
-          const int b = __builtin_ctzll(mask);
-          mask &= mask - 1;
-          list64_insert_aux(lk, la, lr, lane, rl_f2(key, b), rl_f2(lp, b), __builtin_amdgcn_readlane(rid, b), K, cat);
+      // the other workgroups' sorted lists merged in pairs (list64_merge_aux), all loads
+      // issued before the merges
+      if (lane >= K) {
+        lk = -CWQ_INF;
+        la = CWQ_INF;
+        lr = 0x7fffffff;
+      }
+      for (int w0 = 0; w0 < S; w0 += 8) {
+        float mk[8], ma[8];
+        int mr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int w = w0 + u;
+          const size_t o = ((size_t)q * S + (w < S ? w : sidx)) * 64 + lane;
+          const bool use = w < S && w != sidx && lane < K;
+          mk[u] = use ? __builtin_nontemporal_load(&fx.sk[o]) : -CWQ_INF;
+          ma[u] = use ? __builtin_nontemporal_load(&fx.sa[o]) : CWQ_INF;
+          mr[u] = use ? __builtin_nontemporal_load(&fx.sr[o]) : 0x7fffffff;
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (w0 + u < S && w0 + u != sidx) list64_merge_aux(lk, la, lr, lane, mk[u], ma[u], mr[u], cat);
       }
     }
     nx = __hip_atomic_load(&n_exact[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
