@@ -1383,87 +1383,134 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // node with lp == G ends it) and no second root of the group is popped; nodes below the
 // group (b < G) end it too.  Otherwise status = 1 and the host re-runs the query DENSE.
 // ---------------------------------------------------------------------------
-// The heap lives in LDS (kTwoHeapLds entries, one wave per workgroup): a two-level replay
-// pushes ~1.5k entries on C2's tree, and its pops / pushes are dependent round trips --
-// ~100 cycles in LDS instead of ~1-2 us in global memory.  A heap that outgrows it ends the
-// replay uncertified (the query goes DENSE).  Each entry carries what its pop needs (a side
-// record moved with it): the bottleneck b (BF[node], or min(BF[parent], lp) of a row), the
-// second-level b2 (T2[node] / min(T2[parent], lp), cat_t2_kernel's values: the chain minimum
-// below the group root, formed down the path as the children are pushed), the parent's
-// bottleneck and has_sent -- all known when the entry is pushed (a child's BF is
-// min(BF[parent], LPF), run_internal's own recurrence) -- and an internal node's child range
-// and child count, read with the node's own LPF when its parent pushes it.  So a pop of an
-// internal node is one load round trip (its children's LPF / BFS index / has_sent / child
-// ranges, 64 at a time), a row's none.  The heap holds kTwoHeapLds entries of 44 B.
-constexpr int kTwoHeapLds = 3072;
+// The frontier is kept as sorted runs (one wave per workgroup).  An expansion's pushes --
+// a popped internal node's children (64 at a time) and the list rows whose parent it is
+// (per list) -- are ranked among themselves in the heap order (wheap_before; they share
+// the parent's score, so (score, BFS index) decides) and written, in that order, to an LDS
+// arena; only each run's head is in the frontier: kTwoSlots head slots per lane in
+// registers.  A pop is one wave-wide argmax over the heads (a DPP max of the score, the
+// pscore / BFS tie-breaks only when scores tie) and the winner's run advances by one.  This
+// is the k-way merge of the runs, so the pops come out in exactly the order of one heap
+// holding every pushed entry (the order is total: BFS indices are distinct).  Each entry
+// carries what its pop needs (a side record beside it): the bottleneck b (BF[node], or
+// min(BF[parent], lp) of a row), the second-level b2 (T2[node] / min(T2[parent], lp),
+// cat_t2_kernel's values: the chain minimum below the group root, formed down the path as
+// the children are pushed), the parent's bottleneck and has_sent -- all known when the
+// entry is pushed (a child's BF is min(BF[parent], LPF), run_internal's own recurrence) --
+// and an internal node's child range and child count, read with the node's own LPF when
+// its parent pushes it.  So a pop of an internal node is one load round trip (its
+// children's LPF / BFS index / has_sent / child ranges, 64 at a time), a row's none.  An
+// arena or slot overflow ends the replay uncertified (the query goes DENSE).
+// (The 64-ary LDS heap this replaces spent ~4.8k cycles per pop in its three-pass wave
+// argmin and ~760 per serial push: profiles/r05_basic_percall_stamps_s32.log.)
+constexpr int kTwoArena = 3072;   // pushed entries per query (44 B each in LDS)
+constexpr int kTwoSlots = 4;      // run heads per lane: 256 live runs
 struct TwoRec {
   float b, b2, pb;
   int hs;
   int cb, ce, nch;   // an internal node's child range and child count (read when it is pushed)
 };
 
-__device__ void xheap_push(HeapEnt* h, TwoRec* hx, int64_t& n, const HeapEnt& e, const TwoRec& x, int lane) {
-  if (lane == 0) {
-    int64_t i = n;
-    while (i > 0) {
-      const int64_t p = (i - 1) >> 6;
-      const HeapEnt hp = h[p];
-      if (!wheap_before(e.score, e.pscore, e.tb, hp.score, hp.pscore, hp.tb)) break;
-      h[i] = hp;
-      hx[i] = hx[p];
-      i = p;
-    }
-    h[i] = e;
-    hx[i] = x;
-  }
-  ++n;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// float -> u32 whose unsigned order is the float order (NaN as -inf, -0 as +0: equal floats
+// equal keys); 0 is below them all
+__device__ __forceinline__ unsigned ord_f32(float f) {
+  const unsigned u = __float_as_uint(f == f ? (f == 0.f ? 0.f : f) : -CWQ_INF);
+  return u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
 }
 
-__device__ HeapEnt xheap_pop(HeapEnt* h, TwoRec* hx, int64_t& n, int lane, TwoRec& xtop) {
-  const HeapEnt top = h[0];
-  xtop = hx[0];
-  --n;
-  const HeapEnt last = h[n];
-  const TwoRec xlast = hx[n];
-  int64_t i = 0;
-  for (;;) {
-    const int64_t c0 = (i << 6) + 1;
-    if (c0 >= n) break;
-    const int64_t c = c0 + lane;
-    const bool ok = c < n;
-    HeapEnt ce = ok ? h[c] : HeapEnt{-CWQ_INF, 0.f, 0x7fffffff, 0};
-    const int b = wave_best(ok, ce.score, ce.pscore, ce.tb);
-    const float bs = __shfl(ce.score, b, 64), bp = __shfl(ce.pscore, b, 64);
-    const int bt = __shfl(ce.tb, b, 64), bn = __shfl(ce.node, b, 64);
-    if (!wheap_before(bs, bp, bt, last.score, last.pscore, last.tb)) break;
-    if (lane == 0) {
-      h[i] = HeapEnt{bs, bp, bt, bn};
-      hx[i] = hx[c0 + b];
-    }
-    i = c0 + b;
-  }
-  if (n > 0 && lane == 0) {
-    h[i] = last;
-    hx[i] = xlast;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return top;
+// max over the wave by DPP (quad swaps, half-row and row mirrors, row broadcasts): lane 63
+// ends with the maximum, read back to every lane
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));    // quad_perm 1,0,3,2
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));    // quad_perm 2,3,0,1
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));   // row_mirror
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast15
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));   // row_bcast31
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
+
+// the lane holding the frontier's first entry (wheap_before order) among lanes with ok;
+// -1 if none
+__device__ __forceinline__ int wave_first(bool ok, float sc, float ps, int tb) {
+  const unsigned k1 = ok ? ord_f32(sc) : 0u;
+  const unsigned m1 = wave_max_u32(k1);
+  uint64_t c = __ballot(ok && k1 == m1);
+  if (!c) return -1;
+  if (c & (c - 1)) {   // scores tie: the smaller pscore, then the smaller BFS index
+    const bool in = (c >> (threadIdx.x & 63)) & 1;
+    const unsigned k2 = in ? ~ord_f32(ps) : 0u;
+    const unsigned m2 = wave_max_u32(k2);
+    c = __ballot(in && k2 == m2);
+    if (c & (c - 1)) {
+      const bool in2 = (c >> (threadIdx.x & 63)) & 1;
+      const unsigned k3 = in2 ? ~(unsigned)tb : 0u;
+      const unsigned m3 = wave_max_u32(k3);
+      c = __ballot(in2 && k3 == m3);
+    }
+  }
+  return __builtin_ctzll(c);
+}
+
+__device__ __forceinline__ bool rank_before(float s1, int t1, float s2, int t2) {   // one run: same pscore
+  s1 = s1 == s1 ? s1 : -CWQ_INF;
+  s2 = s2 == s2 ? s2 : -CWQ_INF;
+  return s1 != s2 ? s1 > s2 : t1 < t2;
+}
+
+#ifndef CWQ_STAMP
+#define CWQ_STAMP 0   // diagnostic builds only (scripts/build_variant.py): cycle counts
+#endif
+#if CWQ_STAMP
+// simulate_two_kernel, query 0 of the last launch: cycles in pops / child loads / child
+// runs / list-row runs, counts of pops / internal pops / children / list rows, total
+__device__ unsigned long long g_two_stamp[16];
+extern "C" int cwq_debug_two_stamp(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_two_stamp), sizeof(unsigned long long) * (size_t)std::min(n, 16));
+}
+#define TWO_CLK() ((unsigned long long)clock64())
+#else
+#define TWO_CLK() 0ull
+#endif
 
 __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   extern __shared__ HeapEnt s_heap[];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x;
   if (q >= a.nq) return;
-  HeapEnt* h = s_heap;
-  TwoRec* hx = reinterpret_cast<TwoRec*>(s_heap + kTwoHeapLds);
-  const int64_t hcap = kTwoHeapLds;
-  int64_t hn = 0;
+  HeapEnt* ae = s_heap;                                            // the arena: runs of entries
+  TwoRec* ax = reinterpret_cast<TwoRec*>(s_heap + kTwoArena);      // their side records
+  int an = 0;                                                      // arena entries used
+  // run heads: the head entry's (score, pscore, BFS index), its arena index, the run's end
+  float hsc[kTwoSlots], hps[kTwoSlots];
+  int htb[kTwoSlots], hix[kTwoSlots], hend[kTwoSlots];
+#pragma unroll
+  for (int j = 0; j < kTwoSlots; ++j) {
+    hsc[j] = hps[j] = 0.f;
+    htb[j] = hix[j] = hend[j] = 0;   // empty: hix == hend
+  }
+  int nruns = 0;
+  // a run [i0, i1) of the arena into a free slot (the first lane with one): uniform call
+  auto add_run = [&](int i0, int i1, float sc, float ps, int tb) {
+    bool fr = false;
+#pragma unroll
+    for (int j = 0; j < kTwoSlots; ++j) fr |= hix[j] == hend[j];
+    const uint64_t fm = __ballot(fr);
+    if (lane == __builtin_ctzll(fm)) {
+      bool done = false;
+#pragma unroll
+      for (int j = 0; j < kTwoSlots; ++j)
+        if (!done && hix[j] == hend[j]) {
+          hsc[j] = sc;
+          hps[j] = ps;
+          htb[j] = tb;
+          hix[j] = i0;
+          hend[j] = i1;
+          done = true;
+        }
+    }
+    ++nruns;
+  };
   const float* BF = a.BF + (size_t)q * a.ldI;
   const int R = a.R;
   const size_t lo = (size_t)q * R;
@@ -1489,19 +1536,69 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   const int hs2 = v2 ? ((a.row_flags[w2] & FLAG_HAS_SENT) != 0) : 0;
   int status = 0, found = 0, gpops = 0;
   int64_t calls = 1, visited = 0;
+  unsigned long long c_pop = 0, c_load = 0, c_push = 0, c_rows = 0, n_int = 0, n_ch = 0, n_rows = 0;
+  const unsigned long long t_start = TWO_CLK();
   // list 1 must be full, end inside the tie at G, and hold every group root among the rows
   if (!(G > -CWQ_INF) || wG == 0x7fffffff || !(xG > G) || a.NI <= 0) status = 1;
 
   if (!status) {
     const float b0 = BF[0];   // the root: BF = its own lp; T2 = +inf when at G (it is the group root)
-    xheap_push(h, hx, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0},
-               TwoRec{b0, b0 == G ? CWQ_INF : -CWQ_INF, CWQ_INF, a.int_has_sent[0] != 0 ? 1 : 0,
-                      a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0]},
-               lane);
+    const float s0 = a.LPF[(size_t)q * a.ldI];
+    if (lane == 0) {
+      ae[0] = HeapEnt{s0, 0.f, a.int_bfs[0], 0};
+      ax[0] = TwoRec{b0, b0 == G ? CWQ_INF : -CWQ_INF, CWQ_INF, a.int_has_sent[0] != 0 ? 1 : 0, a.int_child_begin[0],
+                     a.int_child_end[0], a.int_nchild[0]};
+    }
+    an = 1;
+    add_run(0, 1, s0, 0.f, a.int_bfs[0]);
   }
-  while (hn > 0) {
-    TwoRec x;
-    const HeapEnt e = xheap_pop(h, hx, hn, lane, x);
+  while (nruns > 0) {
+    const unsigned long long tp0 = TWO_CLK();
+    // the frontier's first entry: each lane's best head, then the wave's
+    int bj = -1;
+    float bs = 0.f, bp = 0.f;
+    int bt = 0;
+#pragma unroll
+    for (int j = 0; j < kTwoSlots; ++j)
+      if (hix[j] != hend[j] && (bj < 0 || wheap_before(hsc[j], hps[j], htb[j], bs, bp, bt))) {
+        bj = j;
+        bs = hsc[j];
+        bp = hps[j];
+        bt = htb[j];
+      }
+    const int wl = wave_first(bj >= 0, bs, bp, bt);
+    if (wl < 0) {   // (the run count says a head exists)
+      status = 1;
+      break;
+    }
+    int idx = 0, iend = 0;
+#pragma unroll
+    for (int j = 0; j < kTwoSlots; ++j)
+      if (bj == j) {
+        idx = hix[j];
+        iend = hend[j];
+      }
+    idx = __builtin_amdgcn_readlane(idx, wl);
+    iend = __builtin_amdgcn_readlane(iend, wl);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the arena writes of earlier runs
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const HeapEnt e = ae[idx];
+    const TwoRec x = ax[idx];
+    if (lane == wl) {   // the run advances: its next entry is the new head
+      const bool more = idx + 1 < iend;
+      const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
+#pragma unroll
+      for (int j = 0; j < kTwoSlots; ++j)
+        if (bj == j) {
+          hix[j] = idx + 1;
+          hsc[j] = nx.score;
+          hps[j] = nx.pscore;
+          htb[j] = nx.tb;
+        }
+    }
+    if (idx + 1 >= iend) --nruns;
+    c_pop += TWO_CLK() - tp0;
     ++visited;
     const bool is_int = e.node >= 0;
     const float b = x.b;
@@ -1527,12 +1624,12 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
       const int u = e.node;
       const int cb = x.cb, ce = x.ce;   // from the entry: no load round trip before the children's
       calls += x.nch;
-      // room for every push of this pop (internal children + at most 2R list rows)
-      if (hn + (ce - cb) + 2 * R > hcap) {
+      // room for every run of this pop (internal children + at most 2R list rows)
+      if (an + (ce - cb) + 2 * R > kTwoArena || nruns + (ce - cb + 63) / 64 + 2 > 64 * kTwoSlots) {
         status = 1;
         break;
       }
-      for (int c0 = cb; c0 < ce; c0 += 64) {   // the children: one load round trip per 64
+      for (int c0 = cb; c0 < ce; c0 += 64) {   // the children: one load round trip per 64, one run
         const int c = c0 + lane;
         const bool ok = c < ce;
         const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
@@ -1541,28 +1638,56 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
         const int ccb = ok ? a.int_child_begin[c] : 0, cce = ok ? a.int_child_end[c] : 0;
         const int cnc = ok ? a.int_nchild[c] : 0;
         const int m = min(64, ce - c0);
-        for (int j = 0; j < m; ++j) {
-          const float lj = __shfl(lpf, j, 64);
-          const float bj = fminf(b, lj);   // BF[child] = min(BF[u], LPF[child])
-          const float t2 = bj != G ? -CWQ_INF : (b > G ? CWQ_INF : fminf(lj, x.b2));
-          xheap_push(h, hx, hn, HeapEnt{lj, e.score, __shfl(tb, j, 64), c0 + j},
-                     TwoRec{bj, t2, b, __shfl(hs, j, 64), __shfl(ccb, j, 64), __shfl(cce, j, 64), __shfl(cnc, j, 64)},
-                     lane);
+#if CWQ_STAMP
+        const unsigned long long tl0 = TWO_CLK();
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tl1 = TWO_CLK();
+        c_load += tl1 - tl0;
+        ++n_int;
+        n_ch += m;
+#endif
+        // rank inside the run (m broadcasts), then every lane writes its own entry
+        int rk = 0;
+        for (int j = 0; j < m; ++j) rk += rank_before(rl_f(lpf, j), rl_i(tb, j), lpf, tb);
+        if (ok) {
+          const float bj2 = fminf(b, lpf);   // BF[child] = min(BF[u], LPF[child])
+          const float t2 = bj2 != G ? -CWQ_INF : (b > G ? CWQ_INF : fminf(lpf, x.b2));
+          ae[an + rk] = HeapEnt{lpf, e.score, tb, c};
+          ax[an + rk] = TwoRec{bj2, t2, b, hs, ccb, cce, cnc};
         }
+        const uint64_t hm = __ballot(ok && rk == 0);
+        const int hl = __builtin_ctzll(hm);
+        add_run(an, an + m, rl_f(lpf, hl), e.score, rl_i(tb, hl));
+        an += m;
+#if CWQ_STAMP
+        c_push += TWO_CLK() - tl1;
+#endif
       }
-      for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint)
-        uint64_t bm = __ballot(l == 0 ? p1 == u : p2 == u);
-        while (bm) {
-          const int j = __builtin_ctzll(bm);
-          bm &= bm - 1;
-          const int r = l == 0 ? rl_i(w1, j) : rl_i(w2, j);
-          const float sc = l == 0 ? rl_f(x1, j) : rl_f(x2, j);
-          const int tbr = l == 0 ? rl_i(tb1, j) : rl_i(tb2, j);
-          const int hsr = l == 0 ? rl_i(hs1, j) : rl_i(hs2, j);
-          xheap_push(h, hx, hn, HeapEnt{sc, e.score, tbr, -(r + 1)}, TwoRec{fminf(b, sc), fminf(x.b2, sc), b, hsr, 0, 0, 0},
-                     lane);
+      const unsigned long long tr0 = TWO_CLK();
+      for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint): a run each
+        const bool in = l == 0 ? p1 == u : p2 == u;
+        uint64_t bm = __ballot(in);
+        if (!bm) continue;
+        const float sc = l == 0 ? x1 : x2;
+        const int tbr = l == 0 ? tb1 : tb2;
+        int rk = 0;
+        for (uint64_t mm = bm; mm;) {
+          const int j = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          rk += rank_before(rl_f(sc, j), rl_i(tbr, j), sc, tbr);
         }
+        if (in) {
+          const int r = l == 0 ? w1 : w2;
+          ae[an + rk] = HeapEnt{sc, e.score, tbr, -(r + 1)};
+          ax[an + rk] = TwoRec{fminf(b, sc), fminf(x.b2, sc), b, l == 0 ? hs1 : hs2, 0, 0, 0};
+        }
+        const int nr = __popcll(bm);
+        const int hl = __builtin_ctzll(__ballot(in && rk == 0));
+        add_run(an, an + nr, rl_f(sc, hl), e.score, rl_i(tbr, hl));
+        an += nr;
+        n_rows += nr;
       }
+      c_rows += TWO_CLK() - tr0;
     }
   }
   if (lane == 0) {
@@ -1570,6 +1695,15 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
     if (a.n_calls) a.n_calls[q] = calls;
     a.status[q] = status;
   }
+#if CWQ_STAMP
+  if (lane == 0 && q == 0) {
+    const unsigned long long v[9] = {c_pop, c_load, c_push, c_rows, (unsigned long long)visited, n_int, n_ch, n_rows,
+                                     TWO_CLK() - t_start};
+    for (int i = 0; i < 9; ++i) g_two_stamp[i] = v[i];
+  }
+#else
+  (void)c_pop, (void)c_load, (void)c_push, (void)c_rows, (void)n_int, (void)n_ch, (void)n_rows, (void)t_start;
+#endif
 }
 
 // nodes[q][i] = -1 for i >= n_found[q]: the entries past a query's retrievals are defined
@@ -1604,7 +1738,7 @@ hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hip
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
   if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
   static bool attr = false;   // dynamic LDS above the 64 KiB default
-  const size_t lds = (size_t)kTwoHeapLds * (sizeof(HeapEnt) + sizeof(TwoRec));
+  const size_t lds = (size_t)kTwoArena * (sizeof(HeapEnt) + sizeof(TwoRec));
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&simulate_two_kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

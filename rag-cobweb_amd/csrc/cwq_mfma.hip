@@ -2041,6 +2041,26 @@ __device__ bool fw_chain_prefixes(FwChainLds& L, const f32x16* __restrict__ xg, 
   return true;
 }
 
+#ifndef CWQ_STAMP
+#define CWQ_STAMP 0   // diagnostic builds only (scripts/build_variant.py): wall-clock phase stamps
+#endif
+#if CWQ_STAMP
+// final_wide_kernel's phases, per workgroup (the last launch's), 100 MHz wall clock
+__device__ unsigned long long g_fw_stamp[256 * 16];
+#define FW_ST(ph)                                                                       \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_fw_stamp[blockIdx.x * 16 + (ph)] = wall_clock64(); \
+  } while (0)
+extern "C" int cwq_debug_fw_stamp(unsigned long long* out, int n) {   // copies out, then clears
+  static unsigned long long zero[256 * 16] = {};
+  const hipError_t e =
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fw_stamp), sizeof(unsigned long long) * (size_t)std::min(n, 4096));
+  return e != hipSuccess ? (int)e : (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fw_stamp), zero, sizeof(zero));
+}
+#else
+#define FW_ST(ph) ((void)0)
+#endif
+
 __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     const float* __restrict__ X, const float* __restrict__ Mf, int DP, int nq, int K, int capq,
     const int* __restrict__ qcnt, const int* __restrict__ qover, const int* __restrict__ crow,
@@ -2067,6 +2087,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   const int q = blockIdx.x / S, sidx = blockIdx.x - q * S;
   const size_t base = (size_t)q * capq;
   // ---- one round trip: counters + the first window of the candidate lists ----
+  FW_ST(0);
   const int n = qcnt[q];
   const float Tq = T[(size_t)q * ldT];
   const int ov = qover[q];
@@ -2108,6 +2129,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   float lk = -CWQ_INF, la = 0.f;
   int lr = 0x7fffffff, nx = 0;
   __syncthreads();
+  FW_ST(1);
   if (ok) {
     // T2 = K-th largest l: every wave keeps the top-K of its slice, wave 0 merges the lists
     {
@@ -2130,19 +2152,45 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       if (tid == 0) s_T2 = -CWQ_INF;   // defined even if no entry qualifies below
       __syncthreads();
       // T2 = the K-th largest of the 8 lists' K entries: entry v is it when fewer than K
-      // entries exceed it and at least K reach it (all such entries are equal)
+      // entries exceed it and at least K reach it (all such entries are equal).  Each list is
+      // sorted (descending, -inf past K), so its counts are two binary searches -- the 8
+      // lists' searches stepped together: 7 rounds of 16 independent LDS reads, not 512
+      // dependent ones
       if (lane < K) {
+        constexpr int NW = kFwThreads / 64;
         const float v = s_ml[tid];
-        int cg = 0, cge = 0;
-        for (int w = 0; w < kFwThreads / 64; ++w)
-          for (int i = 0; i < K; ++i) {
-            const float u = s_ml[w * 64 + i];
-            cg += u > v;
-            cge += u >= v;
+        int glo[NW], ghi[NW], elo[NW], ehi[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          glo[w] = elo[w] = 0;
+          ghi[w] = ehi[w] = 64;
+        }
+#pragma unroll
+        for (int st = 0; st < 7; ++st) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const int mg = (glo[w] + ghi[w]) >> 1, me = (elo[w] + ehi[w]) >> 1;
+            const float ug = s_ml[w * 64 + min(mg, 63)], ue = s_ml[w * 64 + min(me, 63)];
+            if (glo[w] < ghi[w]) {
+              if (ug > v) glo[w] = mg + 1;
+              else ghi[w] = mg;
+            }
+            if (elo[w] < ehi[w]) {
+              if (ue >= v) elo[w] = me + 1;
+              else ehi[w] = me;
+            }
           }
+        }
+        int cg = 0, cge = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          cg += glo[w];
+          cge += elo[w];
+        }
         if (cg < K && cge >= K) s_T2 = v;
       }
       __syncthreads();
+      FW_ST(2);
     }
     const float T2 = s_T2;
     // survivors u >= T2, compacted by all waves (their order does not matter: the top-K
@@ -2159,6 +2207,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       if (c) s_surv[o + __popcll(bm & ((1ull << lane) - 1))] = j;
     }
     __syncthreads();
+    FW_ST(3);
     const int ns = s_ns;
     const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X) + (size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ);
     // survivors per round: `rows` (a multiple of 64: thread t < cnt forms survivor t's key in
@@ -2283,6 +2332,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       }
     }
     // the key waves' lists -> wave 0's (same insertion; a no-op with one key wave)
+    FW_ST(4);
     const int nkw = ns > 0 ? (min(RR, ns) + 63) / 64 : 0;
     if (nkw > 1) {
       __syncthreads();
@@ -2306,6 +2356,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   for (int off = 32; off > 0; off >>= 1) nx += __shfl_xor(nx, off, 64);
   if (lane == 0 && nx) atomicAdd(&s_nx, nx);
   __syncthreads();
+  FW_ST(5);
   if (wave != 0) return;
   nx = s_nx;
   if (S > 1) {
@@ -2322,6 +2373,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     last = __shfl(last, 0, 64);
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    FW_ST(6);
     if (ok) {
       // the other workgroups' sorted lists merged in pairs (list64_merge_aux), all loads
       // issued before the merges
@@ -2348,6 +2400,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       }
     }
     nx = __hip_atomic_load(&n_exact[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    FW_ST(7);
   }
   if (fx.ids) {
     // merge_expand_kernel's expansion of the (already sorted) top-K rows, in place
@@ -2387,6 +2440,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     }
     return;
   }
+  FW_ST(8);
   if (lane < K) {
     const size_t o = (size_t)q * lstride + lane;
     pkey[o] = ok ? lk : -CWQ_INF;

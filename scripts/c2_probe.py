@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--load-struct", default=None,
                     help="skip ifit: the tree structure from a --save-struct file, node statistics by batch "
                          "Welford over the same corpus (synth.tree_synth) -- the same shape for the query legs")
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic builds (CWQ_LIB=a -DCWQ_STAMP=1 variant): after the Basic per-call leg, "
+                         "final_wide phase stamps and simulate_two cycle counts of a few one-query calls")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
     X, Qn, pick = corpus(args.n, args.dim, args.clusters, args.nq)
@@ -271,6 +274,33 @@ def basic_legs(args, w, ix, Q, Qn, k):
         ts.append(time.perf_counter() - t0)
     ts.sort()
     print(f"Basic per call cobweb_predict(numpy, {k}): median {ts[len(ts) // 2] * 1e6:.1f} us", flush=True)
+    if args.stamps:
+        print_stamps(w, Qn, k)
+
+
+def print_stamps(w, Qn, k):
+    import ctypes
+    L = ctypes.CDLL(os.environ["CWQ_LIB"])
+    fw = (ctypes.c_ulonglong * 4096)()
+    two = (ctypes.c_ulonglong * 16)()
+    names = ["pop", "load", "push", "rows", "pops", "int_pops", "child_push", "row_push", "total"]
+    for i in range(5):
+        L.cwq_debug_fw_stamp(fw, 4096)   # clears
+        w.cobweb_predict(Qn[i], k)
+        torch.cuda.synchronize()
+        L.cwq_debug_fw_stamp(fw, 4096)
+        L.cwq_debug_two_stamp(two, 16)
+        blocks = [[fw[b * 16 + p] for p in range(9)] for b in range(256) if fw[b * 16]]
+        t0 = min(r[0] for r in blocks)
+        rel = lambda v: (v - t0) * 0.01 if v >= t0 else float("nan")
+        lines = []
+        for b, r in enumerate(blocks):
+            lines.append(" ".join(f"{rel(v):7.2f}" for v in r))
+        print(f"-- call {i}: final_wide (last launch) {len(blocks)} workgroups, phase stamps us "
+              f"(0 entry,1 cands,2 T2,3 surv,4 rounds,5 kw-merge,6 last-arrival,7 split-merge,8 end)", flush=True)
+        for ln in lines[:4] + (["..."] if len(lines) > 8 else []) + lines[-4:] if len(lines) > 8 else lines:
+            print("   ", ln)
+        print("   simulate_two q0 (cycles):", {n: int(two[j]) for j, n in enumerate(names)}, flush=True)
 
 
 if __name__ == "__main__":
