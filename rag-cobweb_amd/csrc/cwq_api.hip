@@ -144,6 +144,10 @@ struct cwq_index {
   // tree's rows), auto mode takes the exact scan from then on (same results, less work)
   int64_t filt_q = 0, filt_fb = 0;
   bool filt_auto_off = false;
+  // categorize: the last call's queries all went to the two-level replay, so the next call
+  // launches the second list with the first replay (gated on its status) instead of after
+  // reading that status back (categorize_impl)
+  bool cat_two_spec = false;
   int prn_gmax = 1;   // the most internal nodes of one pruning group
   int prn_maxdep = 0;   // deepest internal node of any group
   int *gi_dep = nullptr, *gi_ppos = nullptr;   // per group-list entry: depth, the parent's list position
@@ -2859,7 +2863,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     const int slabs = n_slabs(nqb);
     const int64_t nqf = round_up(nqc, kFgTile);
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
-                                                              (size_t)cap_list * 16 + 8) + 16 * 256 +
+                                                              (size_t)cap_list * 16 + 12) + 17 * 256 +
                   (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
     if (scat)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
       need += 2 * stream_cat_bytes(ix, nqc) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
@@ -2950,8 +2954,9 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(launch_cat_count(sa, s));
       sa.pre_status = 1;
     }
-    std::vector<int> cst(by_count ? nqc : 0);
-    if (by_count) HIPCHK(hipMemcpyAsync(cst.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
+    // the count pass's status, kept on the device for the one read-back below
+    int* cst_d = by_count ? b.take<int>((size_t)nq_pad) : nullptr;
+    if (by_count) HIPCHK(hipMemcpyAsync(cst_d, status, nqc * sizeof(int), hipMemcpyDeviceToDevice, s));
     if (okf_d) {
       // queries whose filter lists overflowed have no list (every entry -inf, which the
       // replay would read as "every leaf listed" and search the whole tree for: 117 ms of a
@@ -2960,11 +2965,70 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       sa.pre_status = 1;
     }
     HIPCHK(launch_simulate(sa, s));
-    std::vector<int> st(nqc);
-    HIPCHK(hipMemcpyAsync(st.data(), status, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
-    // the filter's certified flags come back with the status (one sync)
-    if (okf_d) HIPCHK(hipMemcpyAsync(okh.data(), okf_d, nqc * sizeof(int), hipMemcpyDeviceToHost, s));
+    // Two-level replay (simulate_two_kernel, §4.7) of the queries whose top-R list ended
+    // inside a tie: a second exact leaf scan keyed by the second-level bottleneck, then
+    // the replay on both lists; what it cannot certify goes to the DENSE re-run below.
+    const char* tle = getenv("CWQ_CAT_TWO");
+    const bool two = ix->NI > 0 && !ix->any_int_sent && !complete && R == 64 && !(tle && *tle && atoi(tle) == 0);
+    // the replay on the chunk itself -- its BF / LPF, the group term tables and list 1 (okey)
+    // stay on the device; list 2 by the stream filter keyed by T2 (plus the anisotropic
+    // rows' exact scan); results straight into the outputs.  gate: the first replay's
+    // status (queries it resolved are skipped)
+    int* status2 = nullptr;
+    int* okf2 = nullptr;
+    auto two_chunk = [&](const int* gate) -> int {
+      const size_t ldI = (size_t)std::max(ix->NI, 1);
+      float* T2 = b.take<float>((size_t)nq_pad * ldI);
+      float* pk2 = b.take<float>((size_t)nq_pad * slabs * R);
+      float* pa2 = b.take<float>((size_t)nq_pad * slabs * R);
+      int* pr2 = b.take<int>((size_t)nq_pad * slabs * R);
+      float* l2k = b.take<float>((size_t)nq_pad * R);
+      float* l2a = b.take<float>((size_t)nq_pad * R);
+      int* l2r = b.take<int>((size_t)nq_pad * R);
+      HeapEnt* heap2 = b.take<HeapEnt>((size_t)nq_pad * cap2);
+      status2 = b.take<int>((size_t)nq_pad);
+      okf2 = b.take<int>((size_t)nq_pad);
+      HIPCHK(launch_cat_t2(c.BF, c.LPF, (int64_t)ldI, ix->NI, nqc, ix->par_int, okey, R, T2, s));
+      Chunk c2t = c;
+      c2t.BF = T2;   // the categorize key reads min(T2[parent], lp)
+      int nst2 = 0;
+      int rc2;
+      if ((rc2 = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
+        return rc2;
+      if ((rc2 = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2, b,
+                                 s)))
+        return rc2;
+      HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
+      SimArgs st2 = sa;
+      st2.pre_status = 0;
+      st2.lkey2 = l2k;
+      st2.laux2 = l2a;
+      st2.lrow2 = l2r;
+      st2.T2 = T2;
+      st2.heap = heap2;
+      st2.heap_cap = cap2;
+      st2.status = status2;
+      st2.gate = gate;
+      HIPCHK(launch_simulate_two(st2, s));
+      return 0;
+    };
+    // speculative: the second list goes out with the first replay, one status read-back for
+    // both (the last call needed it for every query; CWQ_CAT_SPEC=0 turns it off, =2 forces
+    // it -- tests)
+    const char* spe = getenv("CWQ_CAT_SPEC");
+    const int spv = spe && *spe ? atoi(spe) : 1;
+    const bool spec = two && scat && spv != 0 && (ix->cat_two_spec || spv == 2);
+    if (spec && (rc = two_chunk(status))) return rc;
+    // the count status, the replay status, the filter's certified flags (and the second
+    // list's) written by one kernel into host-mapped memory: one sync, no pageable copies
+    if ((rc = ix->host_flags((size_t)5 * nqc))) return rc;
+    HIPCHK(launch_gather_flags(ix->hflags, nqc, cst_d, status, okf_d, spec ? status2 : nullptr, spec ? okf2 : nullptr, s));
     HIPCHK(hipStreamSynchronize(s));
+    const int* hf = ix->hflags;
+    std::vector<int> cst(hf, hf + (by_count ? nqc : 0)), st(hf + nqc, hf + 2 * (size_t)nqc);
+    std::vector<int> hs(spec ? hf + 3 * (size_t)nqc : hf, spec ? hf + 4 * (size_t)nqc : hf);
+    std::vector<int> ho(spec ? hf + 4 * (size_t)nqc : hf, spec ? hf + 5 * (size_t)nqc : hf);
+    if (okf_d) okh.assign(hf + 2 * (size_t)nqc, hf + 3 * (size_t)nqc);
     for (int i = 0; i < (int)okh.size(); ++i)
       if (!okh[i]) {
         fbad[i] = 1;
@@ -2977,54 +3041,19 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       if (by_count && cst[i] == 0 && !fbad[i]) ++ix->stats[3];
       else if (!fbad[i]) ++ix->stats[4];
     }
+    if (scat && two) ix->cat_two_spec = (int)redo.size() == nqc;
     if (redo.empty()) continue;
 
-    // Two-level replay (simulate_two_kernel, §4.7) of the queries whose top-R list ended
-    // inside a tie: a second exact leaf scan keyed by the second-level bottleneck, then
-    // the replay on both lists; what it cannot certify goes to the DENSE re-run below.
-    const char* tle = getenv("CWQ_CAT_TWO");
-    const bool two = ix->NI > 0 && !ix->any_int_sent && !complete && R == 64 && !(tle && *tle && atoi(tle) == 0);
-    if (two && scat && (int)redo.size() == nqc) {
-      // every query of the call: the replay on the chunk itself -- its BF / LPF, the group
-      // term tables and list 1 (okey) stay on the device; list 2 by the stream filter keyed
-      // by T2 (plus the anisotropic rows' exact scan); results straight into the outputs
-      const size_t ldI = (size_t)std::max(ix->NI, 1);
-      float* T2 = b.take<float>((size_t)nq_pad * ldI);
-      float* pk2 = b.take<float>((size_t)nq_pad * slabs * R);
-      float* pa2 = b.take<float>((size_t)nq_pad * slabs * R);
-      int* pr2 = b.take<int>((size_t)nq_pad * slabs * R);
-      float* l2k = b.take<float>((size_t)nq_pad * R);
-      float* l2a = b.take<float>((size_t)nq_pad * R);
-      int* l2r = b.take<int>((size_t)nq_pad * R);
-      HeapEnt* heap2 = b.take<HeapEnt>((size_t)nq_pad * cap2);
-      int* status2 = b.take<int>((size_t)nq_pad);
-      int* okf2 = b.take<int>((size_t)nq_pad);
-      HIPCHK(launch_cat_t2(c.BF, c.LPF, (int64_t)ldI, ix->NI, nqc, ix->par_int, okey, R, T2, s));
-      Chunk c2t = c;
-      c2t.BF = T2;   // the categorize key reads min(T2[parent], lp)
-      int nst2 = 0;
-      if ((rc = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
-        return rc;
-      if ((rc = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2, b,
-                                s)))
-        return rc;
-      HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
-      SimArgs st2 = sa;
-      st2.pre_status = 0;
-      st2.lkey2 = l2k;
-      st2.laux2 = l2a;
-      st2.lrow2 = l2r;
-      st2.T2 = T2;
-      st2.heap = heap2;
-      st2.heap_cap = cap2;
-      st2.status = status2;
-      HIPCHK(launch_simulate_two(st2, s));
-      std::vector<int> hs(nqc), ho(nqc);
-      HIPCHK(hipMemcpyAsync(hs.data(), status2, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(ho.data(), okf2, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+    if (spec || (two && scat && (int)redo.size() == nqc)) {
+      if (!spec) {   // every query of the call, after the status read-back
+        if ((rc = two_chunk(nullptr))) return rc;
+        HIPCHK(launch_gather_flags(ix->hflags, nqc, status2, okf2, nullptr, nullptr, nullptr, s));
+        HIPCHK(hipStreamSynchronize(s));
+        hs.assign(ix->hflags, ix->hflags + nqc);
+        ho.assign(ix->hflags + nqc, ix->hflags + 2 * (size_t)nqc);
+      }
       std::vector<int> left;
-      for (int i = 0; i < nqc; ++i) {
+      for (const int i : redo) {
         if (hs[i] || !ho[i]) left.push_back(i);   // uncertified, or list 2 overflowed: DENSE
         else ++ix->stats[5];
       }

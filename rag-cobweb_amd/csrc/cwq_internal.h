@@ -99,6 +99,9 @@ struct SimArgs {
   // (cat_t2_kernel) and the list by the second-level key [nq][R]
   const float* T2;
   const float* lkey2; const float* laux2; const int* lrow2;
+  // simulate_two_kernel: skip the queries whose gate[q] is 0 (the first replay resolved them;
+  // launched before the host has read that status), writing nothing for them; null: none
+  const int* gate;
 };
 
 // Node variances read by the index build.  Full: [n_nodes][D] rows (compute_var of every
@@ -241,6 +244,10 @@ hipError_t launch_cat_t2(const float* BF, const float* LPF, int64_t ldI, int NI,
                          const float* lkey, int R, float* T2, hipStream_t s);
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
 hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hipStream_t s);
+// dst[j * nq + q] = src[j] ? src[j][q] : 0 for j < 5: a call's per-query flag arrays into one
+// host-mapped buffer, read back with a single stream sync (no pageable copies)
+hipError_t launch_gather_flags(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
+                               const int* s4, hipStream_t s);
 hipError_t launch_clear_tail(int64_t* nodes, const int* n_found, int64_t nq, int k, hipStream_t s);
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
                         float* okey, float* oaux, int* orow, hipStream_t s, bool cat);

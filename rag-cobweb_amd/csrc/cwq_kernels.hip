@@ -1477,7 +1477,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   extern __shared__ HeapEnt s_heap[];
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x;
-  if (q >= a.nq) return;
+  if (q >= a.nq || (a.gate && a.gate[q] == 0)) return;
   HeapEnt* ae = s_heap;                                            // the arena: runs of entries
   TwoRec* ax = reinterpret_cast<TwoRec*>(s_heap + kTwoArena);      // their side records
   int an = 0;                                                      // arena entries used
@@ -1536,7 +1536,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   const int hs2 = v2 ? ((a.row_flags[w2] & FLAG_HAS_SENT) != 0) : 0;
   int status = 0, found = 0, gpops = 0;
   int64_t calls = 1, visited = 0;
-  unsigned long long c_pop = 0, c_load = 0, c_push = 0, c_rows = 0, n_int = 0, n_ch = 0, n_rows = 0;
+  unsigned long long c_pop = 0, c_load = 0, c_push = 0, c_rows = 0, n_int = 0, n_ch = 0, n_rows = 0, c_sel = 0;
   const unsigned long long t_start = TWO_CLK();
   // list 1 must be full, end inside the tie at G, and hold every group root among the rows
   if (!(G > -CWQ_INF) || wG == 0x7fffffff || !(xG > G) || a.NI <= 0) status = 1;
@@ -1580,6 +1580,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
       }
     idx = __builtin_amdgcn_readlane(idx, wl);
     iend = __builtin_amdgcn_readlane(iend, wl);
+    c_sel += TWO_CLK() - tp0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the arena writes of earlier runs
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1697,12 +1698,13 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   }
 #if CWQ_STAMP
   if (lane == 0 && q == 0) {
-    const unsigned long long v[9] = {c_pop, c_load, c_push, c_rows, (unsigned long long)visited, n_int, n_ch, n_rows,
-                                     TWO_CLK() - t_start};
-    for (int i = 0; i < 9; ++i) g_two_stamp[i] = v[i];
+    const unsigned long long v[10] = {c_pop, c_load, c_push, c_rows, (unsigned long long)visited, n_int, n_ch, n_rows,
+                                      TWO_CLK() - t_start, c_sel};
+    for (int i = 0; i < 10; ++i) g_two_stamp[i] = v[i];
   }
 #else
-  (void)c_pop, (void)c_load, (void)c_push, (void)c_rows, (void)n_int, (void)n_ch, (void)n_rows, (void)t_start;
+  (void)c_pop, (void)c_load, (void)c_push, (void)c_rows, (void)n_int, (void)n_ch, (void)n_rows, (void)t_start,
+      (void)c_sel;
 #endif
 }
 
@@ -1727,6 +1729,23 @@ __global__ void skip_failed_kernel(int* status, const int* okf, int nq, int init
   if (q >= nq) return;
   if (init) status[q] = okf[q] ? 1 : 0;
   else if (!okf[q]) status[q] = 0;
+}
+
+__global__ void gather_flags_kernel(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
+                                    const int* s4) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const int* src[5] = {s0, s1, s2, s3, s4};
+#pragma unroll
+  for (int j = 0; j < 5; ++j) dst[(size_t)j * nq + q] = src[j] ? src[j][q] : 0;
+}
+
+hipError_t launch_gather_flags(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
+                               const int* s4, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_flags_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, dst, nq, s0, s1, s2, s3,
+                     s4);
+  return hipGetLastError();
 }
 
 hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hipStream_t s) {

@@ -2136,6 +2136,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
       const bool pre = d && wave == 0;   // wave 0 continues the list of the first d candidates
       float tk = pre ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
       int tr = pre ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
+      FW_ST(9);
       for (int j0 = d + wave * 64; j0 < n; j0 += kFwThreads) {
         const int j = j0 + lane;
         const float lv = j >= n ? -CWQ_INF : j < kFwCand ? s_wl[j] : cl[base + j];
@@ -2148,9 +2149,11 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           list64_offer(tk, tr, lane, lv, j, K);
         }
       }
+      FW_ST(10);
       s_ml[tid] = lane < K ? tk : -CWQ_INF;
       if (tid == 0) s_T2 = -CWQ_INF;   // defined even if no entry qualifies below
       __syncthreads();
+      FW_ST(11);
       // T2 = the K-th largest of the 8 lists' K entries: entry v is it when fewer than K
       // entries exceed it and at least K reach it (all such entries are equal).  Each list is
       // sorted (descending, -inf past K), so its counts are two binary searches -- the 8
@@ -2261,11 +2264,13 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           s_part[sv * LDP + v] = part;
         }
       }
+      if (r0 == 0) FW_ST(12);
       float pp = 0.f;
       // exact parent chains (bounded internal prefixes): the whole workgroup, every distinct
       // ancestor once (fw_chain_prefixes); the per-lane chain if its table overflows
       const bool chained = use_chain && fw_chain_prefixes(s_chain, xg, chain, DP, tid < cnt && p > 0, p,
                                                           P[(size_t)q * ldP]);
+      if (r0 == 0) FW_ST(13);
       if (tid < cnt) {
         pp = p < 0 ? (cat ? CWQ_INF : 0.f)
                    : (use_chain && p > 0 ? (chained ? s_chain.pp[lane] : exact_prefix(X, chain, DP, q, p, P[(size_t)q * ldP]))

@@ -143,13 +143,16 @@ def test_two_level_replay_on_clustered_ifit_tree(gpu, filt):
     assert two >= 0.5 * Q.shape[0], two
 
 
-@pytest.mark.parametrize("nq", [1, 8, 64])
-def test_small_calls_stream_lists_equal_dense(gpu, nq):
+@pytest.mark.parametrize("nq,spec", [(1, "1"), (8, "1"), (64, "1"), (1, "2"), (8, "2")])
+def test_small_calls_stream_lists_equal_dense(gpu, nq, spec):
     """Calls of <= 64 queries take the per-call stream filter for both lists (the categorize
     key min(BF or T2 [parent], lp) in cwq_stream.hip) and replay the two-level lists on the
     chunk itself.  On the clustered device-ifit tree (every query ends in a bottleneck tie)
     and a two-level tree, pop order, n_found and calls equal the DENSE re-run and the batch
-    call's rows, k = 10 and k = 64, max_nodes cutting inside the search too."""
+    call's rows, k = 10 and k = 64, max_nodes cutting inside the search too.  spec "1": the
+    second list goes out speculatively after a call that needed it for every query; "2":
+    always (CWQ_CAT_SPEC=2), so queries the first replay resolves are gated off the
+    two-level replay (the two-level tree resolves most of them that way)."""
     import random
     rng = np.random.default_rng(7)
     n, d, nc = 20_000, 64, 40
@@ -170,7 +173,7 @@ def test_small_calls_stream_lists_equal_dense(gpu, nq):
         for k, mx in [(10, 100000), (64, 100000), (10, 40)]:
             ref, _ = _run(ix, Q, k, mx, CWQ_CAT_COUNT="0", CWQ_CAT_TWO="0")
             for a in range(0, 128, nq):
-                got, st = _run(ix, Q[a:a + nq].contiguous(), k, mx)
+                got, st = _run(ix, Q[a:a + nq].contiguous(), k, mx, CWQ_CAT_SPEC=spec)
                 for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
                     assert torch.equal(x[a:a + nq], y), (name, k, mx, a, st)
     ix2.close()
