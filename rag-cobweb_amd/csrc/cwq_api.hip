@@ -2760,7 +2760,9 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   int* tr = b.take<int>((size_t)nqc * 64);
   // the rerank split over workgroups (categorize lists: ~1k candidates, most reranked --
   // their keys tie at the parents' bottlenecks); arrivals counted in the zeroed ok slot
-  const int fws = fw_split(ix, nqc, true);
+  // (at most 8: the last workgroup's merge inserts the others' tie-heavy lists serially --
+  // C2 list 2: 8 workgroups end at 33 us, 32 at 61 us, profiles/r05_basic_percall_stamps_radix_s{8,32}.log)
+  const int fws = std::min(8, fw_split(ix, nqc, true));
   FwExpand fx{nullptr, nullptr, nullptr, nullptr, 0, nullptr, fws, b.take<float>((size_t)nqc * fws * 64),
               b.take<float>((size_t)nqc * fws * 64), b.take<int>((size_t)nqc * fws * 64), qcnt + nqc};
   // the counters (qcnt, qover, done, the fused select's) zeroed by the prep's block 0

@@ -482,6 +482,16 @@ __device__ __forceinline__ bool entry_before(float k, float a, int r, float k2, 
   return k > k2 || (k == k2 && (cat && a != a2 ? a < a2 : r < r2));
 }
 
+// float -> u32 whose unsigned order is the float order (NaN as -inf, -0 as +0: equal floats
+// equal keys); 0 is below them all.  unord_f32 inverts it.
+__device__ __forceinline__ unsigned ord_f32(float f) {
+  const unsigned u = __float_as_uint(f == f ? (f == 0.f ? 0.f : f) : -__builtin_inff());
+  return u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+
 // list64_insert with an aux value carried along (final_wide_kernel's (key, lp, row) lists)
 __device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr, int lane, float ck, float ca, int cr,
                                                   int K, bool cat = false) {
@@ -508,7 +518,8 @@ __device__ __forceinline__ void list64_insert_aux(float& lk, float& la, int& lr,
 // list reversed against this one keeps the better of each pair -- a bitonic sequence that
 // holds the union's best 64 -- and six half-cleaner stages sort it.  Rows are distinct
 // across the two lists, so the result's first K lanes are exactly what K serial
-// list64_insert_aux calls would leave, in ~7 shuffle rounds instead of up to 64 inserts.
+// list64_insert_aux calls would leave, in ~7 shuffle rounds instead of up to 64 inserts
+// (categorize lists, whose ties make most entries enter; short Fast lists insert).
 __device__ __forceinline__ void list64_merge_aux(float& lk, float& la, int& lr, int lane, float ok, float oa, int orow,
                                                  bool cat) {
   {

@@ -1403,20 +1403,15 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // arena or slot overflow ends the replay uncertified (the query goes DENSE).
 // (The 64-ary LDS heap this replaces spent ~4.8k cycles per pop in its three-pass wave
 // argmin and ~760 per serial push: profiles/r05_basic_percall_stamps_s32.log.)
-constexpr int kTwoArena = 3072;   // pushed entries per query (44 B each in LDS)
+constexpr int kTwoArena = 3072;   // pushed entries per query (48 B each in LDS)
 constexpr int kTwoSlots = 4;      // run heads per lane: 256 live runs
-struct TwoRec {
+struct alignas(16) TwoRec {
   float b, b2, pb;
   int hs;
   int cb, ce, nch;   // an internal node's child range and child count (read when it is pushed)
+  int pad_;
 };
 
-// float -> u32 whose unsigned order is the float order (NaN as -inf, -0 as +0: equal floats
-// equal keys); 0 is below them all
-__device__ __forceinline__ unsigned ord_f32(float f) {
-  const unsigned u = __float_as_uint(f == f ? (f == 0.f ? 0.f : f) : -CWQ_INF);
-  return u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
-}
 
 // max over the wave by DPP (quad swaps, half-row and row mirrors, row broadcasts): lane 63
 // ends with the maximum, read back to every lane
@@ -1430,16 +1425,23 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
   return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// the lane holding the frontier's first entry (wheap_before order) among lanes with ok;
-// -1 if none
-__device__ __forceinline__ int wave_first(bool ok, float sc, float ps, int tb) {
-  const unsigned k1 = ok ? ord_f32(sc) : 0u;
-  const unsigned m1 = wave_max_u32(k1);
-  uint64_t c = __ballot(ok && k1 == m1);
-  if (!c) return -1;
+// A run head's key in the heap order (wheap_before) as one unsigned 64-bit value: the
+// score's order above the complemented pscore's (a smaller pscore first); the BFS index
+// breaks exact ties.  0: an empty slot (below every key: an ordered score is >= 0x007fffff).
+__device__ __forceinline__ uint64_t head_key(float sc, float ps) {
+  return ((uint64_t)ord_f32(sc) << 32) | (uint64_t)(~ord_f32(ps));
+}
+
+// the lane holding the frontier's first entry: the largest key, then the smallest BFS
+// index; -1 if every key is 0.  One DPP max on the high words, the rest only on ties.
+__device__ __forceinline__ int wave_first(uint64_t k, int tb) {
+  const unsigned h = (unsigned)(k >> 32), l = (unsigned)k;
+  const unsigned m1 = wave_max_u32(h);
+  if (m1 == 0u) return -1;
+  uint64_t c = __ballot(h == m1);
   if (c & (c - 1)) {   // scores tie: the smaller pscore, then the smaller BFS index
     const bool in = (c >> (threadIdx.x & 63)) & 1;
-    const unsigned k2 = in ? ~ord_f32(ps) : 0u;
+    const unsigned k2 = in ? l : 0u;
     const unsigned m2 = wave_max_u32(k2);
     c = __ballot(in && k2 == m2);
     if (c & (c - 1)) {
@@ -1481,36 +1483,37 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   HeapEnt* ae = s_heap;                                            // the arena: runs of entries
   TwoRec* ax = reinterpret_cast<TwoRec*>(s_heap + kTwoArena);      // their side records
   int an = 0;                                                      // arena entries used
-  // run heads: the head entry's (score, pscore, BFS index), its arena index, the run's end
-  float hsc[kTwoSlots], hps[kTwoSlots];
+  // run heads: the head entry's key (head_key) and BFS index, its arena index, the run's end
+  uint64_t hk[kTwoSlots];
   int htb[kTwoSlots], hix[kTwoSlots], hend[kTwoSlots];
 #pragma unroll
   for (int j = 0; j < kTwoSlots; ++j) {
-    hsc[j] = hps[j] = 0.f;
-    htb[j] = hix[j] = hend[j] = 0;   // empty: hix == hend
+    hk[j] = 0;   // empty
+    htb[j] = hix[j] = hend[j] = 0;
   }
   int nruns = 0;
-  // a run [i0, i1) of the arena into a free slot (the first lane with one): uniform call
-  auto add_run = [&](int i0, int i1, float sc, float ps, int tb) {
-    bool fr = false;
-#pragma unroll
-    for (int j = 0; j < kTwoSlots; ++j) fr |= hix[j] == hend[j];
-    const uint64_t fm = __ballot(fr);
-    if (lane == __builtin_ctzll(fm)) {
-      bool done = false;
-#pragma unroll
-      for (int j = 0; j < kTwoSlots; ++j)
-        if (!done && hix[j] == hend[j]) {
-          hsc[j] = sc;
-          hps[j] = ps;
-          htb[j] = tb;
-          hix[j] = i0;
-          hend[j] = i1;
-          done = true;
-        }
-    }
-    ++nruns;
-  };
+  // a run [i0, i1) of the arena into a free slot (the first lane with one): uniform use
+  // (a macro, not a lambda over the slot arrays: those must stay in registers)
+#define TWO_ADD_RUN(i0, i1, sc, ps, tb)                   \
+  do {                                                    \
+    bool fr_ = false;                                     \
+    _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) fr_ |= hk[j_] == 0; \
+    const uint64_t fm_ = __ballot(fr_);                   \
+    const uint64_t nk_ = head_key((sc), (ps));            \
+    const int tb_ = (tb), i0_ = (i0), i1_ = (i1);         \
+    if (lane == __builtin_ctzll(fm_)) {                   \
+      bool done_ = false;                                 \
+      _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) { \
+        const bool put_ = !done_ && hk[j_] == 0;          \
+        hk[j_] = put_ ? nk_ : hk[j_];                     \
+        htb[j_] = put_ ? tb_ : htb[j_];                   \
+        hix[j_] = put_ ? i0_ : hix[j_];                   \
+        hend[j_] = put_ ? i1_ : hend[j_];                 \
+        done_ |= put_;                                    \
+      }                                                   \
+    }                                                     \
+    ++nruns;                                              \
+  } while (0)
   const float* BF = a.BF + (size_t)q * a.ldI;
   const int R = a.R;
   const size_t lo = (size_t)q * R;
@@ -1550,55 +1553,47 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
                      a.int_child_end[0], a.int_nchild[0]};
     }
     an = 1;
-    add_run(0, 1, s0, 0.f, a.int_bfs[0]);
+    TWO_ADD_RUN(0, 1, s0, 0.f, a.int_bfs[0]);
   }
   while (nruns > 0) {
     const unsigned long long tp0 = TWO_CLK();
-    // the frontier's first entry: each lane's best head, then the wave's
-    int bj = -1;
-    float bs = 0.f, bp = 0.f;
-    int bt = 0;
+    // the frontier's first entry: each lane's best head (branch-free over its slots), then
+    // the wave's
+    uint64_t bk = 0;
+    int btb = 0x7fffffff, bj = -1, bix = 0, bend = 0;
 #pragma unroll
-    for (int j = 0; j < kTwoSlots; ++j)
-      if (hix[j] != hend[j] && (bj < 0 || wheap_before(hsc[j], hps[j], htb[j], bs, bp, bt))) {
-        bj = j;
-        bs = hsc[j];
-        bp = hps[j];
-        bt = htb[j];
-      }
-    const int wl = wave_first(bj >= 0, bs, bp, bt);
+    for (int j = 0; j < kTwoSlots; ++j) {
+      const bool bt = hk[j] > bk || (hk[j] == bk && hk[j] != 0 && htb[j] < btb);
+      bk = bt ? hk[j] : bk;
+      btb = bt ? htb[j] : btb;
+      bj = bt ? j : bj;
+      bix = bt ? hix[j] : bix;
+      bend = bt ? hend[j] : bend;
+    }
+    const int wl = wave_first(bk, btb);
     if (wl < 0) {   // (the run count says a head exists)
       status = 1;
       break;
     }
-    int idx = 0, iend = 0;
-#pragma unroll
-    for (int j = 0; j < kTwoSlots; ++j)
-      if (bj == j) {
-        idx = hix[j];
-        iend = hend[j];
-      }
-    idx = __builtin_amdgcn_readlane(idx, wl);
-    iend = __builtin_amdgcn_readlane(iend, wl);
+    const int idx = __builtin_amdgcn_readlane(bix, wl), iend = __builtin_amdgcn_readlane(bend, wl);
     c_sel += TWO_CLK() - tp0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the arena writes of earlier runs
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const HeapEnt e = ae[idx];
     const TwoRec x = ax[idx];
-    if (lane == wl) {   // the run advances: its next entry is the new head
-      const bool more = idx + 1 < iend;
-      const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
+    // the run advances: its next entry (read by every lane: one broadcast) is the new head
+    const bool more = idx + 1 < iend;
+    const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
+    const uint64_t nk = more ? head_key(nx.score, nx.pscore) : 0;
 #pragma unroll
-      for (int j = 0; j < kTwoSlots; ++j)
-        if (bj == j) {
-          hix[j] = idx + 1;
-          hsc[j] = nx.score;
-          hps[j] = nx.pscore;
-          htb[j] = nx.tb;
-        }
+    for (int j = 0; j < kTwoSlots; ++j) {
+      const bool adv = lane == wl && bj == j;
+      hk[j] = adv ? nk : hk[j];
+      htb[j] = adv ? nx.tb : htb[j];
+      hix[j] = adv ? idx + 1 : hix[j];
     }
-    if (idx + 1 >= iend) --nruns;
+    if (!more) --nruns;
     c_pop += TWO_CLK() - tp0;
     ++visited;
     const bool is_int = e.node >= 0;
@@ -1648,24 +1643,30 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
         n_ch += m;
 #endif
         // rank inside the run (m broadcasts), then every lane writes its own entry
+        const float lc = lpf == lpf ? lpf : -CWQ_INF;   // (rank_before's order)
         int rk = 0;
-        for (int j = 0; j < m; ++j) rk += rank_before(rl_f(lpf, j), rl_i(tb, j), lpf, tb);
+        for (int j = 0; j < m; ++j) {
+          const float sj = rl_f(lc, j);
+          const int tj = rl_i(tb, j);
+          rk += sj > lc || (sj == lc && tj < tb);
+        }
         if (ok) {
           const float bj2 = fminf(b, lpf);   // BF[child] = min(BF[u], LPF[child])
           const float t2 = bj2 != G ? -CWQ_INF : (b > G ? CWQ_INF : fminf(lpf, x.b2));
           ae[an + rk] = HeapEnt{lpf, e.score, tb, c};
-          ax[an + rk] = TwoRec{bj2, t2, b, hs, ccb, cce, cnc};
+          ax[an + rk] = TwoRec{bj2, t2, b, hs, ccb, cce, cnc, 0};
         }
         const uint64_t hm = __ballot(ok && rk == 0);
         const int hl = __builtin_ctzll(hm);
-        add_run(an, an + m, rl_f(lpf, hl), e.score, rl_i(tb, hl));
+        TWO_ADD_RUN(an, an + m, rl_f(lpf, hl), e.score, rl_i(tb, hl));
         an += m;
 #if CWQ_STAMP
         c_push += TWO_CLK() - tl1;
 #endif
       }
       const unsigned long long tr0 = TWO_CLK();
-      for (int l = 0; l < 2; ++l) {   // the list rows whose parent is u (the two lists are disjoint): a run each
+      const bool anyrow = __ballot(p1 == u || p2 == u) != 0;
+      for (int l = 0; anyrow && l < 2; ++l) {   // the list rows whose parent is u (the lists are disjoint): a run each
         const bool in = l == 0 ? p1 == u : p2 == u;
         uint64_t bm = __ballot(in);
         if (!bm) continue;
@@ -1680,11 +1681,11 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
         if (in) {
           const int r = l == 0 ? w1 : w2;
           ae[an + rk] = HeapEnt{sc, e.score, tbr, -(r + 1)};
-          ax[an + rk] = TwoRec{fminf(b, sc), fminf(x.b2, sc), b, l == 0 ? hs1 : hs2, 0, 0, 0};
+          ax[an + rk] = TwoRec{fminf(b, sc), fminf(x.b2, sc), b, l == 0 ? hs1 : hs2, 0, 0, 0, 0};
         }
         const int nr = __popcll(bm);
         const int hl = __builtin_ctzll(__ballot(in && rk == 0));
-        add_run(an, an + nr, rl_f(sc, hl), e.score, rl_i(tbr, hl));
+        TWO_ADD_RUN(an, an + nr, rl_f(sc, hl), e.score, rl_i(tbr, hl));
         an += nr;
         n_rows += nr;
       }
@@ -1707,6 +1708,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
       (void)c_sel;
 #endif
 }
+#undef TWO_ADD_RUN
 
 // nodes[q][i] = -1 for i >= n_found[q]: the entries past a query's retrievals are defined
 // whichever path (count, replay, two-level, DENSE) resolved it.

@@ -2091,7 +2091,9 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   const int n = qcnt[q];
   const float Tq = T[(size_t)q * ldT];
   const int ov = qover[q];
-  const int d = done[q];
+  (void)lkb;   // the stream select's list of the first done[q] candidates: not needed (T2 below)
+  (void)lrb;
+  (void)done;
   if (tid < capq) {
     s_wl[tid] = cl[base + tid];
     s_wu[tid] = cu[base + tid];
@@ -2131,67 +2133,67 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
   __syncthreads();
   FW_ST(1);
   if (ok) {
-    // T2 = K-th largest l: every wave keeps the top-K of its slice, wave 0 merges the lists
+    // T2 = the K-th largest l over the whole list (multiplicity counted; -inf with fewer than
+    // K candidates): a radix select of the ordered keys (ord_f32), 8 bits a pass -- an LDS
+    // histogram of the keys under the prefix so far, one wave finds the digit holding the
+    // K-th from the top.  (The list of the first `done` candidates the stream select kept is
+    // not needed: every candidate's l is staged.)  Replaces per-wave top-K lists whose serial
+    // inserts and merge took ~20 us of a categorize list's rerank
+    // (profiles/r05_basic_percall_stamps_runmerge.log).
     {
-      const bool pre = d && wave == 0;   // wave 0 continues the list of the first d candidates
-      float tk = pre ? lkb[(size_t)q * 64 + lane] : -CWQ_INF;
-      int tr = pre ? lrb[(size_t)q * 64 + lane] : 0x7fffffff;
       FW_ST(9);
-      for (int j0 = d + wave * 64; j0 < n; j0 += kFwThreads) {
-        const int j = j0 + lane;
-        const float lv = j >= n ? -CWQ_INF : j < kFwCand ? s_wl[j] : cl[base + j];
-        if (j0 == d + wave * 64 && !pre) {   // empty list: sort the first 64 (-inf never enters)
-          tk = lv == lv ? lv : -CWQ_INF;      // a NaN bound never enters (as list64_offer)
-          tr = tk == -CWQ_INF ? 0x7fffffff : j;
-          float dummy = 0.f;
-          wave_sort64<false>(tk, tr, dummy, lane);
-        } else {
-          list64_offer(tk, tr, lane, lv, j, K);
-        }
-      }
-      FW_ST(10);
-      s_ml[tid] = lane < K ? tk : -CWQ_INF;
-      if (tid == 0) s_T2 = -CWQ_INF;   // defined even if no entry qualifies below
-      __syncthreads();
-      FW_ST(11);
-      // T2 = the K-th largest of the 8 lists' K entries: entry v is it when fewer than K
-      // entries exceed it and at least K reach it (all such entries are equal).  Each list is
-      // sorted (descending, -inf past K), so its counts are two binary searches -- the 8
-      // lists' searches stepped together: 7 rounds of 16 independent LDS reads, not 512
-      // dependent ones
-      if (lane < K) {
-        constexpr int NW = kFwThreads / 64;
-        const float v = s_ml[tid];
-        int glo[NW], ghi[NW], elo[NW], ehi[NW];
+      unsigned* s_hist = reinterpret_cast<unsigned*>(s_ml);   // [256] (s_ml is free until the merges)
+      unsigned* s_rsel = reinterpret_cast<unsigned*>(s_ma);   // [2]: prefix, rank left
+      unsigned pref = 0u, kk = (unsigned)K;
+      if (n >= K) {
+        for (int pass = 0; pass < 4; ++pass) {
+          const int sh = 24 - 8 * pass;
+          const unsigned hm = pass == 0 ? 0u : (~0u << (sh + 8));
+          if (tid < 256) s_hist[tid] = 0u;
+          __syncthreads();
+          for (int j = tid; j < n; j += kFwThreads) {
+            const unsigned u = ord_f32(j < kFwCand ? s_wl[j] : cl[base + j]);
+            if ((u & hm) == pref) atomicAdd(&s_hist[(u >> sh) & 255u], 1u);
+          }
+          __syncthreads();
+          if (wave == 0) {
+            // lane L holds bins 255-4L .. 252-4L (lane 0: the top); inclusive prefix over lanes
+            unsigned c[4], tot = 0u;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          glo[w] = elo[w] = 0;
-          ghi[w] = ehi[w] = 64;
-        }
-#pragma unroll
-        for (int st = 0; st < 7; ++st) {
-#pragma unroll
-          for (int w = 0; w < NW; ++w) {
-            const int mg = (glo[w] + ghi[w]) >> 1, me = (elo[w] + ehi[w]) >> 1;
-            const float ug = s_ml[w * 64 + min(mg, 63)], ue = s_ml[w * 64 + min(me, 63)];
-            if (glo[w] < ghi[w]) {
-              if (ug > v) glo[w] = mg + 1;
-              else ghi[w] = mg;
+            for (int i = 0; i < 4; ++i) {
+              c[i] = s_hist[255 - 4 * lane - i];
+              tot += c[i];
             }
-            if (elo[w] < ehi[w]) {
-              if (ue >= v) elo[w] = me + 1;
-              else ehi[w] = me;
+            unsigned inc = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+              const unsigned t = __shfl_up(inc, o, 64);
+              if (lane >= o) inc += t;
+            }
+            const unsigned exc = inc - tot;
+            if (exc < kk && kk <= inc) {   // exactly one lane: the counts under the prefix reach kk
+              unsigned above = exc;
+              int dg = 252 - 4 * lane;
+              bool got = false;   // the first bin (from the top) whose running count reaches kk
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (!got && above + c[i] >= kk) {
+                  dg = 255 - 4 * lane - i;
+                  got = true;
+                } else if (!got) {
+                  above += c[i];
+                }
+              }
+              s_rsel[0] = pref | ((unsigned)dg << sh);
+              s_rsel[1] = kk - above;
             }
           }
+          __syncthreads();
+          pref = s_rsel[0];
+          kk = s_rsel[1];
         }
-        int cg = 0, cge = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          cg += glo[w];
-          cge += elo[w];
-        }
-        if (cg < K && cge >= K) s_T2 = v;
       }
+      if (tid == 0) s_T2 = n >= K ? unord_f32(pref) : -CWQ_INF;
       __syncthreads();
       FW_ST(2);
     }
@@ -2353,8 +2355,23 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           la = CWQ_INF;
           lr = 0x7fffffff;
         }
-        for (int w = 1; w < nkw; ++w)
-          list64_merge_aux(lk, la, lr, lane, s_ml[w * 64 + lane], s_ma[w * 64 + lane], s_mr[w * 64 + lane], cat);
+        for (int w = 1; w < nkw; ++w) {
+          const float key = s_ml[w * 64 + lane], lp = s_ma[w * 64 + lane];
+          const int rid = s_mr[w * 64 + lane];
+          if (cat) {   // (as the split merge below)
+            list64_merge_aux(lk, la, lr, lane, key, lp, rid, true);
+            continue;
+          }
+          const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
+          const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+          uint64_t mask = __ballot(rid != 0x7fffffff && entry_before(key, lp, rid, tk, ta, tr, cat));
+          while (mask) {
+            const int bb = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            list64_insert_aux(lk, la, lr, lane, rl_f2(key, bb), rl_f2(lp, bb), __builtin_amdgcn_readlane(rid, bb), K,
+                              cat);
+          }
+        }
       }
     }
   }
@@ -2380,8 +2397,7 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     FW_ST(6);
     if (ok) {
-      // the other workgroups' sorted lists merged in pairs (list64_merge_aux), all loads
-      // issued before the merges
+      // the other workgroups' lists, 8 in flight per round trip, inserted into this one
       if (lane >= K) {
         lk = -CWQ_INF;
         la = CWQ_INF;
@@ -2400,8 +2416,25 @@ __global__ __launch_bounds__(kFwThreads) void final_wide_kernel(
           mr[u] = use ? __builtin_nontemporal_load(&fx.sr[o]) : 0x7fffffff;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (w0 + u < S && w0 + u != sidx) list64_merge_aux(lk, la, lr, lane, mk[u], ma[u], mr[u], cat);
+        for (int u = 0; u < 8; ++u) {
+          // categorize lists (ties: most entries enter): a bitonic merge per list; Fast lists:
+          // only entries that beat the K-th enter, a few serial inserts (a bitonic merge per
+          // list, ~1.1 us, made C3's per-call rerank 36 -> 78 us:
+          // profiles/r05_basic_percall_stamps_radix_s32.log, r05_bench_v2.log)
+          if (cat) {
+            if (w0 + u < S && w0 + u != sidx) list64_merge_aux(lk, la, lr, lane, mk[u], ma[u], mr[u], true);
+            continue;
+          }
+          const float tk = rl_f2(lk, K - 1), ta = rl_f2(la, K - 1);
+          const int tr = __builtin_amdgcn_readlane(lr, K - 1);
+          uint64_t mask = __ballot(mr[u] != 0x7fffffff && entry_before(mk[u], ma[u], mr[u], tk, ta, tr, cat));
+          while (mask) {
+            const int bb = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            list64_insert_aux(lk, la, lr, lane, rl_f2(mk[u], bb), rl_f2(ma[u], bb), __builtin_amdgcn_readlane(mr[u], bb),
+                              K, cat);
+          }
+        }
       }
     }
     nx = __hip_atomic_load(&n_exact[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
