@@ -148,6 +148,10 @@ struct cwq_index {
   // launches the second list with the first replay (gated on its status) instead of after
   // reading that status back (categorize_impl)
   bool cat_two_spec = false;
+  // categorize: calls since the counting pass last resolved a query (after 8 such calls
+  // cat_count_kernel is skipped -- every query then goes to the replay anyway -- and tried
+  // again every kCatCountRetry calls)
+  int cat_count_idle = 0;
   int prn_gmax = 1;   // the most internal nodes of one pruning group
   int prn_maxdep = 0;   // deepest internal node of any group
   int *gi_dep = nullptr, *gi_ppos = nullptr;   // per group-list entry: depth, the parent's list position
@@ -2832,6 +2836,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
   return CWQ_OK;
 }
 
+constexpr int kCatCountRetry = 16;   // (cwq_index::cat_count_idle)
 int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
                     int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
@@ -2951,7 +2956,9 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     // the pop sequence by counting over the bottleneck order (cat_count_kernel); the
     // queries it cannot certify go through the heap replay (CWQ_CAT_COUNT=0: replay all)
     const char* cce = getenv("CWQ_CAT_COUNT");
-    const bool by_count = ix->NI > 0 && !ix->any_int_sent && !(cce && *cce && atoi(cce) == 0);
+    const int ccv = cce && *cce ? atoi(cce) : 1;   // 0: never, 2: always (tests)
+    const bool by_count = ix->NI > 0 && !ix->any_int_sent && ccv != 0 &&
+                          (ccv == 2 || ix->cat_count_idle < 8 || ix->cat_count_idle % kCatCountRetry == 0);
     if (by_count) {
       HIPCHK(launch_cat_count(sa, s));
       sa.pre_status = 1;
@@ -3039,10 +3046,12 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     std::vector<int> redo;
     for (int i = 0; i < nqc; ++i)
       if (st[i] && !fbad[i]) redo.push_back(i);   // filter failures are re-run whole below
+    int n_counted = 0;
     for (int i = 0; i < nqc; ++i) {
-      if (by_count && cst[i] == 0 && !fbad[i]) ++ix->stats[3];
+      if (by_count && cst[i] == 0 && !fbad[i]) ++ix->stats[3], ++n_counted;
       else if (!fbad[i]) ++ix->stats[4];
     }
+    if (ccv != 0) ix->cat_count_idle = by_count && n_counted > 0 ? 0 : std::min(ix->cat_count_idle + 1, 1 << 30);
     if (scat && two) ix->cat_two_spec = (int)redo.size() == nqc;
     if (redo.empty()) continue;
 
