@@ -283,21 +283,21 @@ def print_stamps(w, Qn, k):
     L = ctypes.CDLL(os.environ["CWQ_LIB"])
     fw = (ctypes.c_ulonglong * 4096)()
     two = (ctypes.c_ulonglong * 16)()
-    names = ["pop", "load", "push", "rows", "pops", "int_pops", "child_push", "row_push", "total"]
+    names = ["pop", "load", "push", "rows", "pops", "int_pops", "child_push", "row_push", "total", "pop_select"]
     for i in range(5):
         L.cwq_debug_fw_stamp(fw, 4096)   # clears
         w.cobweb_predict(Qn[i], k)
         torch.cuda.synchronize()
         L.cwq_debug_fw_stamp(fw, 4096)
         L.cwq_debug_two_stamp(two, 16)
-        blocks = [[fw[b * 16 + p] for p in range(9)] for b in range(256) if fw[b * 16]]
+        blocks = [[fw[b * 16 + p] for p in range(14)] for b in range(256) if fw[b * 16]]
         t0 = min(r[0] for r in blocks)
         rel = lambda v: (v - t0) * 0.01 if v >= t0 else float("nan")
         lines = []
         for b, r in enumerate(blocks):
             lines.append(" ".join(f"{rel(v):7.2f}" for v in r))
         print(f"-- call {i}: final_wide (last launch) {len(blocks)} workgroups, phase stamps us "
-              f"(0 entry,1 cands,2 T2,3 surv,4 rounds,5 kw-merge,6 last-arrival,7 split-merge,8 end)", flush=True)
+              f"(0 entry,1 cands,2 T2,3 surv,4 rounds,5 kw-merge,6 last-arrival,7 split-merge,8 end | 9 T2 pre-load,10 T2 lists,11 T2 staged,12 round-0 partials,13 round-0 chains)", flush=True)
         for ln in lines[:4] + (["..."] if len(lines) > 8 else []) + lines[-4:] if len(lines) > 8 else lines:
             print("   ", ln)
         print("   simulate_two q0 (cycles):", {n: int(two[j]) for j, n in enumerate(names)}, flush=True)
