@@ -2862,6 +2862,10 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   // per-call stream filter (stream_cat_list), and a two-level replay of every query of the
   // call reuses the chunk's internal pass instead of gathering and recomputing it
   const bool scat = filt && nq <= cq && stream_cat_ok(ix, (int)nq, R);
+  // a few queries without the filter (small trees): the two-level replay on the chunk too,
+  // list 2 by the exact scan (instead of gathering the queries and re-running the internal
+  // pass: qqp1k's Basic call 1.02 ms, profiles/r05_published_shapes_v3.log)
+  const bool small2 = !filt && nq <= std::min<int64_t>(cq, 64);
   const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
@@ -2872,8 +2876,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 12) + 17 * 256 +
                   (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
-    if (scat)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
-      need += 2 * stream_cat_bytes(ix, nqc) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
+    if (scat || small2)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
+      need += (scat ? 2 * stream_cat_bytes(ix, nqc) : 0) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
                                                                  (size_t)R * 12 + (size_t)cap2 * 16 + 16) + 32 * 256;
     if ((rc = ix->reserve(need))) return rc;
     Bump b(ix->ws, ix->ws_size);
@@ -2996,17 +3000,22 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       int* l2r = b.take<int>((size_t)nq_pad * R);
       HeapEnt* heap2 = b.take<HeapEnt>((size_t)nq_pad * cap2);
       status2 = b.take<int>((size_t)nq_pad);
-      okf2 = b.take<int>((size_t)nq_pad);
+      okf2 = scat ? b.take<int>((size_t)nq_pad) : nullptr;   // (the exact scan's lists are certified)
       HIPCHK(launch_cat_t2(c.BF, c.LPF, (int64_t)ldI, ix->NI, nqc, ix->par_int, okey, R, T2, s));
       Chunk c2t = c;
       c2t.BF = T2;   // the categorize key reads min(T2[parent], lp)
       int nst2 = 0;
       int rc2;
-      if ((rc2 = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
-        return rc2;
-      if ((rc2 = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2, b,
-                                 s)))
-        return rc2;
+      if (!scat) {   // both segments by the exact scan
+        if ((rc2 = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 3, 0, slabs)))
+          return rc2;
+      } else {
+        if ((rc2 = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
+          return rc2;
+        if ((rc2 = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2,
+                                   b, s)))
+          return rc2;
+      }
       HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
       SimArgs st2 = sa;
       st2.pre_status = 0;
@@ -3026,7 +3035,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     // it -- tests)
     const char* spe = getenv("CWQ_CAT_SPEC");
     const int spv = spe && *spe ? atoi(spe) : 1;
-    const bool spec = two && scat && spv != 0 && (ix->cat_two_spec || spv == 2);
+    const bool spec = two && (scat || small2) && spv != 0 && (ix->cat_two_spec || spv == 2);
     if (spec && (rc = two_chunk(status))) return rc;
     // the count status, the replay status, the filter's certified flags (and the second
     // list's) written by one kernel into host-mapped memory: one sync, no pageable copies
@@ -3052,12 +3061,12 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       else if (!fbad[i]) ++ix->stats[4];
     }
     if (ccv != 0) ix->cat_count_idle = by_count && n_counted > 0 ? 0 : std::min(ix->cat_count_idle + 1, 1 << 30);
-    if (scat && two) ix->cat_two_spec = (int)redo.size() == nqc;
+    if ((scat || small2) && two) ix->cat_two_spec = (int)redo.size() == nqc;
     if (redo.empty()) continue;
 
-    if (spec || (two && scat && (int)redo.size() == nqc)) {
-      if (!spec) {   // every query of the call, after the status read-back
-        if ((rc = two_chunk(nullptr))) return rc;
+    if (spec || (two && ((scat && (int)redo.size() == nqc) || small2))) {
+      if (!spec) {   // after the status read-back (gated: the first replay's resolved queries keep their results)
+        if ((rc = two_chunk(status))) return rc;
         HIPCHK(launch_gather_flags(ix->hflags, nqc, status2, okf2, nullptr, nullptr, nullptr, s));
         HIPCHK(hipStreamSynchronize(s));
         hs.assign(ix->hflags, ix->hflags + nqc);
@@ -3065,7 +3074,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       }
       std::vector<int> left;
       for (const int i : redo) {
-        if (hs[i] || !ho[i]) left.push_back(i);   // uncertified, or list 2 overflowed: DENSE
+        if (hs[i] || (okf2 && !ho[i])) left.push_back(i);   // uncertified, or list 2 overflowed: DENSE
         else ++ix->stats[5];
       }
       redo.swap(left);
