@@ -2846,7 +2846,11 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int kl = 64;
   int rc;
   const char* ce = getenv("CWQ_CAT_FILTER");
-  const bool filt = allow_filter && use_filter(ix, R, kFiltMinRows, false) && !(ce && *ce && atoi(ce) == 0);
+  // a call of a few queries takes the per-call stream lists from kStreamMinRows rows on (as
+  // Fast does): the exact 64-wide list scan of a small tree is its latency chain -- qqp1k
+  // (1,000 rows x 1,024): 285 us a list, profiles/r05_published_shapes_v4.log
+  const bool filt = allow_filter && use_filter(ix, R, nq <= 64 ? kStreamMinRows : kFiltMinRows, false) &&
+                    !(ce && *ce && atoi(ce) == 0);
   const int n_rt = filt ? (int)(ix->ld_f / kFgTile) : 0;
   const size_t filt_q = filt ? iso_filter_bytes_per_query(ix, n_rt) : 0;
   const int nqb_est = n_qblocks_for(nq, kl);
