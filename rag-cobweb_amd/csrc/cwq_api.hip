@@ -1443,7 +1443,11 @@ int run_internal(cwq_index* ix, Chunk& c, hipStream_t s, bool bf_lpf = true, con
   const int nslab2 = (a.nrows_pad + a.rows_per_slab - 1) / a.rows_per_slab;
   a.out = c.S_int;
   a.ldo = ix->NI;
-  HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
+  const char* rse = getenv("CWQ_RAW_SPLIT");   // 0: the scan kernel for one query too (A/B)
+  if (c.nq == 1 && (size_t)(ix->DP / 16) * kWave * 4 <= 65536 && !(rse && *rse && atoi(rse) == 0))
+    HIPCHK(launch_raw_split(c.X, ix->int_A, ix->int_B, a, s));
+  else
+    HIPCHK(launch_scan(false, EPI_RAW, false, kl, c.X, ix->int_A, ix->int_B, a, nslab2, s));
   return internal_prefixes(ix, c, s, BF, LPF, dfull, q, grp_cat);
 }
 

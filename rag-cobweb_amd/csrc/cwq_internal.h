@@ -137,6 +137,8 @@ hipError_t launch_logdet(const VarSrc& var, int D, const int64_t* nodes, int64_t
 hipError_t launch_inv_var0(const VarSrc& var, int D, const int64_t* nodes, int64_t n, float* out, hipStream_t s);
 
 // The fused scan: ISO/ANISO rows x {RAW, KEY, TOPK} x {fast, categorize}.
+// the internal pass of a one-query call (anisotropic rows, EPI_RAW), D split over 4 waves
+hipError_t launch_raw_split(const float* X, const float* A, const float* B, const ScanArgs& a, hipStream_t s);
 hipError_t launch_scan(bool iso, int epi, bool cat, int kl, const float* X, const float* A, const float* B,
                        const ScanArgs& a, int nslab, hipStream_t s);
 constexpr int kScanSmallQ = 256;     // calls with at most this many queries use the shared-query scan

@@ -309,6 +309,56 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X, 
   }
 }
 
+// The internal pass (anisotropic rows, raw sums) of a one-query call with D split over the
+// workgroup's 4 waves: 64 rows a workgroup (lane = row, coalesced dim-major loads), each wave
+// forms the 16-dim partials of a quarter of the slices, and the row's sum folds them in slice
+// order from LDS -- the scan's exact arithmetic (per-slice fma chain, left fold from 0), with a
+// dependent chain a quarter as long and NI/64 workgroups instead of NI/512.  (scan_kernel's
+// shared-query form: 69 us for C2's 35.5k internal nodes in 70 workgroups, 74 us for 366 nodes
+// -- the per-slice latency chain, not the bytes; profiles/r05_basic_percall_c2_timeline_v4.txt.)
+__global__ __launch_bounds__(256) void raw_split_kernel(const float* __restrict__ X, const float* __restrict__ A,
+                                                        const float* __restrict__ B, const ScanArgs a) {
+  extern __shared__ float s_part[];   // [NS][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int r0 = blockIdx.x * kWave;
+  const int row = min(r0 + lane, a.nrows_pad - 1);
+  const int NS = a.DP / 16;
+  const int per = (NS + kWavesPerWG - 1) / kWavesPerWG;
+  const int s_lo = wave * per, s_hi = min(NS, s_lo + per);
+  const f32x16* __restrict__ xg = reinterpret_cast<const f32x16*>(X);   // query 0 of block 0
+  for (int sl = s_lo; sl < s_hi; ++sl) {
+    float m[16], sv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      m[j] = A[(size_t)(sl * 16 + j) * a.ld + row];
+      sv[j] = B[(size_t)(sl * 16 + j) * a.ld + row];
+    }
+    const f32x16 xa = xg[(size_t)sl * kXQ];
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float t = fmaf(xa[j], m[j], -sv[j]);
+      part = (j == 0) ? t * t : fmaf(t, t, part);
+    }
+    s_part[sl * kWave + lane] = part;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float acc = 0.f;
+    for (int sl = 0; sl < NS; ++sl) acc += s_part[sl * kWave + lane];
+    const int r = r0 + lane;
+    if (r < a.nrows) a.out[a.out_base + r] = acc;
+  }
+}
+
+hipError_t launch_raw_split(const float* X, const float* A, const float* B, const ScanArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)(a.DP / 16) * kWave * sizeof(float);
+  if (a.nq != 1 || a.DP % 16 || lds > 65536 || a.nrows <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(raw_split_kernel, dim3((unsigned)((a.nrows + kWave - 1) / kWave)), dim3(256), lds, s, X, A, B, a);
+  return hipGetLastError();
+}
+
 // Scan configurations for the hot path (ISO/ANISO x TOPK/KEY/RAW, list width 16),
 // selectable at run time with CWQ_SCAN_CFG for A/B measurement.
 struct ScanCfg {
