@@ -1922,11 +1922,15 @@ int stream_topk_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64
                 int_bounds_bytes(ix, kFgTile) + (size_t)nq16 * ix->DPB + (size_t)nq16 * 16 + 512 +
                 (size_t)nqc * kFwSplitMax * 64 * 12 + 3 * 256 + (size_t)((ix->NL_iso + 15) / 16) * 4 + 256;
   const bool ib = use_int_bounds(ix);
-  // int8 pass on flat trees only: with bounded internal prefixes the ~9x exact reranks pay
-  // the exact parent chains too (b4/L9 one query per call 692 -> 1166 us,
-  // profiles/r03_i8_ab_hier_*.log); CWQ_STREAM_I8=1 forces it
+  // int8 pass: flat trees, and hierarchical ones for calls of <= 8 queries.  With bounded
+  // internal prefixes the ~9x exact reranks pay the exact parent chains too: round 3, b4/L9
+  // one query per call 692 -> 1166 us (profiles/r03_i8_ab_hier_*.log); with the split rerank
+  // tail and its radix T2 it pays at a few queries (nq 1 / 8: 670 -> 601 / 722 -> 664 us) and
+  // not at 64 (1373 -> 3161 us), profiles/r05_percall_b4d9_i8_ab.log.  CWQ_STREAM_I8=1 / 0
+  // forces it on / off.
   const char* e8 = getenv("CWQ_STREAM_I8");
-  const bool i8 = (!ib || (e8 && *e8 && atoi(e8) == 1)) && ensure_i8(ix, s);
+  const int e8v = e8 && *e8 ? atoi(e8) : -1;
+  const bool i8 = e8v != 0 && (!ib || nqc <= 8 || e8v == 1) && ensure_i8(ix, s);
   int rc;
   if ((rc = ix->reserve(need))) return rc;
   Bump b(ix->ws, ix->ws_size);

@@ -39,13 +39,13 @@ def main():
         fs = pkg.synth.flat_synth(X)
     ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)
     del fs
-    Q, _ = pkg.synth.synthetic_queries(X, max(int(v) for v in args.nq.split(",")), seed=1)
+    Q, _ = pkg.synth.synthetic_queries(X, max(int(v) for v in args.nq.replace("+", ",").split(",")), seed=1)
     del X
     torch.cuda.empty_cache()
     fp32_bytes = 4.0 * args.n * args.dim
     bf16_bytes = 2.0 * args.n * args.dim
     ref = {}
-    for nq in [int(v) for v in args.nq.split(",")]:
+    for nq in [int(v) for v in args.nq.replace("+", ",").split(",")]:
         q = Q[:nq].contiguous()
         for mode in [int(m) for m in args.modes.split(",")]:
             ix.set_filter(mode)
