@@ -1534,7 +1534,8 @@ int run_internal_bounds(cwq_index* ix, Chunk& c, const float* q, int64_t nqf, Bu
     sa.root_ld = ix->root_ld;
     sa.pout = c.P;
     sa.ldpout = g.ldlb;
-    HIPCHK(launch_stream(sa, 2, ix->cus, s));
+    const char* iwe = getenv("CWQ_INT_STREAM_WGS");   // workgroups per CU (A/B; read per call)
+    HIPCHK(launch_stream(sa, 2, ix->cus * (iwe && atoi(iwe) > 0 ? std::min(4, atoi(iwe)) : 1), s));
   } else {
     HIPCHK(hipMemsetAsync(tctr, 0, 64 * 4, s));   // the tile claim counters (the stream pass has none)
     HIPCHK(launch_fgemm(Xb2, ix->int_Mb2, g, ix->cus, s));
