@@ -1590,6 +1590,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   int status = 0, found = 0, gpops = 0;
   int64_t calls = 1, visited = 0;
   unsigned long long c_pop = 0, c_load = 0, c_push = 0, c_rows = 0, n_int = 0, n_ch = 0, n_rows = 0, c_sel = 0;
+  int max_runs = 0;
   const unsigned long long t_start = TWO_CLK();
   // list 1 must be full, end inside the tie at G, and hold every group root among the rows
   if (!(G > -CWQ_INF) || wG == 0x7fffffff || !(xG > G) || a.NI <= 0) status = 1;
@@ -1644,6 +1645,9 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
       hix[j] = adv ? idx + 1 : hix[j];
     }
     if (!more) --nruns;
+#if CWQ_STAMP
+    max_runs = max(max_runs, nruns + 1);
+#endif
     c_pop += TWO_CLK() - tp0;
     ++visited;
     const bool is_int = e.node >= 0;
@@ -1749,13 +1753,13 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
   }
 #if CWQ_STAMP
   if (lane == 0 && q == 0) {
-    const unsigned long long v[10] = {c_pop, c_load, c_push, c_rows, (unsigned long long)visited, n_int, n_ch, n_rows,
-                                      TWO_CLK() - t_start, c_sel};
-    for (int i = 0; i < 10; ++i) g_two_stamp[i] = v[i];
+    const unsigned long long v[11] = {c_pop, c_load, c_push, c_rows, (unsigned long long)visited, n_int, n_ch, n_rows,
+                                      TWO_CLK() - t_start, c_sel, (unsigned long long)max_runs};
+    for (int i = 0; i < 11; ++i) g_two_stamp[i] = v[i];
   }
 #else
   (void)c_pop, (void)c_load, (void)c_push, (void)c_rows, (void)n_int, (void)n_ch, (void)n_rows, (void)t_start,
-      (void)c_sel;
+      (void)c_sel, (void)max_runs;
 #endif
 }
 #undef TWO_ADD_RUN

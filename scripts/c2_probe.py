@@ -283,7 +283,7 @@ def print_stamps(w, Qn, k):
     L = ctypes.CDLL(os.environ["CWQ_LIB"])
     fw = (ctypes.c_ulonglong * 4096)()
     two = (ctypes.c_ulonglong * 16)()
-    names = ["pop", "load", "push", "rows", "pops", "int_pops", "child_push", "row_push", "total", "pop_select"]
+    names = ["pop", "load", "push", "rows", "pops", "int_pops", "child_push", "row_push", "total", "pop_select", "max_live_runs"]
     for i in range(5):
         L.cwq_debug_fw_stamp(fw, 4096)   # clears
         w.cobweb_predict(Qn[i], k)
