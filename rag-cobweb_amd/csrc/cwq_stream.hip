@@ -459,14 +459,18 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
     __syncthreads();
     if (s_last) {
+      if (2 * a.nq <= SK_WAVES) {
       // T0 = the K-th largest of the probe's values (group maxima, or every probed row's
       // bound with probe_rows; multiplicity counted, -inf with fewer than K): a radix select
       // of ord_f32 keys, 6-bit digits from the top (5 passes, then the last 2 bits), wpq waves
       // per query sharing an LDS histogram (past the flag word: the query image is no longer
       // read).  Only T0 = sel_lk[q][K-1] is read downstream (the pass's threshold; the rerank
       // forms its own).  All waves run the same passes and rounds, so the barriers are uniform.
-      // (It replaces per-wave top-K lists whose serial inserts made the C2 categorize probe of
-      // list 1 -- 18.7k finite bounds -- twice as long as list 2's, profiles/r05_basic_percall_c2_timeline_v3.txt.)
+      // (Per-wave top-K lists' serial inserts made the C2 categorize probe of list 1 -- 18.7k
+      // finite bounds -- twice as long as list 2's, profiles/r05_basic_percall_c2_timeline_v3.txt;
+      // with a wave per query -- nq >= SK_WAVES / 2 -- the lists are kept: six passes over
+      // each query's values cost more there, C3 nq = 64 probe 0.16 -> 0.31 ms,
+      // profiles/r05_bench_v4.log.)
       unsigned* s_h = reinterpret_cast<unsigned*>(sq) + 16;   // [qpr][64] histograms
       unsigned* s_rs = s_h + SK_WAVES * 64;                    // [qpr][2] prefix, rank left
       const int n = (int)(a.probe_rows ? a.n_probe * 16 : a.n_probe);
@@ -530,6 +534,45 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
           a.sel_lk[(size_t)q * 64 + lane] = lane == a.K - 1 ? T0 : -CWQ_INF;
           a.sel_lr[(size_t)q * 64 + lane] = 0x7fffffff;
         }
+      }
+      } else {
+      // the K-th largest of the probe's values (group maxima, or every probed row's bound
+      // with probe_rows) one by one: wpq waves per query on its value range, the first of
+      // them merging the others' lists (LDS past the flag word: the query image is no
+      // longer read); all waves run the same rounds, so the barriers are uniform
+      float* s_lk = reinterpret_cast<float*>(sq) + 16;
+      int* s_lr = reinterpret_cast<int*>(sq) + 16 + SK_WAVES * 64;
+      const int n = (int)(a.probe_rows ? a.n_probe * 16 : a.n_probe);
+      const int wpq = a.nq >= SK_WAVES ? 1 : SK_WAVES / a.nq;
+      const int qpr = SK_WAVES / wpq;   // queries per round
+      const int sub = wave % wpq;
+      const int per = (n + wpq * 64 - 1) / (wpq * 64) * 64;
+      for (int q0 = 0; q0 < a.nq; q0 += qpr) {
+        const int q = q0 + wave / wpq;
+        const bool act = wave / wpq < qpr && q < a.nq;
+        float lk = -CWQ_INF;
+        int lr = 0x7fffffff;
+        if (act) {
+          const int lo = min(n, sub * per);
+          select_values_wave(a.lb + (size_t)q * a.ldlb, lo, min(n, lo + per), a.K, lane, lk, lr);
+        }
+        if (wpq > 1) {
+          s_lk[wave * 64 + lane] = lk;
+          s_lr[wave * 64 + lane] = lr;
+          __syncthreads();
+          if (act && sub == 0)
+            for (int w = wave + 1; w < wave + wpq; ++w) {
+              const int r = s_lr[w * 64 + lane];
+              list64_offer(lk, lr, lane, lane < a.K && r != 0x7fffffff ? s_lk[w * 64 + lane] : -CWQ_INF, r, a.K);
+            }
+        }
+        if (act && sub == 0) {
+          if (a.sel_floor && lane == a.K - 1) lk = fmaxf(lk, a.sel_floor[q]);
+          a.sel_lk[(size_t)q * 64 + lane] = lk;
+          a.sel_lr[(size_t)q * 64 + lane] = lr;
+        }
+        if (wpq > 1) __syncthreads();
+      }
       }
       if (threadIdx.x == 0) __hip_atomic_store(a.sel_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
