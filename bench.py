@@ -241,10 +241,32 @@ def per_call_harness(pkg, index, Q, k, reps=200, basic=False, node_of_sentence=N
         ts.append(time.perf_counter() - t)
     ts.sort()
     name = "cobweb_predict" if basic else "cobweb_predict_fast"
-    return {"call": f"CobwebWrapper.{name}(numpy_query, k) -> list of sentences",
-            "queries": reps, "us_per_call_median": round(ts[reps // 2] * 1e6, 1),
-            "us_per_call_p10": round(ts[reps // 10] * 1e6, 1), "us_per_call_mean": round(float(np.mean(ts)) * 1e6, 1),
-            "queries_per_s": round(reps / float(np.sum(ts)), 1)}
+    out = {"call": f"CobwebWrapper.{name}(numpy_query, k) -> list of sentences",
+           "queries": reps, "us_per_call_median": round(ts[reps // 2] * 1e6, 1),
+           "us_per_call_p10": round(ts[reps // 10] * 1e6, 1), "us_per_call_mean": round(float(np.mean(ts)) * 1e6, 1),
+           "queries_per_s": round(reps / float(np.sum(ts)), 1)}
+    if basic:
+        # where the call's time goes: the search itself (cwq_categorize_host, host query in,
+        # node ids out) and the wrapper's advance of Python's global `random` stream by the
+        # reference's draw count (one random() per log_prob call and per retrieval,
+        # CobwebTorchTree.py:243,268,285 -- a million on this flat tree)
+        import random as _random
+        tc, tr = [], []
+        for i in range(reps):
+            t = time.perf_counter()
+            _, found, calls = index.categorize_host(Qh[i:i + 1], k, w.max_init_search)
+            tc.append(time.perf_counter() - t)
+            st = _random.getstate()
+            t = time.perf_counter()
+            pkg.wrapper.advance_random(int(calls[0]) + int(found[0]))
+            tr.append(time.perf_counter() - t)
+            _random.setstate(st)
+        tc.sort()
+        tr.sort()
+        out["categorize_host_us_median"] = round(tc[reps // 2] * 1e6, 1)
+        out["rng_advance_us_median"] = round(tr[reps // 2] * 1e6, 1)
+        out["log_prob_calls_per_query"] = int(calls[0])
+    return out
 
 
 def main():
