@@ -2917,8 +2917,10 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 2, 1, slabs)))
         return rc;
       okf_d = b.take<int>((size_t)nq_pad);
-      if ((rc = stream_cat_list(ix, c, q + q0 * ix->D, nqc, R, c.BF, dfull, pkey, paux, prow, (int64_t)nst * R, okf_d, b,
-                                s)))
+      // no anisotropic rows (nst == 1): the rerank writes list 1 itself, no merge launch
+      if ((rc = nst == 1 ? stream_cat_list(ix, c, q + q0 * ix->D, nqc, R, c.BF, dfull, okey, oaux, orow, R, okf_d, b, s)
+                         : stream_cat_list(ix, c, q + q0 * ix->D, nqc, R, c.BF, dfull, pkey, paux, prow,
+                                           (int64_t)nst * R, okf_d, b, s)))
         return rc;
     } else if (filt) {
       // isotropic rows: the filter with the categorize key -> exact keys in list slot 0;
@@ -2935,7 +2937,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     } else if ((rc = run_leaf_scan(ix, c, EPI_TOPK, true, kl, dfull, nullptr, 0, pkey, paux, prow, R, &nst, s, 3, 0, slabs))) {
       return rc;
     }
-    HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s, true));
+    if (!(filt && scat && nst == 1)) HIPCHK(launch_merge(pkey, paux, prow, nqc, nst * R, R, okey, oaux, orow, s, true));
     SimArgs sa;
     memset(&sa, 0, sizeof(sa));
     sa.nq = nqc;
@@ -3025,11 +3027,12 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       } else {
         if ((rc2 = run_leaf_scan(ix, c2t, EPI_TOPK, true, kl, dfull, nullptr, 0, pk2, pa2, pr2, R, &nst2, s, 2, 1, slabs)))
           return rc2;
-        if ((rc2 = stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2, (int64_t)nst2 * R, okf2,
-                                   b, s)))
+        if ((rc2 = nst2 == 1 ? stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, l2k, l2a, l2r, R, okf2, b, s)
+                             : stream_cat_list(ix, c2t, q + q0 * ix->D, nqc, R, T2, dfull, pk2, pa2, pr2,
+                                               (int64_t)nst2 * R, okf2, b, s)))
           return rc2;
       }
-      HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
+      if (!(scat && nst2 == 1)) HIPCHK(launch_merge(pk2, pa2, pr2, nqc, nst2 * R, R, l2k, l2a, l2r, s, true));
       SimArgs st2 = sa;
       st2.pre_status = 0;
       st2.lkey2 = l2k;
