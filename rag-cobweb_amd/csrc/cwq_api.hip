@@ -148,6 +148,7 @@ struct cwq_index {
   // launches the second list with the first replay (gated on its status) instead of after
   // reading that status back (categorize_impl)
   bool cat_two_spec = false;
+  bool cat_tail_done = false;   // categorize_impl: the node tails are cleared, nothing runs after its last sync
   // categorize: calls since the counting pass last resolved a query (after 8 such calls
   // cat_count_kernel is skipped -- every query then goes to the replay anyway -- and tried
   // again every kCatCountRetry calls)
@@ -2879,6 +2880,9 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   // list 2 by the exact scan (instead of gathering the queries and re-running the internal
   // pass: qqp1k's Basic call 1.02 ms, profiles/r05_published_shapes_v3.log)
   const bool small2 = !filt && nq <= std::min<int64_t>(cq, 64);
+  // every query resolved in the first chunk by the list paths: the flag gathers cleared the
+  // node tails after the last results, so the caller needs no clear_tail launch / sync
+  ix->cat_tail_done = nq <= cq;
   const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
@@ -3056,7 +3060,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     // the count status, the replay status, the filter's certified flags (and the second
     // list's) written by one kernel into host-mapped memory: one sync, no pageable copies
     if ((rc = ix->host_flags((size_t)5 * nqc))) return rc;
-    HIPCHK(launch_gather_flags(ix->hflags, nqc, cst_d, status, okf_d, spec ? status2 : nullptr, spec ? okf2 : nullptr, s));
+    HIPCHK(launch_gather_flags(ix->hflags, nqc, cst_d, status, okf_d, spec ? status2 : nullptr, spec ? okf2 : nullptr, s,
+                               nodes + q0 * k, n_found + q0, k));
     HIPCHK(hipStreamSynchronize(s));
     const int* hf = ix->hflags;
     std::vector<int> cst(hf, hf + (by_count ? nqc : 0)), st(hf + nqc, hf + 2 * (size_t)nqc);
@@ -3083,7 +3088,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     if (spec || (two && ((scat && (int)redo.size() == nqc) || small2))) {
       if (!spec) {   // after the status read-back (gated: the first replay's resolved queries keep their results)
         if ((rc = two_chunk(status))) return rc;
-        HIPCHK(launch_gather_flags(ix->hflags, nqc, status2, okf2, nullptr, nullptr, nullptr, s));
+        HIPCHK(launch_gather_flags(ix->hflags, nqc, status2, okf2, nullptr, nullptr, nullptr, s, nodes + q0 * k,
+                                   n_found + q0, k));
         HIPCHK(hipStreamSynchronize(s));
         hs.assign(ix->hflags, ix->hflags + nqc);
         ho.assign(ix->hflags + nqc, ix->hflags + 2 * (size_t)nqc);
@@ -3095,6 +3101,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       }
       redo.swap(left);
     } else if (two) {
+      ix->cat_tail_done = false;   // the gathered replay writes after the flag gather
       std::vector<float> h1k((size_t)nqc * R), h1a((size_t)nqc * R);
       std::vector<int> h1r((size_t)nqc * R);
       HIPCHK(hipMemcpyAsync(h1k.data(), okey, h1k.size() * 4, hipMemcpyDeviceToHost, s));
@@ -3200,6 +3207,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     }
     ix->stats[1] += (int64_t)redo.size();
     if (redo.empty()) continue;
+    ix->cat_tail_done = false;   // the DENSE re-run below writes after the last flag gather
 
     // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
     const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
@@ -3289,6 +3297,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HIPCHK(launch_copy_rows(fd, 1, nullptr, n_found, 1, d_idx, n, 1, s));
     if (n_calls) HIPCHK(launch_copy_rows(cl, 2, nullptr, n_calls, 2, d_idx, n, 2, s));
     HIPCHK(hipStreamSynchronize(s));
+    ix->cat_tail_done = false;
   }
   return CWQ_OK;
 }
@@ -3309,7 +3318,7 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   const int rc = categorize_impl(ix, q, nq, k, max_nodes, nodes, n_found, n_calls, s, true);
   ix->stats[0] = nq;
   if (rc) return rc;
-  HIPCHK(launch_clear_tail(nodes, n_found, nq, k, s));
+  if (!ix->cat_tail_done) HIPCHK(launch_clear_tail(nodes, n_found, nq, k, s));
   return CWQ_OK;
 }
 
@@ -3340,8 +3349,10 @@ extern "C" int cwq_categorize_host(cwq_index* ix, const float* q, int64_t nq, in
   rc = categorize_impl(ix, (const float*)ix->dq, nq, k, max_nodes, hn, hf, hc, s, true);
   ix->stats[0] = nq;
   if (rc) return rc;
-  HIPCHK(launch_clear_tail(hn, hf, nq, k, s));
-  HIPCHK(sync_spin(s));
+  if (!ix->cat_tail_done) {   // (otherwise categorize_impl's last sync already covers every write)
+    HIPCHK(launch_clear_tail(hn, hf, nq, k, s));
+    HIPCHK(sync_spin(s));
+  }
   ix->ws_idle = true;   // synchronized
   memcpy(nodes, hn, (size_t)nq * k * 8);
   memcpy(n_found, hf, fb);

@@ -248,8 +248,10 @@ hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s);
 hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hipStream_t s);
 // dst[j * nq + q] = src[j] ? src[j][q] : 0 for j < 5: a call's per-query flag arrays into one
 // host-mapped buffer, read back with a single stream sync (no pageable copies)
+// nodes (optional): also nodes[q][i] = -1 for i >= n_found[q] (clear_tail_kernel's work)
 hipError_t launch_gather_flags(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
-                               const int* s4, hipStream_t s);
+                               const int* s4, hipStream_t s, int64_t* nodes = nullptr, const int* n_found = nullptr,
+                               int k = 0);
 hipError_t launch_clear_tail(int64_t* nodes, const int* n_found, int64_t nq, int k, hipStream_t s);
 hipError_t launch_merge(const float* pkey, const float* paux, const int* prow, int nq, int nent, int K,
                         float* okey, float* oaux, int* orow, hipStream_t s, bool cat);

@@ -1788,19 +1788,22 @@ __global__ void skip_failed_kernel(int* status, const int* okf, int nq, int init
 }
 
 __global__ void gather_flags_kernel(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
-                                    const int* s4) {
+                                    const int* s4, int64_t* nodes, const int* n_found, int k) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
   const int* src[5] = {s0, s1, s2, s3, s4};
 #pragma unroll
   for (int j = 0; j < 5; ++j) dst[(size_t)j * nq + q] = src[j] ? src[j][q] : 0;
+  if (nodes)   // clear_tail_kernel's work for these queries (their results so far)
+    for (int i = max(n_found[q], 0); i < k; ++i) nodes[(size_t)q * k + i] = -1;
 }
 
 hipError_t launch_gather_flags(int* dst, int nq, const int* s0, const int* s1, const int* s2, const int* s3,
-                               const int* s4, hipStream_t s) {
+                               const int* s4, hipStream_t s, int64_t* nodes, const int* n_found, int k) {
   if (nq <= 0) return hipSuccess;
+  if (nodes && (!n_found || k <= 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_flags_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, dst, nq, s0, s1, s2, s3,
-                     s4);
+                     s4, nodes, n_found, k);
   return hipGetLastError();
 }
 
