@@ -311,6 +311,10 @@ int cwq_fit_node_op(int32_t op, float* count, float* mean, float* meanSq, int32_
  *   cwq_mt19937_draw n draws of Python's random.random() from state625 (host; updates it)
  *   cwq_mt19937_words n 32-bit outputs (Python's getrandbits(32)) from state625 through the
  *                    chain-form twist the device's parallel generator runs (host; updates it)
+ *   cwq_mt19937_skip  advance state625 past nwords 32-bit outputs without producing them
+ *                    (host; updates it): the Basic query's random() advance -- one random()
+ *                    = 2 words per heap push and retrieval (CobwebTorchTree.py:243,268,285),
+ *                    replacing getrandbits(64 n) (CobwebWrapper.cobweb_predict, wrapper.py)
  */
 typedef struct cwq_fit cwq_fit;
 int cwq_fit_create(int device, int32_t dim, float prior_var, int32_t cap_nodes, cwq_fit** out);
@@ -324,6 +328,7 @@ int cwq_fit_export(cwq_fit* h, int32_t* out2, int32_t* parent, int32_t* child_pt
 const char* cwq_fit_last_error(void);
 int cwq_mt19937_draw(uint32_t* state625, int64_t n, double* out);
 int cwq_mt19937_words(uint32_t* state625, int64_t n, uint32_t* out);
+int cwq_mt19937_skip(uint32_t* state625, int64_t nwords);
 
 /*
  * PCA + ICA whitening transform (F4).  Replaces PCAICAWhiteningModel.transform

@@ -56,6 +56,7 @@ SIGNATURES = {
     "cwq_fit_last_error": (_c.c_char_p, []),
     "cwq_mt19937_draw": (_c.c_int, [_P, _I64, _P]),
     "cwq_mt19937_words": (_c.c_int, [_P, _I64, _P]),
+    "cwq_mt19937_skip": (_c.c_int, [_P, _I64]),
 }
 
 _lock = threading.Lock()

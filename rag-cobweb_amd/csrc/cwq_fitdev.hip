@@ -35,6 +35,7 @@
 #include <unistd.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -1596,6 +1597,51 @@ extern "C" int cwq_mt19937_words(uint32_t* state625, int64_t n, uint32_t* out) {
       idx = 0;
     }
     out[i] = mt_temper(state625[idx++]);
+  }
+  state625[kMtN] = (uint32_t)idx;
+  return CWQ_OK;
+}
+
+// Advance state625 past nwords 32-bit outputs (Python's genrand_uint32 stream) without
+// tempering them: the rest of the current block by its index, then whole twists.  A
+// Basic query advances the global random() stream by the draws the reference makes
+// (CobwebTorchTree.py:243,268,285 -- 2 words per random()): ~2M words on a flat 1M tree,
+// where getrandbits(64 n) built an 8 MB integer (4.5 ms).  The twist is the standard
+// three-segment loop (no loop-carried dependence closer than 227 words, so the compiler
+// vectorises each segment).
+namespace {
+void mt_twist_plain(uint32_t* __restrict__ mt) {
+  for (int kk = 0; kk < kMtN - kMtM; ++kk) {
+    const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+    mt[kk] = mt[kk + kMtM] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  for (int base = kMtN - kMtM; base < kMtN - 1; base += kMtN - kMtM) {   // reads words >= 227 back
+    const int end = std::min(base + (kMtN - kMtM), kMtN - 1);
+    for (int kk = base; kk < end; ++kk) {
+      const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + (kMtM - kMtN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+  }
+  const uint32_t y = (mt[kMtN - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+  mt[kMtN - 1] = mt[kMtM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+}
+}  // namespace
+
+extern "C" int cwq_mt19937_skip(uint32_t* state625, int64_t nwords) {
+  if (!state625 || nwords < 0) return CWQ_ERR_ARG;
+  int64_t idx = state625[kMtN];
+  if (idx > kMtN) return CWQ_ERR_ARG;
+  const int64_t avail = kMtN - idx;
+  if (nwords <= avail) {
+    state625[kMtN] = (uint32_t)(idx + nwords);
+    return CWQ_OK;
+  }
+  nwords -= avail;
+  while (nwords > 0) {   // Python twists when the index reaches 624, then takes words 0..
+    mt_twist_plain(state625);
+    const int64_t take = std::min<int64_t>(nwords, kMtN);
+    idx = take;
+    nwords -= take;
   }
   state625[kMtN] = (uint32_t)idx;
   return CWQ_OK;

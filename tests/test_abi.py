@@ -138,3 +138,29 @@ def test_device_mt19937_chain_twist_is_pythons_stream(pkg):
     want = np.array([r.getrandbits(32) for _ in range(n)], np.uint32)
     np.testing.assert_array_equal(out, want)
     assert tuple(int(v) for v in st) == r.getstate()[1]
+
+
+@pytest.mark.parametrize("n", [0, 1, 311, 312, 624, 4095, 4096, 10**6 + 1])
+def test_native_random_advance_equals_getrandbits(pkg, n):
+    """The Basic query's random() advance (wrapper.advance_random: cwq_mt19937_skip for
+    large n, getrandbits below) leaves the state getrandbits(64 n) leaves -- from fresh,
+    mid-block and end-of-block indices -- and the stream continues identically."""
+    import random
+    for warm in (0, 1, 311, 624):
+        a, b = random.Random(5 + warm), random.Random(5 + warm)
+        for _ in range(warm):
+            a.random()
+            b.random()
+        pkg.wrapper.advance_random(n, a)
+        if n:
+            b.getrandbits(64 * n)
+        assert a.getstate() == b.getstate()
+        assert [a.random() for _ in range(700)] == [b.random() for _ in range(700)]
+    # the native entry point on its own (also below the wrapper's cut-over)
+    r = random.Random(9)
+    r.random()
+    st = np.ascontiguousarray(np.asarray(r.getstate()[1], np.uint32))
+    assert pkg.lib().cwq_mt19937_skip(st.ctypes.data_as(ctypes.c_void_p), 2 * n) == 0
+    if n:
+        r.getrandbits(64 * n)
+    assert tuple(int(v) for v in st) == r.getstate()[1]
