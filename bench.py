@@ -19,7 +19,10 @@ over the ranks by `sharded_query` (strong scaling).  No collective in the timed 
 
 Also reported: `per_call` (the reference harness's one-query-per-call mode at nq = 1, 8,
 64, plus the wrapper's numpy-query Fast and Basic calls: harness_call_nq1,
-harness_basic_nq1) and `cpu_baseline` (the reference op sequence in torch-CPU, all threads + 1 thread).
+harness_basic_nq1), `hier` (a device-ifit Cobweb tree over a 100k x 768 clustered corpus:
+ifit inserts/s, Fast batch / per call, Basic batch / per call, the filter and pruning
+stats; hier_leg) and `cpu_baseline` (the reference op sequence in torch-CPU, all threads +
+1 thread).
 """
 import argparse
 import json
@@ -269,6 +272,105 @@ def per_call_harness(pkg, index, Q, k, reps=200, basic=False, node_of_sentence=N
     return out
 
 
+def hier_leg(pkg, n=100_000, dim=768, n_clusters=100, nq=1000, k=10, calls=100):
+    """A real-shaped Cobweb tree in the driver's record (BASELINE configs[1]'s shape, C2):
+    the drop-in's own device ifit over the clustered stand-in corpus (synth.clustered_corpus,
+    the corpus of tests/test_gpu_c2.py) -- the reference's workflow, CobwebWrapper(corpus,
+    embeddings) (CobwebWrapper.py:13-80 via benchmark_utils.py:438-467) then
+    build_prediction_index and queries (benchmark_utils.py:576-581, 801-805).  Reports the
+    ifit inserts/s and tree shape, the tree-adaptive cut, Fast batch q/s with its filter and
+    pruning stats (ids and scores checked against the exact scan), Fast per call (nq = 1, 8,
+    64, and the harness's cobweb_predict_fast(numpy, k)), Basic batch q/s and the harness's
+    cobweb_predict(numpy, k).  Not the headline `value` (a 1,000-query batch on a 100k tree)."""
+    import random as _random
+    X, Qn, pick = pkg.synth.clustered_corpus(n, dim, n_clusters, nq)
+    _random.seed(2)
+    w0 = pkg.CobwebWrapper(corpus=None, corpus_embeddings=X[:8])   # libcwq warm (fitter kernels loaded)
+    w0.build_prediction_index()
+    torch.cuda.synchronize()
+    _random.seed(2)
+    t0 = time.perf_counter()
+    w = pkg.CobwebWrapper(corpus=[f"p{i}" for i in range(n)], corpus_embeddings=X)
+    torch.cuda.synchronize()
+    t_fit = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    w.build_prediction_index()
+    torch.cuda.synchronize()
+    t_ix = time.perf_counter() - t0
+    ix = w._index
+    inf = ix.info
+    out = {"workload": f"device-ifit Cobweb tree over {n}x{dim} clustered embeddings ({n_clusters} Gaussian clusters, "
+                       f"synth.clustered_corpus seed 2), {nq} queries, k={k} (BASELINE configs[1] shape, C2)",
+           "ifit_s": round(t_fit, 2), "ifit_inserts_per_s": round(n / t_fit, 1), "index_build_s": round(t_ix, 3),
+           "tree": {"nodes": inf["n_nodes"], "internal": inf["internal_nodes"], "max_depth": inf["max_depth"],
+                    "root_children": len(w.tree.root.children)},
+           "cut": ix.cut_info(), "filter_rows": ix.filter_info()}
+    Q = torch.from_numpy(Qn).cuda()
+
+    def med(f, reps):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t)
+        ts.sort()
+        return ts[len(ts) // 2]
+
+    ix.set_filter(0)
+    ids0, s0 = ix.score_topk(Q, k)
+    t_scan = med(lambda: ix.score_topk(Q, k), 5)
+    ix.set_filter(-1)
+    ids1, s1 = ix.score_topk(Q, k)
+    t_fast = med(lambda: ix.score_topk(Q, k), 11)
+    st, ps = ix.last_stats(), ix.last_prune_stats()
+    out["fast_batch"] = {"ms": round(t_fast * 1e3, 3), "queries_per_s": round(nq / t_fast, 1),
+                         "exact_scan_ms": round(t_scan * 1e3, 3),
+                         "equal_to_exact_scan": bool(torch.equal(ids0, ids1) and torch.equal(s0, s1)),
+                         "filter": {k_: st[k_] for k_ in ("filter_used", "fallback_queries", "candidates",
+                                                          "exact_reranks")},
+                         "prune": ps,
+                         "perturbed_row_first": round(float((ids1[:len(pick), 0].cpu().numpy() == pick).mean()), 4)}
+    pc = {}
+    for m in (1, 8, 64):
+        qs = [Q[i:i + m].contiguous() for i in range(0, min(nq, calls * m), m)][:calls]
+        same = all(torch.equal(ix.score_topk(q, k)[0], ids0[i * m:i * m + m]) for i, q in enumerate(qs[:10]))
+        ts = []
+        for q in qs:
+            t = time.perf_counter()
+            ix.score_topk(q, k)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t)
+        ts.sort()
+        pc[str(m)] = {"us_per_call": round(ts[len(ts) // 2] * 1e6, 1), "path": ix.last_stats()["path"],
+                      "equal_to_exact_scan": bool(same)}
+    out["fast_per_call"] = pc
+    ts = []
+    for i in range(calls):
+        t = time.perf_counter()
+        w.cobweb_predict_fast(Qn[i % nq], k)
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    out["harness_call_nq1_us"] = round(ts[len(ts) // 2] * 1e6, 1)
+    nodes, found, ncalls = ix.categorize(Q, k, w.max_init_search)
+    t_b = med(lambda: ix.categorize(Q, k, w.max_init_search), 5)
+    out["basic_batch"] = {"ms": round(t_b * 1e3, 3), "queries_per_s": round(nq / t_b, 1),
+                          "found_k": round(float((found == k).float().mean()), 4),
+                          "log_prob_calls_per_query": round(float(ncalls.float().mean()), 1),
+                          "resolved": ix.last_categorize_stats()}
+    ts = []
+    for i in range(calls):
+        t = time.perf_counter()
+        w.cobweb_predict(Qn[i % nq], k)
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    out["harness_basic_nq1_us"] = round(ts[len(ts) // 2] * 1e6, 1)
+    w._invalidate_prediction_index()
+    w0._invalidate_prediction_index()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,6 +388,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-call", action="store_true")
     ap.add_argument("--recall-queries", type=int, default=512)
+    ap.add_argument("--no-hier", action="store_true",
+                    help="skip the hierarchical leg (device ifit of a 100k x 768 clustered corpus + its queries)")
+    ap.add_argument("--hier-n", type=int, default=100_000)
     ap.add_argument("--pmc-file", default=None,
                     help="PMC summary (scripts/pmc_summary.py) of the filter kernel; default: the newest "
                          "profiles/pmc_rNN_fgemm.json whose workload matches this run")
@@ -458,6 +563,15 @@ def main():
         mem["device_used_after_per_call"] = dev_used()
         mem["peak_sampled"] = max(mem["peak_sampled"], mem["device_used_after_per_call"])
 
+    hier = None
+    if rank == 0 and world == 1 and not args.no_hier:
+        log(f"hierarchical leg: device ifit of {args.hier_n} x 768 clustered rows + queries ...")
+        try:
+            hier = hier_leg(pkg, n=args.hier_n)
+        except Exception as e:            # recorded, never hides the headline line
+            hier = {"error": repr(e)}
+        torch.cuda.empty_cache()
+
     base = None
     if Xh is not None:
         log(f"cpu baseline: {args.cpu_sample} queries (all threads) + {args.cpu_sample_1t} (1 thread) ...")
@@ -499,6 +613,7 @@ def main():
                                       "per_query_hbm_roof_qps": round(PEAK_HBM_GBS * 1e9 / bytes_q, 1),
                                       "qps_over_that_roof": round(qps / world * bytes_q / (PEAK_HBM_GBS * 1e9), 3)},
             "per_call": pc,
+            "hier": hier,
             "recall@10": {"vs_flat_l2": rec_l2, "vs_flat_ip": rec_ip, "target_in_top10": rec_tgt,
                           "n_queries": n_rec,
                           # N(0,I) data: inner product and L2 rank differently (|x|^2 varies by

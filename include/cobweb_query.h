@@ -108,10 +108,17 @@ int cwq_index_info(const cwq_index* idx, int64_t* out8);
 
 /* How the filters centre their rows (no reference counterpart: a property of this
  * index's bf16 filter operands): out[0] = 1 when isotropic rows are stored centred at
- * their depth-1 ancestor's mean (clustered trees, cwq_group.hip; CWQ_GROUP_CENTRE=0 / 1 at
+ * their group centre's mean (clustered trees, cwq_group.hip; CWQ_GROUP_CENTRE=0 / 1 at
  * index creation: off / on wherever it applies), out[1] = groups, out[2] = group-centred
  * rows, out[3] = 1 when the per-call int8 panel was built. */
 int cwq_index_filter_info(const cwq_index* idx, int64_t* out4);
+
+/* The tree-adaptive cut the index chose (no reference counterpart): out[0] =
+ * groups (centre nodes; 0: none planned), out[1] = top nodes (the root and the centres'
+ * ancestors, computed exactly by every pruned query), out[2] = the deepest centre's depth,
+ * out[3] = groups whose rows qualify for centring at their centre.  CWQ_GROUP_CUT=1 at index
+ * creation keeps the depth-1 cut. */
+int cwq_index_cut_info(const cwq_index* idx, int64_t* out4);
 
 /*
  * "Cobweb Fast" batched top-k (A6).  Replaces CobwebWrapper.cobweb_predict_indexed

@@ -131,6 +131,13 @@ struct cwq_index {
   bool grp_mode = false;
   int G = 0;
   int64_t n_grp_rows = 0;
+  // the cut plan_groups chose (host copies, build_prune reads them): the group of every
+  // internal node (-1: a top node -- the root and the ancestors of the group centres, which
+  // every query computes exactly), each group's centre (internal id) and whether its rows are
+  // centred there (grp_ok; a group that fails the centring rule is still a pruning group)
+  std::vector<int> cut_gint, cut_centre;
+  std::vector<char> cut_ok;
+  int cut_maxdep = 0, cut_top = 0;   // deepest centre, number of top nodes (filter_info)
   float* grp_c = nullptr;
   int* grp_par = nullptr;
   double *grp_F = nullptr, *grp_Fc = nullptr;
@@ -139,11 +146,16 @@ struct cwq_index {
   // per-group bound constants.  prune_ctr: the last call's stage-B pair count (diagnostics).
   bool prune_ok = false;
   int *prn_gint = nullptr, *gi_ptr = nullptr, *gi_nodes = nullptr;
+  // top nodes in BFS order (root first) with their parents' list positions and depths; per
+  // group the list position of its centre's parent (a top node)
+  int *top_nodes = nullptr, *top_ppos = nullptr, *top_dep = nullptr, *grp_tpos = nullptr;
+  int n_top = 0, top_maxdep = 0;
   // auto mode's record of the filter on this index: queries filtered / re-run exactly; when
   // at least 9 in 10 of >= 256 queries had to be re-run (the bounds too loose for this
   // tree's rows), auto mode takes the exact scan from then on (same results, less work)
   int64_t filt_q = 0, filt_fb = 0;
   bool filt_auto_off = false;
+  int filt_off_calls = 0;   // auto-mode Fast calls on the exact scan since the filter went off
   // categorize: the last call's queries all went to the two-level replay, so the next call
   // launches the second list with the first replay (gated on its status) instead of after
   // reading that status back (categorize_impl)
@@ -154,7 +166,7 @@ struct cwq_index {
   // again every kCatCountRetry calls)
   int cat_count_idle = 0;
   int prn_gmax = 1;   // the most internal nodes of one pruning group
-  int prn_maxdep = 0;   // deepest internal node of any group
+  int prn_maxdep = 0, prn_mindep = 1;   // deepest / shallowest internal node of any group
   int *gi_dep = nullptr, *gi_ppos = nullptr;   // per group-list entry: depth, the parent's list position
   int* blk_grp = nullptr;   // per 16-row block of isotropic rows: the pruning group of all its rows (-1: mixed)
   int *gs_ptr = nullptr, *gs_rows = nullptr;   // per group: up to 64 usable isotropic rows (the seed threshold)
@@ -373,13 +385,32 @@ float round_up_f(double v) {
 
 // bf16 operands, fp32 rerank copy, per-row and per-tile bound constants, and the
 // strided threshold sample of the isotropic rows.
-// Group-centred rows (cwq_group.hip): which isotropic rows get centred at their depth-1
-// internal ancestor's mean.  A group qualifies when every one of its rows is at most twice
-// as far from the group mean as from the root mean (then the rounding terms stay within the
-// bound's eps and beta margins) and all rows of each of its parents share the key coefficients (the
-// group term is folded into the parent's prefix); the mode is on when the qualifying
-// groups cut the rows' summed squared norms at least 4x (CWQ_GROUP_CENTRE=0 / 1: off /
-// every qualifying group).  rgrp[r] = group index or -1.
+// Group-centred rows and the pruning cut (cwq_group.hip, cwq_prune.hip).
+// A cut is a set of internal nodes, the group centres, such that every internal node lies in
+// exactly one centre's subtree (its group) or is an ancestor of centres (a top node; the root
+// is always one).  A group's rows -- the isotropic rows whose parent is in the group -- are
+// centred at the centre's mean when every one of them is at most twice as far from it as
+// from the root mean (then the rounding terms stay within the bound's eps and beta margins)
+// and all rows of each of its parents share the key coefficients (the group term is folded
+// into the parent's prefix): the group is "ok".  The rows of the other groups, and the rows
+// whose parent is a top node, stay root-centred; every group is still a pruning group.
+//
+// The cut is tree-adaptive: a DP over the internal tree (children before parents) minimises
+// the rows' summed squared norms as stored -- an ok group's rows at their centre, the rest at
+// the root -- plus a penalty lam per group and per top node:
+//   best(c) = min( centre at c:  cost(c) + lam,
+//                  split c:      (rows directly below c, at the root) + sum best(internal child) + lam )
+// A broad root child spanning many clusters (a 500k x 768 ifit tree: 37 root children over
+// 500 clusters) is split down to its cluster-level nodes; a tight one stays one group.  A
+// centre below depth 1 needs >= kCutMinRows isotropic rows (or none): the seed threshold
+// takes the K-th best of a group's sample rows.  Centres are at depth <= 8
+// (CWQ_GROUP_MAXDEP); lam = 64 x the mean squared root norm of a row (CWQ_GROUP_LAMBDA
+// scales the 64), doubled while the cut has more than kCutMaxGroups groups or kCutMaxTop
+// top nodes.  CWQ_GROUP_CUT=1 keeps the round-4 cut (every depth-1 node a centre).  The
+// mode is on when the centred rows cut the summed squared norms at least 4x
+// (CWQ_GROUP_CENTRE=0 / 1: off / on whenever they shrink).  rgrp[r] = the group a row is
+// centred at, or -1.
+constexpr int kCutMinRows = 64, kCutMaxGroups = 4096, kCutMaxTop = kPruneMaxTop;
 int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const std::vector<RowMeta>& meta,
                 const std::vector<int>& row_par, const std::vector<int64_t>& int_nodes, const std::vector<int>& par_int,
                 std::vector<int>& rgrp, hipStream_t s) {
@@ -389,56 +420,132 @@ int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const s
   const char* ge = getenv("CWQ_GROUP_CENTRE");
   const int force = ge && *ge ? atoi(ge) : -1;
   if (force == 0 || NI < 2 || NLi == 0) return CWQ_OK;
-  // group of every internal node: its depth-1 ancestor (internal ids are BFS: parents first)
-  std::vector<int> gint(NI, -1);
-  std::vector<int64_t> gnode;
+  std::vector<int> idep(NI, 0);
+  int maxdep_all = 0;
   for (int i = 1; i < NI; ++i) {
-    if (par_int[i] == 0) {
-      gint[i] = (int)gnode.size();
-      gnode.push_back(int_nodes[i]);
-    } else if (par_int[i] > 0) {
-      gint[i] = gint[par_int[i]];
-    }
+    idep[i] = idep[par_int[i]] + 1;   // BFS internal ids: the parent first
+    maxdep_all = std::max(maxdep_all, idep[i]);
   }
-  const int G = (int)gnode.size();
-  if (G == 0) return CWQ_OK;
-  std::vector<int> cand(NLi, -1);
-  for (int r = 0; r < NLi; ++r) cand[r] = row_par[r] > 0 ? gint[row_par[r]] : -1;
-  int64_t* d_gnode = nullptr;
-  int* d_cand = nullptr;
-  float* cent = nullptr;
-  double *r2 = nullptr, *g2 = nullptr;
-  if ((rc = ix->upload(&d_gnode, gnode, s)) || (rc = ix->upload(&d_cand, cand, s)) ||
-      (rc = ix->alloc(&cent, (size_t)G * D)) || (rc = ix->alloc(&r2, NLi)) || (rc = ix->alloc(&g2, NLi)))
+  const char* ec = getenv("CWQ_GROUP_CUT");
+  const bool depth1 = ec && *ec && atoi(ec) == 1;
+  const char* em = getenv("CWQ_GROUP_MAXDEP");
+  const int maxd = depth1 ? 1 : std::max(1, std::min(maxdep_all, em && *em && atoi(em) > 0 ? atoi(em) : 8));
+  const int W = maxd + 1;
+  // per row: the squared norm centred at the root ([0]) and at each ancestor of depth 1..maxd
+  int *d_rpar = nullptr, *d_pint = nullptr, *d_idep = nullptr;
+  int64_t* d_inodes = nullptr;
+  double* d_dist = nullptr;
+  if ((rc = ix->upload(&d_rpar, row_par, s)) || (rc = ix->upload(&d_pint, par_int, s)) ||
+      (rc = ix->upload(&d_idep, idep, s)) || (rc = ix->upload(&d_inodes, int_nodes, s)) ||
+      (rc = ix->alloc(&d_dist, (size_t)NLi * W)))
     return rc;
-  HIPCHK(launch_gather_rows_f32(mean, D, d_gnode, G, cent, s));
-  HIPCHK(launch_group_norms(mean, D, d_rows, NLi, ix->iso_c, cent, d_cand, r2, g2, s));
-  std::vector<double> hr2(NLi), hg2(NLi);
-  HIPCHK(hipMemcpyAsync(hr2.data(), r2, (size_t)NLi * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hg2.data(), g2, (size_t)NLi * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(launch_group_anc_dist(mean, D, d_rows, NLi, ix->iso_c, d_rpar, d_pint, d_idep, d_inodes, maxd, d_dist, s));
+  std::vector<double> dist((size_t)NLi * W);
+  HIPCHK(hipMemcpyAsync(dist.data(), d_dist, dist.size() * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  std::vector<char> gok(G, 1);
+  // per internal node: the rows below it -- their squared norms centred at its mean (depth <=
+  // maxd) and at the root, their count, and whether they qualify for centring at it; the
+  // rows directly below it at the root
+  std::vector<double> cost(NI, 0.0), rsub(NI, 0.0), rdir(NI, 0.0);
+  std::vector<int64_t> nrow(NI, 0);
+  std::vector<char> ok(NI, 1);
   std::vector<float> pcw(NI, NAN), piv(NI, NAN), pinvL(NI, NAN);
+  std::vector<char> pbad(NI, 0);
+  double sum_root = 0.0;
   for (int r = 0; r < NLi; ++r) {
-    const int g = cand[r];
-    if (g < 0) continue;
-    if (!(hg2[r] <= 4.0 * hr2[r])) gok[g] = 0;   // |M_g| <= 2 |M_0|: the rounding cross term stays in eps
+    const double r0 = dist[(size_t)r * W];
+    sum_root += r0;
     const int p = row_par[r];
+    if (p < 0) continue;
+    rdir[p] += r0;
     if (std::isnan(pcw[p])) {
       pcw[p] = meta[r].cw;
       piv[p] = meta[r].iv;
       pinvL[p] = meta[r].invL;
     } else if (pcw[p] != meta[r].cw || piv[p] != meta[r].iv || pinvL[p] != meta[r].invL) {
-      gok[g] = 0;
+      pbad[p] = 1;
+    }
+    for (int a = p; a > 0; a = par_int[a]) {
+      rsub[a] += r0;
+      nrow[a]++;
+      if (idep[a] <= maxd) {
+        const double v = dist[(size_t)r * W + idep[a]];
+        cost[a] += v;
+        if (!(v <= 4.0 * r0)) ok[a] = 0;   // |M_g| <= 2 |M_0|: the rounding cross term stays in eps
+      }
     }
   }
-  double sum_root = 0.0, sum_sel = 0.0;
-  for (int r = 0; r < NLi; ++r) {
-    sum_root += hr2[r];
-    sum_sel += (cand[r] >= 0 && gok[cand[r]]) ? hg2[r] : hr2[r];
+  for (int p = 1; p < NI; ++p)
+    if (pbad[p])
+      for (int a = p; a > 0; a = par_int[a]) ok[a] = 0;
+  std::vector<int> kptr(NI + 1, 0), kids(NI > 0 ? NI - 1 : 0);
+  for (int i = 1; i < NI; ++i) kptr[par_int[i] + 1]++;
+  for (int i = 0; i < NI; ++i) kptr[i + 1] += kptr[i];
+  {
+    std::vector<int> fill(kptr.begin(), kptr.end() - 1);
+    for (int i = 1; i < NI; ++i) kids[fill[par_int[i]]++] = i;
   }
+  const char* el = getenv("CWQ_GROUP_LAMBDA");
+  double lam = (el && *el ? atof(el) : 64.0) * sum_root / NLi;
+  std::vector<double> best(NI);
+  std::vector<char> centre(NI, 0);
+  std::vector<int> gint(NI, -1);
+  std::vector<int64_t> gnode;
+  std::vector<int> gcent;
+  int ntop = 0;
+  for (int it = 0; it < 64; ++it, lam = lam > 0.0 ? 2.0 * lam : 1.0) {
+    for (int c = NI - 1; c >= 1; --c) {
+      double cc = INFINITY, sp = INFINITY;
+      if (idep[c] == 1 || nrow[c] == 0 || nrow[c] >= kCutMinRows) cc = (ok[c] ? cost[c] : rsub[c]) + lam;
+      if (idep[c] < maxd && kptr[c + 1] > kptr[c]) {
+        sp = rdir[c] + lam;
+        for (int j = kptr[c]; j < kptr[c + 1]; ++j) sp += best[kids[j]];
+      }
+      centre[c] = cc <= sp ? 1 : 0;
+      best[c] = std::min(cc, sp);
+    }
+    // top-down: group ids in BFS order of the centres
+    gnode.clear();
+    gcent.clear();
+    ntop = 1;
+    for (int i = 1; i < NI; ++i) {
+      const int p = par_int[i];
+      if (gint[p] >= 0) {   // inside p's group
+        gint[i] = gint[p];
+      } else if (centre[i]) {   // p is a top node (the root, or split): i a centre ...
+        gint[i] = (int)gnode.size();
+        gnode.push_back(int_nodes[i]);
+        gcent.push_back(i);
+      } else {   // ... or a top node itself
+        gint[i] = -1;
+        ++ntop;
+      }
+    }
+    if ((int)gnode.size() <= kCutMaxGroups && ntop <= kCutMaxTop) break;
+  }
+  const int G = (int)gnode.size();
+  if (G == 0 || G > kCutMaxGroups || ntop > kCutMaxTop) return CWQ_OK;
+  std::vector<char> gok(G, 0);
+  for (int g = 0; g < G; ++g) gok[g] = ok[gcent[g]];
+  std::vector<int> cand(NLi, -1);
+  double sum_sel = 0.0;
+  for (int r = 0; r < NLi; ++r) {
+    cand[r] = row_par[r] >= 0 ? gint[row_par[r]] : -1;
+    const int g = cand[r];
+    sum_sel += (g >= 0 && gok[g]) ? dist[(size_t)r * W + idep[gcent[g]]] : dist[(size_t)r * W];
+  }
+  ix->cut_gint = gint;
+  ix->cut_centre = gcent;
+  ix->cut_ok = gok;
+  ix->cut_top = ntop;
+  ix->cut_maxdep = 0;
+  for (int c : gcent) ix->cut_maxdep = std::max(ix->cut_maxdep, idep[c]);
   const bool on = force == 1 ? sum_sel < sum_root : sum_sel * 4.0 <= sum_root;
   if (!on) return CWQ_OK;
+  int64_t* d_gnode = nullptr;
+  float* cent = nullptr;
+  if ((rc = ix->upload(&d_gnode, gnode, s)) || (rc = ix->alloc(&cent, (size_t)G * D))) return rc;
+  HIPCHK(launch_gather_rows_f32(mean, D, d_gnode, G, cent, s));
   for (int r = 0; r < NLi; ++r) {
     rgrp[r] = (cand[r] >= 0 && gok[cand[r]]) ? cand[r] : -1;
     ix->n_grp_rows += rgrp[r] >= 0;
@@ -621,7 +728,8 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
     // cluster passed the filter (C2 ifit tree: ~1,100 candidates per query, overflowing
     // the record buffers).  Add kPerGroup rows of every group, spread over its rows
     // (distinct rows only: T must bound the K-th best key over distinct rows).
-    constexpr int kPerGroup = 64;
+    // (fewer per group on a deep cut: the sample stays within 32,768 rows)
+    const int kPerGroup = std::max(8, std::min(64, (32768 - (int)srow.size()) / std::max(1, ix->G)));
     std::vector<std::vector<int>> gr(ix->G);
     for (int64_t r = 0; r < NLi; ++r)
       if (rgrp[r] >= 0) gr[rgrp[r]].push_back((int)r);
@@ -650,12 +758,14 @@ int build_filter(cwq_index* ix, const float* mean, const int64_t* d_rows, const 
   return CWQ_OK;
 }
 
-// Group pruning constants (cwq_prune.hip).  Groups are the subtrees of the
-// depth-1 internal nodes; members are their internal nodes and the leaf-class rows below
-// them (a row that is itself an internal node belongs to that node's group).  Needs the
-// group-centred mode (group centres), the row-major A/B copies (exact pass of a group), and
-// every level weight and row weight >= 0 (the key bound adds upper bounds of lp' with
-// non-negative coefficients).  CWQ_GROUP_PRUNE=0 at index creation leaves it off.
+// Group pruning constants (cwq_prune.hip).  Groups are plan_groups' cut:
+// a group's members are the internal nodes of its centre's subtree and the leaf-class rows
+// below them (a row that is itself an internal node belongs to that node's group); the top
+// nodes (the root and the centres' ancestors) belong to no group and every query computes
+// them exactly (prune_head_kernel).  Needs the group-centred mode (group centres), the
+// row-major A/B copies (exact pass of a group), and every level weight and row weight >= 0
+// (the key bound adds upper bounds of lp' with non-negative coefficients).
+// CWQ_GROUP_PRUNE=0 at index creation leaves it off.
 int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::vector<int64_t>& int_nodes,
                 const std::vector<int>& par_int, const std::vector<float>& w_int, const std::vector<int64_t>& rows,
                 const std::vector<int>& int_id, const std::vector<RowMeta>& meta, const std::vector<int>& row_par,
@@ -668,12 +778,29 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     if (!(w >= 0.f)) return CWQ_OK;
   for (int r = 0; r < NL; ++r)
     if (!(meta[r].cw >= 0.f) || !(meta[r].invL >= 0.f)) return CWQ_OK;
-  // pruning group of every internal node: its depth-1 ancestor (plan_groups' numbering)
-  std::vector<int> gint(NI, -1);
-  int ng = 0;
-  for (int i = 1; i < NI; ++i) gint[i] = par_int[i] == 0 ? ng++ : (par_int[i] > 0 ? gint[par_int[i]] : -1);
-  if (ng != G) return CWQ_OK;   // plan_groups numbers the same depth-1 nodes
-  // members: internal nodes 1.., then rows
+  // pruning group of every internal node (plan_groups' cut; -1: a top node)
+  const std::vector<int>& gint = ix->cut_gint;
+  if ((int)gint.size() != NI || (int)ix->cut_centre.size() != G) return CWQ_OK;
+  // top nodes, BFS order: their parents are top nodes too (a cut)
+  std::vector<int> tnodes, tpos(NI, -1), tpp, tdep;
+  std::vector<int> idep(NI, 0);
+  for (int i = 1; i < NI; ++i) idep[i] = idep[par_int[i]] + 1;
+  for (int i = 0; i < NI; ++i) {
+    if (gint[i] >= 0) continue;
+    const int p = i == 0 ? -1 : par_int[i];
+    if (p >= 0 && tpos[p] < 0) return CWQ_OK;   // never: the parent of a top node is a top node
+    tpos[i] = (int)tnodes.size();
+    tnodes.push_back(i);
+    tpp.push_back(p >= 0 ? tpos[p] : -1);
+    tdep.push_back(idep[i]);
+  }
+  std::vector<int> gtpos(G);
+  for (int g = 0; g < G; ++g) {
+    const int c = ix->cut_centre[g];
+    if (gint[c] != g || tpos[par_int[c]] < 0) return CWQ_OK;   // never: a centre's parent is a top node
+    gtpos[g] = tpos[par_int[c]];
+  }
+  // members: internal nodes 1.. (top nodes: no group), then rows
   std::vector<int64_t> mnode;
   std::vector<float> miv;
   std::vector<int> mgrp;
@@ -685,7 +812,7 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   std::vector<int> rgrp(NL, -1);
   for (int r = 0; r < NL; ++r) {
     const int own = int_id[rows[r]];
-    rgrp[r] = own >= 0 ? gint[own] : (row_par[r] > 0 ? gint[row_par[r]] : -1);
+    rgrp[r] = own >= 0 ? gint[own] : (row_par[r] >= 0 ? gint[row_par[r]] : -1);
     mnode.push_back(rows[r]);
     miv.push_back(r < ix->NL_iso ? meta[r].iv : 0.f);
     mgrp.push_back(rgrp[r]);
@@ -729,14 +856,17 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     b.ldmin = std::min(b.ldmin, ld);
     b.ldabs = std::max(b.ldabs, std::fabs(ld));
   }
-  // the key coefficients of the usable rows: 1/L and C = invL * sum_{path, a != root} w_a + cw
-  std::vector<double> wsum(NI, 0.0);   // sum of w over the path of internal node i, the root excluded
-  for (int i = 1; i < NI; ++i) wsum[i] = wsum[par_int[i]] + (double)w_int[i];
+  // the key coefficients of the usable rows: 1/L and C = invL * sum_{a in path, a in g} w_a + cw
+  // (the path's top nodes -- the root down to the centre's parent t_g -- are P(t_g), exact)
+  std::vector<double> wsum(NI, 0.0);   // sum of w over the path of internal node i within its group
+  for (int i = 1; i < NI; ++i)
+    if (gint[i] >= 0) wsum[i] = (gint[par_int[i]] == gint[i] ? wsum[par_int[i]] : 0.0) + (double)w_int[i];
   for (int r = 0; r < NL; ++r) {
     const int g = rgrp[r];
     if (g < 0 || !(row_flags[r] & FLAG_HAS_SENT)) continue;
     GroupBound& b = gb[g];
-    const double iL = meta[r].invL, C = iL * (row_par[r] > 0 ? wsum[row_par[r]] : 0.0) + (double)meta[r].cw;
+    const int rp = row_par[r];
+    const double iL = meta[r].invL, C = iL * (rp >= 0 && gint[rp] == g ? wsum[rp] : 0.0) + (double)meta[r].cw;
     b.iLmin = std::min(b.iLmin, iL);
     b.iLmax = std::max(b.iLmax, iL);
     b.Cmin = std::min(b.Cmin, C * (1.0 - 0x1p-40));
@@ -764,20 +894,25 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
     if (gint[i] >= 0) gnodes[fillp[gint[i]]++] = i;
   ix->prn_gmax = 1;
   for (int g = 0; g < G; ++g) ix->prn_gmax = std::max(ix->prn_gmax, gptr[g + 1] - gptr[g]);
-  if ((size_t)ix->prn_gmax * 4 + (size_t)64 * (ix->DP / 16 + 1) * 4 > (size_t)144 * 1024) return CWQ_OK;   // LDS
-  // per list entry: depth (root 0) and the parent's position in the same list (the lists are
-  // BFS-ordered, so a level is finished before the next starts)
-  std::vector<int> idep(NI, 0), lpos(NI, -1), gdep(gnodes.size()), gpp(gnodes.size());
-  for (int i = 1; i < NI; ++i) idep[i] = par_int[i] >= 0 ? idep[par_int[i]] + 1 : 0;
+  // LDS of the seed and stage-B kernels (their group-prefix arrays grow with the largest group)
+  if (prune_lds_max(ix->DP, ix->prn_gmax) > kPruneLdsCap) return CWQ_OK;
+  // per list entry: depth (root 0) and the parent's position in the same list (-1: the
+  // centre, whose parent is a top node; the lists are BFS-ordered, so a level is finished
+  // before the next starts)
+  std::vector<int> lpos(NI, -1), gdep(gnodes.size()), gpp(gnodes.size());
   for (size_t j = 0; j < gnodes.size(); ++j) lpos[gnodes[j]] = (int)j;
   ix->prn_maxdep = 0;
+  ix->prn_mindep = INT32_MAX;
   for (size_t j = 0; j < gnodes.size(); ++j) {
     const int i = gnodes[j], p = par_int[i];
     gdep[j] = idep[i];
-    gpp[j] = p > 0 ? lpos[p] : -1;
+    const bool inner = gint[p] == gint[i];
+    gpp[j] = inner ? lpos[p] : -1;
     ix->prn_maxdep = std::max(ix->prn_maxdep, idep[i]);
-    if (p > 0 && (gint[p] != gint[i] || lpos[p] >= (int)j)) return CWQ_OK;   // never: a group is a subtree in BFS order
+    ix->prn_mindep = std::min(ix->prn_mindep, idep[i]);
+    if (inner ? lpos[p] >= (int)j : i != ix->cut_centre[gint[i]]) return CWQ_OK;   // never: a group is a subtree in BFS order
   }
+  if (ix->prn_mindep == INT32_MAX) ix->prn_mindep = 1;
   if (gdep.empty()) {
     gdep.push_back(0);
     gpp.push_back(-1);
@@ -805,6 +940,12 @@ int build_prune(cwq_index* ix, const float* mean, const VarSrc& var, const std::
   }
   if ((rc = ix->upload(&ix->blk_grp, bg, s))) return rc;
   if ((rc = ix->upload(&ix->gi_dep, gdep, s)) || (rc = ix->upload(&ix->gi_ppos, gpp, s))) return rc;
+  ix->n_top = (int)tnodes.size();
+  ix->top_maxdep = 0;
+  for (int d : tdep) ix->top_maxdep = std::max(ix->top_maxdep, d);
+  if ((rc = ix->upload(&ix->top_nodes, tnodes, s)) || (rc = ix->upload(&ix->top_ppos, tpp, s)) ||
+      (rc = ix->upload(&ix->top_dep, tdep, s)) || (rc = ix->upload(&ix->grp_tpos, gtpos, s)))
+    return rc;
   if ((rc = ix->upload(&ix->prn_gint, gint, s)) || (rc = ix->upload(&ix->gi_ptr, gptr, s)) ||
       (rc = ix->upload(&ix->gi_nodes, gnodes, s)) || (rc = ix->upload(&ix->gbound, gb, s)) ||
       (rc = ix->alloc(&ix->prune_ctr, 8)))
@@ -1179,6 +1320,17 @@ extern "C" int cwq_index_filter_info(const cwq_index* idx, int64_t* o) {
   return CWQ_OK;
 }
 
+extern "C" int cwq_index_cut_info(const cwq_index* idx, int64_t* o) {
+  if (!idx || !o) return fail(CWQ_ERR_ARG, "NULL argument");
+  o[0] = (int64_t)idx->cut_centre.size();
+  o[1] = idx->cut_centre.empty() ? 0 : idx->cut_top;
+  o[2] = idx->cut_maxdep;
+  int64_t n_ok = 0;
+  for (char c : idx->cut_ok) n_ok += c ? 1 : 0;
+  o[3] = n_ok;
+  return CWQ_OK;
+}
+
 // Scan configuration of one query call (cwq_kernels.hip scan_cfg_begin): fixed from the
 // call's total query count, so every chunk and workspace estimate of the call agrees.
 struct ScanCfgScope {
@@ -1287,6 +1439,13 @@ int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipS
   pa.gi_dep = ix->gi_dep;
   pa.gi_ppos = ix->gi_ppos;
   pa.gmaxdep = ix->prn_maxdep;
+  pa.gmindep = ix->prn_mindep;
+  pa.top_nodes = ix->top_nodes;
+  pa.top_ppos = ix->top_ppos;
+  pa.top_dep = ix->top_dep;
+  pa.n_top = ix->n_top;
+  pa.top_maxdep = ix->top_maxdep;
+  pa.grp_tpos = ix->grp_tpos;
   if (live) {   // the per-call filter's live block list (count in ctr[5])
     pa.blk_grp = ix->blk_grp;
     pa.nblk = ((int64_t)ix->NL_iso + 15) / 16;
@@ -1745,12 +1904,28 @@ bool use_filter(const cwq_index* ix, int k, int min_rows = kFiltMinRows, bool fa
   return mode == 1;
 }
 
-// After a Fast call (cwq_last_stats' record): the auto-mode filter record of the index.
+// After a Fast call (cwq_last_stats' record): the auto-mode filter record of the index.  The
+// exact-scan choice is not for good: after kFiltRetryCalls auto-mode Fast calls on the exact
+// scan the record starts afresh and the filter is tried again (an early query mix that
+// defeated the bounds costs speed for a while, never for the index's life).
+constexpr int kFiltRetryCalls = 64;
 void note_filter(cwq_index* ix) {
-  if (ix->stats[2] == 0 || ix->stats[0] <= 0 || ix->filter >= 0) return;
+  if (ix->filter >= 0) return;
+  if (ix->stats[2] == 0) {
+    if (ix->filt_auto_off && ++ix->filt_off_calls >= kFiltRetryCalls) {
+      ix->filt_auto_off = false;
+      ix->filt_q = ix->filt_fb = 0;
+      ix->filt_off_calls = 0;
+    }
+    return;
+  }
+  if (ix->stats[0] <= 0) return;
   ix->filt_q += ix->stats[0];
   ix->filt_fb += ix->stats[1];
-  if (ix->filt_q >= 256 && ix->filt_fb * 10 >= ix->filt_q * 9) ix->filt_auto_off = true;
+  if (ix->filt_q >= 256 && ix->filt_fb * 10 >= ix->filt_q * 9) {
+    ix->filt_auto_off = true;
+    ix->filt_off_calls = 0;
+  }
 }
 
 // fgemm launch geometry: query groups over the 8 XCDs (each keeps its query panel in
@@ -2583,6 +2758,9 @@ extern "C" int cwq_set_filter(cwq_index* ix, int mode) {
   if (!ix) return fail(CWQ_ERR_ARG, "NULL index");
   if (mode < -1 || mode > 1) return fail(CWQ_ERR_ARG, "mode must be -1, 0 or 1");
   ix->filter = mode;
+  ix->filt_q = ix->filt_fb = 0;   // a fresh auto-mode record
+  ix->filt_auto_off = false;
+  ix->filt_off_calls = 0;
   return CWQ_OK;
 }
 

@@ -77,6 +77,52 @@ hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, in
   return hipGetLastError();
 }
 
+// The tree-adaptive cut (cwq_api.hip plan_groups): per isotropic row (one wave), |fl(mu_r -
+// c0)|^2 (out[r][0]) and |fl(mu_r - mu_a)|^2 for each internal ancestor a of the row at depth
+// 1..maxd (out[r][depth(a)]; -1: no ancestor at that depth), in fp64 -- the squared norms of
+// the row centred at the root or at a, as rows_prep would store it.  rpar: the row's parent
+// (internal id); a row is below every ancestor of its parent.
+__global__ void group_anc_dist_kernel(const float* __restrict__ mean, int D, const int64_t* __restrict__ rows,
+                                      int64_t n, const float* __restrict__ c0, const int* __restrict__ rpar,
+                                      const int* __restrict__ par_int, const int* __restrict__ idep,
+                                      const int64_t* __restrict__ int_nodes, int maxd, double* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int W = maxd + 1;   // [0]: the root centre c0, [d]: the ancestor at depth d
+  if (lane == 0)
+    for (int j = 1; j < W; ++j) out[r * W + j] = -1.0;
+  const float* mr = mean + rows[r] * (int64_t)D;
+  double s0 = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float u = mr[d] - c0[d];
+    s0 += (double)u * (double)u;
+  }
+  for (int off = 32; off > 0; off >>= 1) s0 += __shfl_xor(s0, off, 64);
+  if (lane == 0) out[r * W] = s0;
+  for (int a = rpar[r]; a > 0; a = par_int[a]) {
+    const int da = idep[a];
+    if (da > maxd) continue;
+    const float* ma = mean + int_nodes[a] * (int64_t)D;
+    double s = 0.0;
+    for (int d = lane; d < D; d += 64) {
+      const float u = mr[d] - ma[d];
+      s += (double)u * (double)u;
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) out[r * W + da] = s;
+  }
+}
+
+hipError_t launch_group_anc_dist(const float* mean, int D, const int64_t* rows, int64_t n, const float* c0,
+                                 const int* rpar, const int* par_int, const int* idep, const int64_t* int_nodes,
+                                 int maxd, double* out, hipStream_t s) {
+  if (n <= 0 || maxd <= 0) return hipSuccess;
+  hipLaunchKernelGGL(group_anc_dist_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, mean, D, rows, n, c0,
+                     rpar, par_int, idep, int_nodes, maxd, out);
+  return hipGetLastError();
+}
+
 // sh[q][g] = -2 x'.d_g in fp64 (x' = fl(x - c0) exactly as query_prep forms it; d_g = c_g - c0
 // in fp64, exact).  One wave per (query, group).  she[q][g] bounds the fp64 evaluation error
 // of sh: products rounded once, ceil(D/64) sequential adds per lane, 6 butterfly levels, so

@@ -210,10 +210,14 @@ struct PruneArgs {
   const float* cent;
   const float* Ar; const float* Br;   // row-major fp32 A, B of the internal nodes [NI][DP]
   const int* par_int; const float* w_int; const float* logdet_int;
-  const int* gint;              // pruning group of each internal node (-1: the root)
+  const int* gint;              // pruning group of each internal node (-1: a top node)
   const int* gi_ptr; const int* gi_nodes;   // group-major internal node lists (BFS order)
   const int* gi_dep; const int* gi_ppos;    // per list entry: tree depth, the parent's list position (-1: the root)
-  int gmaxdep;                              // deepest internal node of any group
+  int gmaxdep, gmindep;                     // deepest / shallowest internal node of any group
+  // top nodes (no group: the root and the centres' ancestors), BFS order, computed exactly by
+  // the head kernel for every query; per group the top-list position of its centre's parent
+  const int* top_nodes; const int* top_ppos; const int* top_dep; int n_top, top_maxdep;
+  const int* grp_tpos;
   const GroupBound* gb;
   double* kpart;                // [2][nq][G]: P0-free part of KUB, and the margin's magnitude term
   float* S; float* P;           // [nq][ldS]
@@ -239,6 +243,11 @@ struct PruneArgs {
 // pass (many workgroups per query), seed (g*'s prefixes and tables, T, stage-B pairs, sentinel
 // fill), stage B (the pairs' exact passes)
 hipError_t launch_prune(const PruneArgs& a, int cus, bool first, hipStream_t s);
+constexpr int kPruneMaxTop = 1024;                   // top nodes the head kernel holds in LDS
+constexpr size_t kPruneLdsCap = (size_t)150 * 1024;  // the seed / stage-B kernels' dynamic LDS
+size_t prune_lds_max(int DP, int gmax);
+// a kernel's dynamic-LDS attribute raised to `bytes` once per (kernel, device), thread-safe
+hipError_t ensure_dyn_lds(const void* fn, size_t bytes);
 hipError_t launch_raise_threshold(float* T, int64_t ldT, const float* Tfloor, int nq, hipStream_t s);
 hipError_t launch_prune_members(const float* mean, const VarSrc& var, int D, const int64_t* nodes, const float* iv,
                                 const int* grp, const float* cent, int64_t n, double4* out, hipStream_t s);
@@ -765,6 +774,9 @@ hipError_t launch_rows_prep(const float* mean, int D, const int64_t* nodes, int6
 // Group-centred filter rows (cwq_group.hip)
 hipError_t launch_gather_rows_f32(const float* mean, int D, const int64_t* nodes, int64_t n, float* out,
                                   hipStream_t s);
+hipError_t launch_group_anc_dist(const float* mean, int D, const int64_t* rows, int64_t n, const float* c0,
+                                 const int* rpar, const int* par_int, const int* idep, const int64_t* int_nodes,
+                                 int maxd, double* out, hipStream_t s);
 hipError_t launch_group_norms(const float* mean, int D, const int64_t* nodes, int64_t n, const float* c0,
                               const float* cent, const int* grp, double* root2, double* grp2, hipStream_t s);
 // sh [2][nq][G]: -2 x'.d_g and its error bound; dist2 (optional) [nq][G]: |x - c_g|^2 in fp64

@@ -1815,14 +1815,8 @@ hipError_t launch_skip_failed(int* status, const int* okf, int nq, int init, hip
 
 hipError_t launch_simulate_two(const SimArgs& a, hipStream_t s) {
   if (a.R != 64 || a.NI <= 0 || !a.T2 || !a.lkey2 || !a.par_int) return hipErrorInvalidValue;
-  static bool attr = false;   // dynamic LDS above the 64 KiB default
-  const size_t lds = (size_t)kTwoArena * (sizeof(HeapEnt) + sizeof(TwoRec));
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&simulate_two_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  const size_t lds = (size_t)kTwoArena * (sizeof(HeapEnt) + sizeof(TwoRec));   // above the 64 KiB default
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simulate_two_kernel), lds)) return e;
   hipLaunchKernelGGL(simulate_two_kernel, dim3((unsigned)a.nq), dim3(64), lds, s, a);
   return hipGetLastError();
 }

@@ -29,6 +29,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "cwq_internal.h"
 
@@ -107,18 +109,18 @@ __device__ __forceinline__ void prune_write_tables(const PruneArgs& a, int q, in
 
 // The prefixes and tables of group g's internal nodes for query q, level by level down the
 // group's BFS-ordered list: P(i) = fmaf(w_i, lp'(i), P(parent)) with the parent's P from LDS
-// (s_P[position - gi_ptr[g]]; the root's P0 from P[q][0]) -- internal_chain_kernel's
+// (s_P[position - gi_ptr[g]]; the centre's parent's P, a top node's, from P) -- internal_chain_kernel's
 // top-down chain, the same values, without walking every node's chain from the root.  nt threads; the raw
 // sums S of the group's nodes must be complete and visible.
 __device__ __forceinline__ void prune_group_prefixes(const PruneArgs& a, int q, int g, float* s_P, int nt) {
   const int b0 = a.gi_ptr[g], b1 = a.gi_ptr[g + 1];
-  const float P0 = a.P[(size_t)q * a.ldS];
-  for (int L = 1; L <= a.gmaxdep; ++L) {
+  const float Pt = a.P[(size_t)q * a.ldS + a.top_nodes[a.grp_tpos[g]]];   // the centre's parent (head kernel)
+  for (int L = a.gmindep; L <= a.gmaxdep; ++L) {
     for (int j = b0 + (int)threadIdx.x; j < b1; j += nt) {
       if (a.gi_dep[j] != L) continue;
       const int node = a.gi_nodes[j], pp = a.gi_ppos[j];
       const float lp = -0.5f * (a.logdet_int[node] + a.S[(size_t)q * a.ldS + node]);
-      const float P = fmaf(a.w_int[node], lp, pp < 0 ? P0 : s_P[pp - b0]);
+      const float P = fmaf(a.w_int[node], lp, pp < 0 ? Pt : s_P[pp - b0]);
       s_P[j - b0] = P;
       prune_write_tables(a, q, node, P);
     }
@@ -133,7 +135,7 @@ __device__ __forceinline__ void prune_group_prefixes(const PruneArgs& a, int q, 
 //   >= (1 - 2^-16) (sqrt(wmin) dlo - 2^-23 sqrt(wmax) mmax)_+^2 (t = x A - B with B = fl(mu
 //   A), the partial sums' relative error < 64 * 2^-24); lp'_fp32 = fl(-0.5 fl(logdet + S))
 //   <= -logdet/2 + 2^-22 |logdet| - (1/2 - 2^-22) S_fp32 = UB; |lp'| <= mag.
-// xs / c0s: the query and the root centre (LDS copies in the head kernel).
+// xs / c0s: the query and the root centre (prune_terms_kernel: global, L2-resident).
 __device__ __forceinline__ void prune_group_terms(const PruneArgs& a, const float* xs, const float* c0s, int64_t qi, int g,
                                                   int lane) {
   double d1 = 0.0, ab = 0.0, e2 = 0.0;
@@ -242,57 +244,82 @@ size_t prune_pair_lds(int DP, int gmax) {
   return ((size_t)DP + (size_t)kPrChunk * (DP / 16 + 1) + (size_t)gmax) * 4;
 }
 
-// Head, one workgroup per query: every group's bound terms (one wave per group,
-// prune_group_terms); the root's raw sum (exact_aniso_S's arithmetic, bit for bit), its
-// prefix P0 and the root's tables; KUB[q][g] = max(iLmin P0, iLmax P0) + kpart + 2^-16 (iLmax
-// |P0| + Cmax mag) (the exact key's fp32 chain: <= 64 fmaf steps and the final fmaf, < 2^-17
-// of its terms), rounded up; g* = argmax (ties: the smaller g).  Block 0 zeroes the pair and
-// claim counters (and the call's total on its first pruned chunk).
-constexpr int kHdThreads = 512;
+// Every (query, group) pair's bound terms, one wave each over the whole chip
+// (prune_group_terms: the group shift, |x - c_g|^2, the Pt-free part of KUB) -- before the
+// head, so a call of one query spreads its G waves over many CUs.
+__global__ void prune_terms_kernel(const PruneArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (w >= (int64_t)a.nq * a.G) return;
+  const int q = (int)(w / a.G), g = (int)(w % a.G);
+  prune_group_terms(a, a.q + (int64_t)q * a.D, a.c0, q, g, lane);
+}
+
+// Head, one workgroup per query: the top nodes' raw sums (every (node, 16-dim slice) partial
+// in parallel, one thread per node adding them in slice order: the scan's sums bit for bit)
+// and their prefixes level by level (internal_chain_kernel's chain: the root's w lp', then
+// fmaf(w, lp', P(parent))) with their tables; from the bound terms (prune_terms_kernel) KUB[q][g] = max(iLmin Pt, iLmax Pt) + kpart + 2^-16 (iLmax |Pt| + Cmax
+// mag), Pt = P(t_g) the exact prefix of the centre's parent (the rest of the key's fp32 chain:
+// <= 64 fmaf steps and the final fmaf, < 2^-17 of its terms), rounded up; g* = argmax (ties:
+// the smaller g).  Block 0 zeroes the pair and claim counters (and the call's total on its
+// first pruned chunk).
+constexpr int kHdThreads = 512, kHdChunk = 32;
 __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs a) {
-  __shared__ float s_root[128];   // DP <= 2048
-  __shared__ float s_xq[2048], s_c0[2048];   // the query and the root centre (D <= DP <= 2048)
-  __shared__ float s_p0;
+  __shared__ float s_x[2048];                // the query's padded slices (DP <= 2048)
+  __shared__ float s_tp[kHdChunk * 129];     // partials of a chunk of top nodes [kHdChunk][NV16 + 1]
+  __shared__ float s_St[kPruneMaxTop], s_Pt[kPruneMaxTop];   // the top nodes' raw sums and prefixes
   __shared__ double s_best[kHdThreads / 64];
   __shared__ int s_bg[kHdThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
-  const int NV16 = a.DP / 16;
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
   if (q == 0 && tid < 6 && (tid != 4 || a.zero_total)) a.ctr[tid] = 0;
-  // the root: 16-dim partials in parallel (added in slice order by thread 0 below)
-  const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
-  if (tid < NV16) {
-    const int v = tid;
-    float part;
+  prune_load_query(a, q, s_x, kHdThreads);
+  __syncthreads();
+  for (int c0 = 0; c0 < a.n_top; c0 += kHdChunk) {
+    const int cnt = min(kHdChunk, a.n_top - c0);
+    for (int it = tid; it < cnt * NV16; it += kHdThreads) {
+      const int e = it / NV16, v = it - e * NV16;
+      const int node = a.top_nodes[c0 + e];
+      const float* __restrict__ ar = a.Ar + (size_t)node * a.DP + v * 16;
+      const float* __restrict__ br = a.Br + (size_t)node * a.DP + v * 16;
+      float4 a4[4], b4[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float tt = fmaf(xq[(size_t)v * kXQ * 16 + j], a.Ar[v * 16 + j], -a.Br[v * 16 + j]);
-      part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+      for (int j = 0; j < 4; ++j) {
+        a4[j] = *reinterpret_cast<const float4*>(ar + j * 4);
+        b4[j] = *reinterpret_cast<const float4*>(br + j * 4);
+      }
+      float part;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float4 ta = a4[j >> 2], tb = b4[j >> 2];
+        const float aj = (j & 3) == 0 ? ta.x : (j & 3) == 1 ? ta.y : (j & 3) == 2 ? ta.z : ta.w;
+        const float bj = (j & 3) == 0 ? tb.x : (j & 3) == 1 ? tb.y : (j & 3) == 2 ? tb.z : tb.w;
+        const float tt = fmaf(s_x[v * 16 + j], aj, -bj);
+        part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+      }
+      s_tp[e * LDP + v] = part;
     }
-    s_root[v] = part;
+    __syncthreads();
+    if (tid < cnt) {
+      float acc = 0.f;
+      for (int v = 0; v < NV16; ++v) acc += s_tp[tid * LDP + v];
+      a.S[(size_t)q * a.ldS + a.top_nodes[c0 + tid]] = acc;
+      s_St[c0 + tid] = acc;
+    }
+    __syncthreads();
   }
-  for (int d = tid; d < a.D; d += kHdThreads) {
-    s_xq[d] = a.q[(int64_t)q * a.D + d];
-    s_c0[d] = a.c0[d];
+  for (int L = 0; L <= a.top_maxdep; ++L) {   // BFS list: a level's parents are finished first
+    for (int j = tid; j < a.n_top; j += kHdThreads) {
+      if (a.top_dep[j] != L) continue;
+      const int node = a.top_nodes[j], pp = a.top_ppos[j];
+      const float lp = -0.5f * (a.logdet_int[node] + s_St[j]);
+      const float P = pp < 0 ? a.w_int[node] * lp : fmaf(a.w_int[node], lp, s_Pt[pp]);
+      s_Pt[j] = P;
+      prune_write_tables(a, q, node, P);
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int g = wave; g < a.G; g += kHdThreads / 64) prune_group_terms(a, s_xq, s_c0, q, g, lane);
-  __syncthreads();
-  if (tid == 0) {
-    float acc = 0.f;
-    for (int v = 0; v < NV16; ++v) acc += s_root[v];
-    a.S[(size_t)q * a.ldS] = acc;
-    const float lp = -0.5f * (a.logdet_int[0] + acc);
-    const float P0 = a.w_int[0] * lp;
-    s_p0 = P0;
-    const size_t o = (size_t)q * a.ldS;
-    a.P[o] = P0;
-    a.Plo[o] = P0;
-    a.Phi[o] = P0;
-  }
-  __threadfence();   // the waves' kpart stores, read back by other waves below
-  __syncthreads();
-  const double P0 = (double)s_p0;
   double best = -INFINITY;
   int bg = 0x7fffffff;
   for (int g = tid; g < a.G; g += kHdThreads) {
@@ -300,8 +327,9 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
     const size_t o = (size_t)q * a.G + g;
     double kub = -INFINITY;
     if (b.valid) {
-      kub = fmax(b.iLmin * P0, b.iLmax * P0) + a.kpart[o] +
-            0x1p-16 * (b.iLmax * fabs(P0) + a.kpart[(size_t)a.nq * a.G + o]);
+      const double Pt = (double)s_Pt[a.grp_tpos[g]];
+      kub = fmax(b.iLmin * Pt, b.iLmax * Pt) + a.kpart[o] +
+            0x1p-16 * (b.iLmax * fabs(Pt) + a.kpart[(size_t)a.nq * a.G + o]);
       if (kub > best || (kub == best && g < bg)) {
         best = kub;
         bg = g;
@@ -440,7 +468,7 @@ __global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArg
     if (t >= (int64_t)a.nq * a.NI) return;
     const int q = (int)(t / a.NI), i = (int)(t % a.NI);
     const int g = a.gint[i];
-    if (i == 0 || (g >= 0 && g == a.gstar[q])) return;
+    if (g < 0 || g == a.gstar[q]) return;   // top nodes (the head's) and g*'s
     const size_t o = (size_t)q * a.ldS + i;
     a.Plo[o] = kPruneSent;
     a.Phi[o] = kPruneSent;
@@ -561,14 +589,30 @@ __global__ __launch_bounds__(kPrThreads) void prune_stage_b_kernel(const PruneAr
 }
 
 // A kernel's dynamic-LDS limit raised to `bytes` when that passes the 64 KiB default (and
-// what was set before): the attribute is only ever set to a size the launch requests, which
-// with the kernel's static LDS stays within the 160 KiB of a CU.
-static hipError_t lds_attr(const void* fn, size_t bytes, size_t& cur) {
-  if (bytes <= (size_t)64 * 1024 || bytes <= cur) return hipSuccess;
+// what was set before for that kernel on the current device): the attribute is only ever set
+// to a size the launch requests, which with the kernel's static LDS stays within the 160 KiB
+// of a CU.  One process-wide table under a mutex: calls on different index handles (each
+// serialised by its own mutex only) may launch the same kernels concurrently.
+hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
+  if (bytes <= (size_t)64 * 1024) return hipSuccess;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> cur;
+  std::lock_guard<std::mutex> lk(mu);
+  size_t& c = cur[{fn, dev}];
+  if (bytes <= c) return hipSuccess;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess) cur = bytes;
+  if (e == hipSuccess) c = bytes;
   else (void)hipGetLastError();   // not left as the runtime's sticky error for the next caller
   return e;
+}
+
+// The seed and stage-B kernels' dynamic LDS for a largest group of gmax internal nodes
+// (build_prune keeps pruning off when it passes kPruneLdsCap).
+size_t prune_lds_max(int DP, int gmax) {
+  const size_t seed = ((size_t)64 * (DP / 16 + 1) + (size_t)gmax) * 4;
+  return std::max(seed, prune_pair_lds(DP, gmax));
 }
 
 // The whole pruned internal pass of a chunk: head, g*'s pass, seed (+ fill), stage B.
@@ -576,17 +620,20 @@ static hipError_t lds_attr(const void* fn, size_t bytes, size_t& cur) {
 // pruned chunk.
 hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s) {
   if (a0.nq <= 0) return hipSuccess;
-  if (a0.DP % 16 || a0.DP / 16 > 128 || a0.gnodes_max < 1) return hipErrorInvalidValue;
+  if (a0.DP % 16 || a0.DP / 16 > 128 || a0.gnodes_max < 1 || a0.n_top < 1 || a0.n_top > kPruneMaxTop ||
+      prune_lds_max(a0.DP, a0.gnodes_max) > kPruneLdsCap)
+    return hipErrorInvalidValue;
   PruneArgs a = a0;
   a.zero_total = first ? 1 : 0;
+  const int64_t npg = (int64_t)a.nq * a.G;
+  hipLaunchKernelGGL(prune_terms_kernel, dim3((unsigned)((npg + 3) / 4)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(prune_head_kernel, dim3((unsigned)a.nq), dim3(kHdThreads), 0, s, a);
   int gmin = kGgMinQ;
   if (const char* e = getenv("CWQ_PRUNE_GROUPED_MIN")) gmin = atoi(e) > 0 ? atoi(e) : kGgMinQ;
   if (a.nq >= gmin) {   // a batch: per (group, node chunk), the group's queries together
     const int nbg = (a.gnodes_max + kGgNodes - 1) / kGgNodes;
     const size_t lds = ((size_t)(2 * kGgNodes + 1) * a.DP + (size_t)kGgNodes * (a.DP / 16 + 1) + kGgWin) * 4;
-    static size_t attr = 0;   // dynamic LDS above the 64 KiB default (DP > 768)
-    if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_gstar_grouped_kernel), lds, attr)) return e;
+    if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&prune_gstar_grouped_kernel), lds)) return e;
     hipLaunchKernelGGL(prune_gstar_grouped_kernel, dim3((unsigned)((int64_t)a.G * nbg)), dim3(kGgThreads), lds, s, a,
                        nbg);
   } else {   // a few queries: per (query, node chunk)
@@ -595,11 +642,10 @@ hipError_t launch_prune(const PruneArgs& a0, int cus, bool first, hipStream_t s)
                        ((size_t)a.DP + (size_t)kGsNodes * (a.DP / 16 + 1)) * 4, s, a, nb);
   }
   // the group-prefix LDS of a large group can pass the 64 KiB default
-  static size_t attr_seed = 0, attr_b = 0;
   const size_t lds_seed = ((size_t)64 * (a.DP / 16 + 1) + (size_t)a.gnodes_max) * 4;
   const size_t lds_b = prune_pair_lds(a.DP, a.gnodes_max);
-  if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_seed_kernel), lds_seed, attr_seed)) return e;
-  if (hipError_t e = lds_attr(reinterpret_cast<const void*>(&prune_stage_b_kernel), lds_b, attr_b)) return e;
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&prune_seed_kernel), lds_seed)) return e;
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&prune_stage_b_kernel), lds_b)) return e;
   const int64_t nfill = ((int64_t)a.nq * a.NI + kSeedThreads - 1) / kSeedThreads;
   hipLaunchKernelGGL(prune_seed_kernel, dim3((unsigned)(a.nq + nfill)), dim3(kSeedThreads), lds_seed, s, a);
   const int64_t nw = (int64_t)a.nq * a.G;

@@ -603,13 +603,9 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
 
 template <int MODE, int MQB, bool I8 = false, int CH = SK_CH>
 static hipError_t launch_one(const StreamArgs& a, int n_wg, size_t lds, hipStream_t s) {
-  static bool attr = false;   // dynamic LDS above the 64 KiB default
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStreamMaxLds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  // dynamic LDS above the 64 KiB default (once per kernel and device, thread-safe)
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH>), kStreamMaxLds))
+    return e;
   hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH>), dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
   return hipGetLastError();
 }

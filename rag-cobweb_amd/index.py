@@ -154,6 +154,14 @@ class CobwebIndex:
         return {"group_centred": bool(out[0]), "groups": int(out[1]), "group_rows": int(out[2]),
                 "int8_panel": bool(out[3])}
 
+    def cut_info(self):
+        """The tree-adaptive cut (cwq_index_cut_info): groups, top nodes (computed exactly by
+        every pruned query), the deepest centre, groups whose rows are centred."""
+        out = np.zeros(4, np.int64)
+        check(self._L.cwq_index_cut_info(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"groups": int(out[0]), "top_nodes": int(out[1]), "max_centre_depth": int(out[2]),
+                "centred_groups": int(out[3])}
+
     def set_timing(self, enable=True):
         check(self._L.cwq_set_timing(self._h, int(bool(enable))))
 

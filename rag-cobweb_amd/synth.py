@@ -38,6 +38,22 @@ def synthetic_queries(X, nq, seed=1, frac_perturbed=0.5, sigma=0.1):
     return torch.cat([pert, fresh]).contiguous(), targets
 
 
+def clustered_corpus(n, dim, n_clusters, nq, seed=2):
+    """Config C2's stand-in corpus (numpy, host): n rows in n_clusters Gaussian clusters
+    (centres N(0, 4I), spread 0.3) and nq queries, half perturbed corpus rows (+0.1 N(0, I);
+    `pick` = their rows), half fresh draws around the cluster centres.  The corpus of
+    tests/test_gpu_c2.py, scripts/c2_probe.py and bench.py's hierarchical leg; the tree over
+    it is built by the drop-in's own device ifit (a real Cobweb hierarchy, not synthesised)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    C = rng.standard_normal((n_clusters, dim)).astype(np.float32) * 2.0
+    X = (C[rng.integers(0, n_clusters, n)] + 0.3 * rng.standard_normal((n, dim))).astype(np.float32)
+    pick = rng.choice(n, nq // 2, replace=False)
+    Qp = X[pick] + 0.1 * rng.standard_normal((nq // 2, dim))
+    Qf = C[rng.integers(0, n_clusters, nq - nq // 2)] + 0.3 * rng.standard_normal((nq - nq // 2, dim))
+    return X, np.concatenate([Qp, Qf]).astype(np.float32), pick
+
+
 def _var_of(count, meanSq):
     # CobwebTorchTree.compute_var: meanSq / count + prior_var (fp32 division then add)
     return meanSq / count[:, None] + float(PRIOR_VAR)

@@ -22,16 +22,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cobweb_pkg  # noqa: E402
 
 
-def corpus(n, d, nc, nq, seed=2):
-    rng = np.random.default_rng(seed)
-    C = rng.standard_normal((nc, d)).astype(np.float32) * 2.0
-    X = (C[rng.integers(0, nc, n)] + 0.3 * rng.standard_normal((n, d))).astype(np.float32)
-    pick = rng.choice(n, nq // 2, replace=False)
-    Qp = X[pick] + 0.1 * rng.standard_normal((nq // 2, d))
-    Qf = C[rng.integers(0, nc, nq - nq // 2)] + 0.3 * rng.standard_normal((nq - nq // 2, d))
-    return X, np.concatenate([Qp, Qf]).astype(np.float32), pick
-
-
 def med(f, reps):
     ts = []
     for _ in range(reps):
@@ -72,7 +62,7 @@ def main():
                          "final_wide phase stamps and simulate_two cycle counts of a few one-query calls")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
-    X, Qn, pick = corpus(args.n, args.dim, args.clusters, args.nq)
+    X, Qn, pick = pkg.synth.clustered_corpus(args.n, args.dim, args.clusters, args.nq)
     random.seed(2)
     w0 = pkg.CobwebWrapper(corpus=None, corpus_embeddings=X[:8])   # warm up libcwq
     w0.build_prediction_index()
@@ -117,7 +107,7 @@ def main():
         print(f"saved the tree structure to {args.save_struct}", flush=True)
     inf = ix.info
     root_c = int((np.load(args.load_struct)['parent'] == 0).sum()) if args.load_struct else len(w.tree.root.children)
-    print(f"filter rows: {ix.filter_info()}", flush=True)
+    print(f"filter rows: {ix.filter_info()}; cut: {ix.cut_info()}", flush=True)
     print(f"C2 corpus {args.n}x{args.dim} ({args.clusters} clusters): " +
           ("tree structure loaded, batch-Welford stats " if args.load_struct else "") + f"device ifit {t_fit:.2f} s "
           f"({args.n / max(t_fit, 1e-9):.0f} inserts/s); tree {inf['n_nodes']} nodes, {inf['internal_nodes']} internal, "
