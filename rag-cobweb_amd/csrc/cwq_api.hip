@@ -401,16 +401,15 @@ float round_up_f(double v) {
 //   best(c) = min( centre at c:  cost(c) + lam,
 //                  split c:      (rows directly below c, at the root) + sum best(internal child) + lam )
 // A broad root child spanning many clusters (a 500k x 768 ifit tree: 37 root children over
-// 500 clusters) is split down to its cluster-level nodes; a tight one stays one group.  A
-// centre below depth 1 needs >= kCutMinRows isotropic rows (or none): the seed threshold
-// takes the K-th best of a group's sample rows.  Centres are at depth <= 8
-// (CWQ_GROUP_MAXDEP); lam = 64 x the mean squared root norm of a row (CWQ_GROUP_LAMBDA
-// scales the 64), doubled while the cut has more than kCutMaxGroups groups or kCutMaxTop
-// top nodes.  CWQ_GROUP_CUT=1 keeps the round-4 cut (every depth-1 node a centre).  The
+// 500 clusters) is split down to its cluster-level nodes; a tight one stays one group (in
+// high dimension splitting a Gaussian cluster saves ~1/D of its norms, far below lam).
+// Centres are at depth <= 8 (CWQ_GROUP_MAXDEP); lam = the mean squared root norm of a row
+// (CWQ_GROUP_LAMBDA scales it), doubled while the cut has more than kCutMaxGroups groups or
+// kCutMaxTop top nodes.  CWQ_GROUP_CUT=1 keeps the round-4 cut (every depth-1 node a centre).  The
 // mode is on when the centred rows cut the summed squared norms at least 4x
 // (CWQ_GROUP_CENTRE=0 / 1: off / on whenever they shrink).  rgrp[r] = the group a row is
 // centred at, or -1.
-constexpr int kCutMinRows = 64, kCutMaxGroups = 4096, kCutMaxTop = kPruneMaxTop;
+constexpr int kCutMaxGroups = 4096, kCutMaxTop = kPruneMaxTop;
 int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const std::vector<RowMeta>& meta,
                 const std::vector<int>& row_par, const std::vector<int64_t>& int_nodes, const std::vector<int>& par_int,
                 std::vector<int>& rgrp, hipStream_t s) {
@@ -486,7 +485,7 @@ int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const s
     for (int i = 1; i < NI; ++i) kids[fill[par_int[i]]++] = i;
   }
   const char* el = getenv("CWQ_GROUP_LAMBDA");
-  double lam = (el && *el ? atof(el) : 64.0) * sum_root / NLi;
+  double lam = (el && *el ? atof(el) : 1.0) * sum_root / NLi;
   std::vector<double> best(NI);
   std::vector<char> centre(NI, 0);
   std::vector<int> gint(NI, -1);
@@ -496,7 +495,7 @@ int plan_groups(cwq_index* ix, const float* mean, const int64_t* d_rows, const s
   for (int it = 0; it < 64; ++it, lam = lam > 0.0 ? 2.0 * lam : 1.0) {
     for (int c = NI - 1; c >= 1; --c) {
       double cc = INFINITY, sp = INFINITY;
-      if (idep[c] == 1 || nrow[c] == 0 || nrow[c] >= kCutMinRows) cc = (ok[c] ? cost[c] : rsub[c]) + lam;
+      cc = (ok[c] ? cost[c] : rsub[c]) + lam;
       if (idep[c] < maxd && kptr[c + 1] > kptr[c]) {
         sp = rdir[c] + lam;
         for (int j = kptr[c]; j < kptr[c + 1]; ++j) sp += best[kids[j]];
@@ -1381,7 +1380,7 @@ bool use_prune(const cwq_index* ix) {
   const char* e = getenv("CWQ_GROUP_PRUNE");
   return !(e && *e && atoi(e) == 0);
 }
-size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 28 + 16 : 0; }
+size_t prune_bytes_per_query(const cwq_index* ix) { return ix->prune_ok ? (size_t)ix->G * 36 + 16 : 0; }
 
 // The pruned Fast chunk's internal pass, in place of run_internal + group_tables (four
 // launches, cwq_prune.hip): the group shifts, the bound terms, the root, KUB and g* (head);
@@ -1413,7 +1412,7 @@ int prune_internal(cwq_index* ix, Chunk& c, const float* q, int K, Bump& b, hipS
   pa.gi_ptr = ix->gi_ptr;
   pa.gi_nodes = ix->gi_nodes;
   pa.gb = ix->gbound;
-  pa.kpart = b.take<double>((size_t)2 * c.nq_pad * G);
+  pa.kpart = b.take<double>((size_t)3 * c.nq_pad * G);
   pa.S = c.S_int;
   pa.P = c.P;
   pa.Plo = c.Pg_lo;

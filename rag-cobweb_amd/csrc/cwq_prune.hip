@@ -161,7 +161,7 @@ __device__ __forceinline__ void prune_group_terms(const PruneArgs& a, const floa
   a.sh[o] = -2.0 * d1;
   a.sh[(size_t)a.nq * a.G + o] = 2.0 * ab * ((double)(a.D / 64 + 8) * 0x1.02p-53);
   const GroupBound b = a.gb[g];
-  double kp = -INFINITY, m2 = 0.0;
+  double kp = -INFINITY, m2 = 0.0, kp0 = -INFINITY;
   if (b.valid) {
     // e2: exact differences, squares and fp64 sums: relative error < 2^-40
     const double dist_lo = sqrt(e2 * (1.0 - 0x1p-40)) * (1.0 - 0x1p-50);
@@ -174,9 +174,15 @@ __device__ __forceinline__ void prune_group_terms(const PruneArgs& a, const floa
     const double mag = 0.5 * (b.ldabs + (1.0 + 0x1p-16) * shv * shv) * (1.0 + 0x1p-20);
     kp = fmax(b.Cmin * UB, b.Cmax * UB);
     m2 = b.Cmax * mag;
+    // the same bound at the centre itself (r_g = 0): not a bound of the group, a point
+    // estimate that ranks the groups for g* (a loose broad group has the largest KUB yet is
+    // rarely where the top-K lies)
+    const double s0 = sqrt(b.wmin) * dist_lo;
+    kp0 = fmax(b.Cmin, b.Cmax) * (-0.5 * b.ldmin - 0.5 * s0 * s0);
   }
   a.kpart[o] = kp;
   a.kpart[(size_t)a.nq * a.G + o] = m2;
+  a.kpart[(size_t)2 * a.nq * a.G + o] = kp0;
 }
 
 // S of cnt nodes of a group's list from position c0, for query q (its slices in s_x): every
@@ -260,8 +266,9 @@ __global__ void prune_terms_kernel(const PruneArgs a) {
 // and their prefixes level by level (internal_chain_kernel's chain: the root's w lp', then
 // fmaf(w, lp', P(parent))) with their tables; from the bound terms (prune_terms_kernel) KUB[q][g] = max(iLmin Pt, iLmax Pt) + kpart + 2^-16 (iLmax |Pt| + Cmax
 // mag), Pt = P(t_g) the exact prefix of the centre's parent (the rest of the key's fp32 chain:
-// <= 64 fmaf steps and the final fmaf, < 2^-17 of its terms), rounded up; g* = argmax (ties:
-// the smaller g).  Block 0 zeroes the pair and claim counters (and the call's total on its
+// <= 64 fmaf steps and the final fmaf, < 2^-17 of its terms), rounded up; g* = the group
+// whose centre point scores best among those with >= K seed rows (any group will do for the
+// threshold: its K rows' exact keys are <= tau_K; a good one prunes the most).  Block 0 zeroes the pair and claim counters (and the call's total on its
 // first pruned chunk).
 constexpr int kHdThreads = 512, kHdChunk = 32;
 __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs a) {
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
   __shared__ float s_tp[kHdChunk * 129];     // partials of a chunk of top nodes [kHdChunk][NV16 + 1]
   __shared__ float s_St[kPruneMaxTop], s_Pt[kPruneMaxTop];   // the top nodes' raw sums and prefixes
   __shared__ double s_best[kHdThreads / 64];
-  __shared__ int s_bg[kHdThreads / 64];
+  __shared__ int s_bg[kHdThreads / 64], s_bt[kHdThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x;
   const int NV16 = a.DP / 16, LDP = NV16 + 1;
@@ -320,18 +327,27 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
     }
     __syncthreads();
   }
+  // g*: the group whose centre scores best (kpart[2], the bound at the centre point) among
+  // the groups with >= K sample rows (the seed threshold needs K of them); none of those: the
+  // best KUB.  Order: (tier, score, smaller g).
   double best = -INFINITY;
-  int bg = 0x7fffffff;
+  int bt = -1, bg = 0x7fffffff;
+  auto better = [](int t1, double s1, int g1, int t2, double s2, int g2) {
+    return t1 != t2 ? t1 > t2 : (s1 != s2 ? s1 > s2 : g1 < g2);
+  };
   for (int g = tid; g < a.G; g += kHdThreads) {
     const GroupBound b = a.gb[g];
     const size_t o = (size_t)q * a.G + g;
     double kub = -INFINITY;
     if (b.valid) {
       const double Pt = (double)s_Pt[a.grp_tpos[g]];
-      kub = fmax(b.iLmin * Pt, b.iLmax * Pt) + a.kpart[o] +
-            0x1p-16 * (b.iLmax * fabs(Pt) + a.kpart[(size_t)a.nq * a.G + o]);
-      if (kub > best || (kub == best && g < bg)) {
-        best = kub;
+      const double pt = fmax(b.iLmin * Pt, b.iLmax * Pt);
+      kub = pt + a.kpart[o] + 0x1p-16 * (b.iLmax * fabs(Pt) + a.kpart[(size_t)a.nq * a.G + o]);
+      const int tier = a.gs_ptr[g + 1] - a.gs_ptr[g] >= a.K ? 1 : 0;
+      const double sc = tier ? pt + a.kpart[(size_t)2 * a.nq * a.G + o] : kub;
+      if (better(tier, sc, g, bt, best, bg)) {
+        bt = tier;
+        best = sc;
         bg = g;
       }
     }
@@ -339,21 +355,25 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
   }
   for (int off = 32; off > 0; off >>= 1) {
     const double ob = __shfl_xor(best, off, 64);
+    const int ot = __shfl_xor(bt, off, 64);
     const int og = __shfl_xor(bg, off, 64);
-    if (ob > best || (ob == best && og < bg)) {
+    if (better(ot, ob, og, bt, best, bg)) {
       best = ob;
+      bt = ot;
       bg = og;
     }
   }
   if (lane == 0) {
     s_best[wave] = best;
+    s_bt[wave] = bt;
     s_bg[wave] = bg;
   }
   __syncthreads();
   if (tid == 0) {
     for (int w = 1; w < kHdThreads / 64; ++w)
-      if (s_best[w] > best || (s_best[w] == best && s_bg[w] < bg)) {
+      if (better(s_bt[w], s_best[w], s_bg[w], bt, best, bg)) {
         best = s_best[w];
+        bt = s_bt[w];
         bg = s_bg[w];
       }
     a.gstar[q] = bg == 0x7fffffff ? -1 : bg;

@@ -57,6 +57,10 @@ def main():
     ap.add_argument("--load-struct", default=None,
                     help="skip ifit: the tree structure from a --save-struct file, node statistics by batch "
                          "Welford over the same corpus (synth.tree_synth) -- the same shape for the query legs")
+    ap.add_argument("--index-env", default=None,
+                    help="';'-separated variants of '&'-separated KEY=VAL set at index creation (e.g. "
+                         "'CWQ_GROUP_CUT=1;' = the depth-1 cut, then the default): the index is rebuilt from "
+                         "the same fitted tree under each and the query legs rerun")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic builds (CWQ_LIB=a -DCWQ_STAMP=1 variant): after the Basic per-call leg, "
                          "final_wide phase stamps and simulate_two cycle counts of a few one-query calls")
@@ -131,6 +135,23 @@ def main():
         basic_legs(args, w, ix, Q, Qn, k)
     if args.env_ab:
         env_ab(args, w, ix, Q, Qn, k)
+    if args.index_env is not None and not args.load_struct:
+        for v in args.index_env.split(";"):
+            env = dict(kv.split("=", 1) for kv in v.split("&") if kv.strip())
+            w._invalidate_prediction_index()
+            os.environ.update(env)
+            t0 = time.perf_counter()
+            w.build_prediction_index()
+            torch.cuda.synchronize()
+            for key in env:
+                os.environ.pop(key, None)
+            ix = w._index
+            print(f"-- index rebuilt under {env or 'default'} ({time.perf_counter() - t0:.2f} s): filter rows "
+                  f"{ix.filter_info()}; cut {ix.cut_info()}", flush=True)
+            if not args.basic_only:
+                fast_legs(args, w, ix, Q, Qn, pick, k)
+            if not args.fast_only:
+                basic_legs(args, w, ix, Q, Qn, k)
     print("done", flush=True)
 
 
