@@ -3386,9 +3386,14 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     if (redo.empty()) continue;
     ix->cat_tail_done = false;   // the DENSE re-run below writes after the last flag gather
 
-    // DENSE re-run: every leaf row materialised for the hard queries (exact by construction).
+    // DENSE re-run: the exact heap replay of the hard queries (exact by construction).  By
+    // default lazily (simulate_lazy_kernel: a popped node's leaf rows scored when their
+    // parent is popped); CWQ_CAT_LAZY=0: every leaf row materialised first by the exact scan.
+    const char* lze = getenv("CWQ_CAT_LAZY");
+    const bool lazy = !(lze && *lze && atoi(lze) == 0) && ix->DP <= 2048;
+    const int64_t ldL = lazy ? 1 : std::max(ix->NL, 1);
     const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
-    const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ix->NL * 4 +
+    const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ldL * 4 +
                          (size_t)cap_dense * 16 + 64 + (size_t)k * 8 + (size_t)ix->D * 4;
     const int64_t sub = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q));
     std::vector<float> hx;
@@ -3397,14 +3402,14 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       const int64_t ns_pad = round_up(ns, kQPad);
       // per hard query: dense keys, heap, then status / nodes[k] / found / calls
       if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) +
-                            (size_t)ns_pad * ((size_t)ix->NL * 4 + cap_dense * 16 + 64 + (size_t)k * 8) + 16 * 256 +
+                            (size_t)ns_pad * ((size_t)ldL * 4 + cap_dense * 16 + 64 + (size_t)k * 8) + 16 * 256 +
                             (size_t)ns_pad * ix->D * 4)))
         return rc;
       Bump b2(ix->ws, ix->ws_size);
       Chunk c2;
       carve_chunk(ix, b2, c2, ns);
       float* qsub = b2.take<float>((size_t)ns * ix->D);
-      float* dense = b2.take<float>((size_t)ns_pad * std::max(ix->NL, 1));
+      float* dense = b2.take<float>((size_t)ns_pad * ldL);
       HeapEnt* heap2 = b2.take<HeapEnt>((size_t)ns_pad * cap_dense);
       int* status2 = b2.take<int>(ns_pad);
       int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
@@ -3418,8 +3423,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(launch_copy_rows(q, ix->D, d_gq, qsub, ix->D, nullptr, ns, ix->D, s));
       HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
       if ((rc = run_internal(ix, c2, s))) return rc;
-      if ((rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1, nullptr,
-                              s)))
+      if (!lazy && (rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1,
+                                       nullptr, s)))
         return rc;
       SimArgs sd = sa;
       sd.pre_status = 0;   // every hard query replays (status2 is fresh scratch)
@@ -3428,7 +3433,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       sd.LPF = c2.LPF ? c2.LPF : ix->dummy;
       sd.BF = c2.BF ? c2.BF : ix->dummy;
       sd.dense_lpf = dense;
-      sd.ldL = std::max(ix->NL, 1);
+      sd.ldL = ldL;
       sd.lkey = okey;
       sd.laux = oaux;
       sd.lrow = orow;
@@ -3438,7 +3443,21 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       sd.n_found = found2;
       sd.n_calls = calls2;
       sd.status = status2;
-      HIPCHK(launch_simulate(sd, s));
+      if (lazy) {
+        sd.X = c2.X;
+        sd.DP = ix->DP;
+        sd.isoM = ix->iso_M;
+        sd.ld_iso = ix->ld_iso;
+        sd.NL_iso = ix->NL_iso;
+        sd.anA = ix->an_A;
+        sd.anB = ix->an_B;
+        sd.ld_an = ix->ld_an;
+        sd.meta = ix->row_meta;
+        sd.dconst = dfull;
+        HIPCHK(launch_simulate_lazy(sd, s));
+      } else {
+        HIPCHK(launch_simulate(sd, s));
+      }
       HIPCHK(launch_copy_rows(nodes2, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_gq, ns, 2 * (int64_t)k, s));
       HIPCHK(launch_copy_rows(found2, 1, nullptr, n_found, 1, d_gq, ns, 1, s));
       if (n_calls) HIPCHK(launch_copy_rows(calls2, 2, nullptr, n_calls, 2, d_gq, ns, 2, s));

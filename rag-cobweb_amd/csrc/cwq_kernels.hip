@@ -1414,6 +1414,123 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
   }
 }
 
+// DENSE replay without materialised leaf keys (§4.7, round 6).  simulate_wave_kernel's
+// dense mode reads every leaf row's full lp from a [nq][NL] table that a whole exact leaf
+// scan fills first -- on a 500k-row tree that scan is most of a hard query's cost, though
+// the search pushes only the children of the nodes it pops (~1,800 log_prob calls per query
+// on the 500k x 768 ifit tree).  Here the wave replays the same heap and, when an internal
+// node is popped, computes the full lp of its leaf-row children on the spot, one row per
+// lane: the scan kernel's arithmetic exactly -- per 16-dim slice t = x - mu (isotropic, mu
+// from the dim-major iso_M: consecutive rows are consecutive addresses) or t = fmaf(x, A,
+// -B) (anisotropic), the slice partial t*t then fmaf(t, t, .), the partials added in slice
+// order from 0, lp by iso_key_tail / the epilogue's expression -- so the keys, and with them
+// the pops, are DENSE mode's bit for bit.  Same pushes in the same order (internal children
+// in child order, then the isotropic and the anisotropic rows in row order), so the heap
+// holds the same entries and pops the same sequence.
+__device__ __forceinline__ float lazy_row_lp(const SimArgs& a, const float* s_x, int r, bool iso) {
+  const int NV16 = a.DP / 16;
+  float acc = 0.f;
+  if (iso) {
+    const float* __restrict__ m = a.isoM + r;
+    for (int v = 0; v < NV16; ++v) {
+      float part;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float t = s_x[v * 16 + j] - m[(size_t)(v * 16 + j) * a.ld_iso];
+        part = (j == 0) ? t * t : fmaf(t, t, part);
+      }
+      acc += part;
+    }
+    float lp;
+    (void)iso_key_tail(acc, a.meta[r], CWQ_INF, lp, 1, a.dconst);
+    return lp;
+  }
+  const int ra = r - a.NL_iso;
+  const float* __restrict__ A = a.anA + ra;
+  const float* __restrict__ B = a.anB + ra;
+  for (int v = 0; v < NV16; ++v) {
+    float part;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const size_t o = (size_t)(v * 16 + j) * a.ld_an;
+      const float t = fmaf(s_x[v * 16 + j], A[o], -B[o]);
+      part = (j == 0) ? t * t : fmaf(t, t, part);
+    }
+    acc += part;
+  }
+  const RowMeta md = a.meta[r];
+  return -0.5f * (md.logdet + a.dconst + acc);
+}
+
+__global__ __launch_bounds__(64) void simulate_lazy_kernel(const SimArgs a) {
+  __shared__ float s_x[2048];   // the query's padded dims (DP <= 2048)
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x;
+  if (q >= a.nq) return;
+  if (a.pre_status && a.status[q] == 0) return;
+  const int NV16 = a.DP / 16;
+  const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+  for (int d = lane; d < a.DP; d += 64) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+  __syncthreads();
+  HeapEnt* h = a.heap + (size_t)q * a.heap_cap;
+  int64_t hn = 0;
+  int found = 0;
+  int64_t calls = 1, visited = 0;
+  if (a.NI > 0) {
+    wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0}, lane);
+  } else {   // single-node tree: the root is leaf row 0
+    const float lp = lazy_row_lp(a, s_x, 0, a.NL_iso > 0);
+    wheap_push(h, hn, HeapEnt{lp, 0.f, a.row_bfs[0], -1}, lane);
+  }
+  while (hn > 0) {
+    const HeapEnt e = wheap_pop(h, hn, lane);
+    ++visited;
+    const bool is_int = e.node >= 0;
+    const int row = is_int ? -1 : -e.node - 1;
+    if (visited >= a.max_nodes) break;
+    const bool has_sent = is_int ? a.int_has_sent[e.node] != 0 : (a.row_flags[row] & FLAG_HAS_SENT) != 0;
+    if (has_sent) {
+      if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+      ++found;
+    }
+    if (found == a.k) break;
+    if (!is_int) continue;
+    const int u = e.node;
+    calls += a.int_nchild[u];
+    wheap_push_children(h, hn, a, q, u, e.score, lane);
+    for (int pass = 0; pass < 2; ++pass) {
+      const int r0 = pass ? a.int_leaf_b0[u] : a.int_leaf_a0[u];
+      const int r1 = pass ? a.int_leaf_b1[u] : a.int_leaf_a1[u];
+      for (int rb = r0; rb < r1; rb += 64) {
+        const int r = rb + lane;
+        const bool in = r < r1;
+        const bool ok = in && !(a.row_flags[r] & FLAG_INT_COPY);
+        const float lp = ok ? lazy_row_lp(a, s_x, r, pass == 0) : 0.f;
+        const int tb = ok ? a.row_bfs[r] : 0;
+        uint64_t bm = __ballot(ok);
+        while (bm) {   // in row order, as the dense replay pushes them
+          const int j = __builtin_ctzll(bm);
+          bm &= bm - 1;
+          wheap_push(h, hn, HeapEnt{__shfl(lp, j, 64), e.score, __shfl(tb, j, 64), -(rb + j + 1)}, lane);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    a.n_found[q] = found < a.k ? found : a.k;
+    if (a.n_calls) a.n_calls[q] = calls;
+    a.status[q] = 0;
+  }
+}
+
+hipError_t launch_simulate_lazy(const SimArgs& a, hipStream_t s) {
+  if (a.R != 0 || !a.X || a.DP <= 0 || a.DP > 2048 || a.DP % 16 || !a.meta || (a.NL_iso > 0 && !a.isoM) ||
+      (a.NL > a.NL_iso && (!a.anA || !a.anB)))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(simulate_lazy_kernel, dim3((unsigned)a.nq), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Two-level replay (§4.7).  A query whose top-R list (lkey, R = 64) ends inside a tie at
 // its last key G -- a group of more than R rows sharing the bottleneck G, e.g. the leaves

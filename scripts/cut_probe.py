@@ -59,6 +59,30 @@ def legs(ix, Q, k, tag):
     os.environ.pop("CWQ_GROUP_PRUNE", None)
 
 
+def basic(ix, Q, k, tag):
+    ref = None
+    for lazy in ("0", "1"):
+        os.environ["CWQ_CAT_LAZY"] = lazy
+        got = ix.categorize(Q, k, 100000)
+        t = med(lambda: ix.categorize(Q, k, 100000), 3)
+        st = ix.last_categorize_stats()
+        ts = []
+        for i in range(16):
+            q = Q[i:i + 1].contiguous()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ix.categorize(q, k, 100000)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        same = ref is None or all(torch.equal(a, b) for a, b in zip(ref, got))
+        ref = ref or got
+        print(f"[{tag}] Basic lazy={lazy} batch {Q.shape[0]}: {t * 1e3:.3f} ms; one query per call median "
+              f"{ts[8] * 1e6:.1f} us; == materialised {same}; calls/query {float(got[2].float().mean()):.0f}; {st}",
+              flush=True)
+    os.environ.pop("CWQ_CAT_LAZY", None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=48000)
@@ -68,9 +92,11 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--nq", type=int, default=256)
     ap.add_argument("--depth1", action="store_true", help="also the depth-1 cut forced on")
+    ap.add_argument("--basic", action="store_true", help="Basic batch / per call, lazy vs materialised DENSE")
+    ap.add_argument("--basic-only", action="store_true")
     args = ap.parse_args()
     pkg = cobweb_pkg.load()
-    fan = tuple(int(x) for x in args.fan.split(","))
+    fan = tuple(int(x) for x in args.fan.replace("x", ",").split(","))
     t, Q = broad_tree(pkg, args.n, args.dim, fan, 62, direct=args.direct, nq=args.nq)
     variants = [("adaptive", {})]
     if args.depth1:
@@ -81,7 +107,10 @@ def main():
         for key in env:
             os.environ.pop(key, None)
         print(f"[{tag}] cut {ix.cut_info()} filter {ix.filter_info()} info {ix.info}", flush=True)
-        legs(ix, Q, args.k, tag)
+        if not args.basic_only:
+            legs(ix, Q, args.k, tag)
+        if args.basic:
+            basic(ix, Q, args.k, tag)
         ix.close()
 
 

@@ -47,7 +47,7 @@ for step in "$@"; do
       tail -1 gpurun_out/${TAG}_bench.log ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
-          python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --recall-queries 0 > gpurun_out/${TAG}_prof.log 2>&1 \
+          python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-hier --recall-queries 0 > gpurun_out/${TAG}_prof.log 2>&1 \
           || { tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
       tail -1 gpurun_out/${TAG}_prof.log ;;
     tl:*)

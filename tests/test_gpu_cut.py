@@ -194,3 +194,32 @@ def test_cut_forced_depth1_matches(gpu, monkeypatch):
     assert torch.equal(ida, idd) and torch.equal(sa, sd)
     ixa.close()
     ixd.close()
+
+
+def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
+    """Basic on a tree whose ties nest two levels deep (4 broad root children x 40 clusters:
+    the root's lp is the lowest on every path, each broad child's the next lowest for all of
+    its rows, so the two-level replay cannot certify and every query takes the DENSE re-run).
+    The lazy DENSE replay (leaf rows scored when their parent is popped, CWQ_CAT_LAZY default)
+    must give the materialised one's nodes, n_found and log_prob calls (CWQ_CAT_LAZY=0), for
+    the batch and one query per call, k = 10 and k = 3 with a small max_nodes."""
+    t, Q = broad_tree(gpu, 40_000, 128, (4, 40), 64, direct=0.02, nq=128)
+    ix = make_index(gpu, t, monkeypatch)
+    for k, mx in ((10, 100000), (3, 40)):
+        monkeypatch.setenv("CWQ_CAT_LAZY", "0")
+        ref = ix.categorize(Q, k, mx)
+        st_ref = ix.last_categorize_stats()
+        monkeypatch.delenv("CWQ_CAT_LAZY")
+        got = ix.categorize(Q, k, mx)
+        st = ix.last_categorize_stats()
+        print(k, mx, "materialised", st_ref, "lazy", st)
+        for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
+            assert torch.equal(a, b), (k, mx, name)
+        if k == 10:
+            assert st["dense_reruns"] >= Q.shape[0] // 2, st
+        for i in range(0, 16):
+            one = ix.categorize(Q[i:i + 1].contiguous(), k, mx)
+            for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, one):
+                assert torch.equal(a[i:i + 1], b), (k, mx, i, name)
+    check_basic(ix, Q[:64])
+    ix.close()
