@@ -120,6 +120,14 @@ int cwq_index_filter_info(const cwq_index* idx, int64_t* out4);
  * creation keeps the depth-1 cut. */
 int cwq_index_cut_info(const cwq_index* idx, int64_t* out4);
 
+/* After cwq_categorize / cwq_categorize_host (no reference counterpart): out[0] =
+ * queries replayed straight away by the exact lazy replay (a call of <= 64 queries on an
+ * index whose list paths left every query of the last calls to the DENSE re-run; env
+ * CWQ_CAT_DIRECT=0 / 1: never / always), out[1] = queries whose DENSE re-run was that lazy
+ * replay (leaf rows scored when their parent is popped; CWQ_CAT_LAZY=0: the materialised
+ * form).  Either way the pop order, n_found and call counts are the heap search's. */
+int cwq_last_lazy_stats(const cwq_index* idx, int64_t* out2);
+
 /*
  * "Cobweb Fast" batched top-k (A6).  Replaces CobwebWrapper.cobweb_predict_indexed
  * (CobwebWrapper.py:210-265, alias cobweb_predict_fast :428-433) for nq queries:

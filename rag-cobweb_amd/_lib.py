@@ -33,6 +33,7 @@ SIGNATURES = {
     "cwq_index_info": (_c.c_int, [_P, _P]),
     "cwq_index_filter_info": (_c.c_int, [_P, _P]),
     "cwq_index_cut_info": (_c.c_int, [_P, _P]),
+    "cwq_last_lazy_stats": (_c.c_int, [_P, _P]),
     "cwq_score_topk": (_c.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
     "cwq_rank_scores": (_c.c_int, [_P, _P, _I64, _P, _P]),
     "cwq_node_logprob": (_c.c_int, [_P, _P, _I64, _I32, _P, _P]),

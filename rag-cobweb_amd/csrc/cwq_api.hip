@@ -161,6 +161,13 @@ struct cwq_index {
   // reading that status back (categorize_impl)
   bool cat_two_spec = false;
   bool cat_tail_done = false;   // categorize_impl: the node tails are cleared, nothing runs after its last sync
+  // categorize: small calls straight to the exact lazy replay (simulate_lazy_runs_kernel) once
+  // the list paths left every query of kCatDirectAfter calls in a row to the DENSE re-run
+  // (ties nested deeper than the two-level replay certifies); the lists are tried again every
+  // kCatDirectRetry direct calls.  lazy_stats: the last call's queries replayed lazily
+  // straight away / after the list paths (cwq_last_lazy_stats)
+  int cat_dense_streak = 0, cat_direct_calls = 0;
+  int64_t lazy_stats[2] = {0, 0};
   // categorize: calls since the counting pass last resolved a query (after 8 such calls
   // cat_count_kernel is skipped -- every query then goes to the replay anyway -- and tried
   // again every kCatCountRetry calls)
@@ -1316,6 +1323,13 @@ extern "C" int cwq_index_filter_info(const cwq_index* idx, int64_t* o) {
   o[1] = idx->G;
   o[2] = idx->n_grp_rows;
   o[3] = idx->i8_state > 0 ? 1 : 0;
+  return CWQ_OK;
+}
+
+extern "C" int cwq_last_lazy_stats(const cwq_index* idx, int64_t* o) {
+  if (!idx || !o) return fail(CWQ_ERR_ARG, "NULL argument");
+  o[0] = idx->lazy_stats[0];
+  o[1] = idx->lazy_stats[1];
   return CWQ_OK;
 }
 
@@ -3024,6 +3038,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
 }
 
 constexpr int kCatCountRetry = 16;   // (cwq_index::cat_count_idle)
+constexpr int kCatDirectAfter = 2, kCatDirectRetry = 32;
 int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
                     int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
@@ -3061,6 +3076,17 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   // node tails after the last results, so the caller needs no clear_tail launch / sync
   ix->cat_tail_done = nq <= cq;
   const int64_t cap2 = 1 + (int64_t)ix->NI + 2 * R;
+  // straight to the exact lazy replay (a call of <= 64 queries; CWQ_CAT_DIRECT=0 / 1: never /
+  // always where it applies)
+  const char* cde = getenv("CWQ_CAT_DIRECT");
+  const int cdv = cde && *cde ? atoi(cde) : -1;
+  const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
+  const bool direct_ok = nq <= 64 && nq <= cq && ix->NI > 0 && ix->DP <= 2048;
+  const bool direct = direct_ok && cdv != 0 &&
+                      (cdv == 1 || (ix->cat_dense_streak >= kCatDirectAfter && ix->cat_direct_calls < kCatDirectRetry));
+  if (direct) ++ix->cat_direct_calls;
+  else if (direct_ok) ix->cat_direct_calls = 0;   // the list paths again (a retry, or never left)
+  int64_t n_dense_call = 0;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
     const int64_t nq_pad = round_up(nqc, kQPad);
@@ -3070,6 +3096,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 12) + 17 * 256 +
                   (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
+    if (direct) need += (size_t)nq_pad * ((size_t)cap_dense * 16 + 16) + 2 * 256;
     if (scat || small2)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
       need += (scat ? 2 * stream_cat_bytes(ix, nqc) : 0) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
                                                                  (size_t)R * 12 + (size_t)cap2 * 16 + 16) + 32 * 256;
@@ -3086,7 +3113,57 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HeapEnt* heap = b.take<HeapEnt>((size_t)nq_pad * cap_list);
     int* status = b.take<int>((size_t)nq_pad);
     HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s, true, q + q0 * ix->D, filt ? 1 : -1))) return rc;
+    if ((rc = run_internal(ix, c, s, true, q + q0 * ix->D, direct ? -1 : (filt ? 1 : -1)))) return rc;
+    if (direct) {
+      // the exact replay straight away: every pushed entry scored when its parent is popped
+      HeapEnt* hd = b.take<HeapEnt>((size_t)nq_pad * cap_dense);
+      SimArgs sd;
+      memset(&sd, 0, sizeof(sd));
+      sd.nq = nqc;
+      sd.k = k;
+      sd.R = 0;
+      sd.max_nodes = max_nodes;
+      sd.NI = ix->NI;
+      sd.NL = ix->NL;
+      sd.LPF = c.LPF ? c.LPF : ix->dummy;
+      sd.BF = c.BF ? c.BF : ix->dummy;
+      sd.ldI = std::max(ix->NI, 1);
+      sd.int_child_begin = ix->int_child_begin;
+      sd.int_child_end = ix->int_child_end;
+      sd.int_nchild = ix->int_nchild;
+      sd.int_bfs = ix->int_bfs;
+      sd.int_has_sent = ix->int_has_sent;
+      sd.int_leaf_a0 = ix->int_leaf_a0;
+      sd.int_leaf_a1 = ix->int_leaf_a1;
+      sd.int_leaf_b0 = ix->int_leaf_b0;
+      sd.int_leaf_b1 = ix->int_leaf_b1;
+      sd.row_par = ix->row_par;
+      sd.row_bfs = ix->row_bfs;
+      sd.row_flags = ix->row_flags;
+      sd.heap = hd;
+      sd.heap_cap = cap_dense;
+      sd.out_nodes = nodes + q0 * k;
+      sd.n_found = n_found + q0;
+      sd.n_calls = n_calls ? n_calls + q0 : nullptr;
+      sd.status = status;
+      sd.par_int = ix->par_int;
+      sd.X = c.X;
+      sd.DP = ix->DP;
+      sd.Mf = ix->iso_Mf;
+      sd.NL_iso = ix->NL_iso;
+      sd.anA = ix->an_A;
+      sd.anB = ix->an_B;
+      sd.ld_an = ix->ld_an;
+      sd.meta = ix->row_meta;
+      sd.dconst = dfull;
+      HIPCHK(launch_simulate_lazy_runs(sd, s));
+      sd.pre_status = 1;   // arena overflows: the global-heap form
+      HIPCHK(launch_simulate_lazy(sd, s));
+      ix->stats[4] += nqc;
+      ix->lazy_stats[0] += nqc;
+      ix->cat_tail_done = false;
+      continue;
+    }
     if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, true, s))) return rc;
     int nst = 0;
     std::vector<char> fbad(nqc, 0);
@@ -3383,6 +3460,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       redo.swap(left);
     }
     ix->stats[1] += (int64_t)redo.size();
+    n_dense_call += (int64_t)redo.size();
     if (redo.empty()) continue;
     ix->cat_tail_done = false;   // the DENSE re-run below writes after the last flag gather
 
@@ -3446,15 +3524,22 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       if (lazy) {
         sd.X = c2.X;
         sd.DP = ix->DP;
-        sd.isoM = ix->iso_M;
-        sd.ld_iso = ix->ld_iso;
+        sd.Mf = ix->iso_Mf;
         sd.NL_iso = ix->NL_iso;
         sd.anA = ix->an_A;
         sd.anB = ix->an_B;
         sd.ld_an = ix->ld_an;
         sd.meta = ix->row_meta;
         sd.dconst = dfull;
+        // the run-merge replay in LDS; a query that overflows its arena is re-run on the
+        // global heap (status 1 gates it; the second kernel writes status 0)
+        const char* lre = getenv("CWQ_CAT_LAZY_RUNS");
+        if (!(lre && *lre && atoi(lre) == 0)) {
+          HIPCHK(launch_simulate_lazy_runs(sd, s));
+          sd.pre_status = 1;
+        }
         HIPCHK(launch_simulate_lazy(sd, s));
+        ix->lazy_stats[1] += ns;
       } else {
         HIPCHK(launch_simulate(sd, s));
       }
@@ -3464,6 +3549,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
     }
   }
+  if (direct_ok && !direct) ix->cat_dense_streak = n_dense_call == nq ? ix->cat_dense_streak + 1 : 0;
   ix->stats[2] += (int64_t)fredo.size();
   if (!fredo.empty()) {
     // filter overflow: those queries through the exact path, results scattered back
@@ -3507,6 +3593,7 @@ extern "C" int cwq_categorize(cwq_index* ix, const float* q, int64_t nq, int32_t
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   for (int64_t& t : ix->stats) t = 0;
+  ix->lazy_stats[0] = ix->lazy_stats[1] = 0;
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
   ScanCfgScope scs(nq);
@@ -3529,6 +3616,7 @@ extern "C" int cwq_categorize_host(cwq_index* ix, const float* q, int64_t nq, in
   std::lock_guard<std::mutex> lk(ix->mu);
   DevGuard dg(ix->device);
   for (int64_t& t : ix->stats) t = 0;
+  ix->lazy_stats[0] = ix->lazy_stats[1] = 0;
   hipStream_t s = (hipStream_t)stream;
   WsUse wu(ix, s);
   ScanCfgScope scs(nq);

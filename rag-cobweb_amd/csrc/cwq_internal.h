@@ -104,9 +104,10 @@ struct SimArgs {
   const int* gate;
   // lazy DENSE replay (simulate_lazy_kernel): a popped node's leaf rows get their full lp
   // computed on the spot from the query's padded slices X (chunk layout) and the rows'
-  // dim-major operands -- isotropic mu (iso_M), anisotropic A / B -- with the scan's arithmetic
+  // operands -- isotropic mu row-major (Mf [row][DP], the rerank's copy), anisotropic A / B
+  // dim-major -- with the scan's arithmetic
   const float* X; int DP;
-  const float* isoM; int64_t ld_iso; int NL_iso;
+  const float* Mf; int NL_iso;
   const float* anA; const float* anB; int64_t ld_an;
   const RowMeta* meta; float dconst;
 };
@@ -286,6 +287,7 @@ hipError_t launch_node_lp(const float* S_int, int64_t ldI, const float* S_leaf, 
                           int64_t n_nodes, float* out, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, hipStream_t s);
 hipError_t launch_simulate_lazy(const SimArgs& a, hipStream_t s);
+hipError_t launch_simulate_lazy_runs(const SimArgs& a, hipStream_t s);
 // Categorize by counting (cat_count_kernel): resolves a query's pop sequence from the
 // bottleneck order (status 0), or leaves it to the heap replay (status 2).
 hipError_t launch_cat_count(const SimArgs& a, hipStream_t s);

@@ -1427,27 +1427,14 @@ __global__ __launch_bounds__(256) void simulate_wave_kernel(const SimArgs a) {
 // the pops, are DENSE mode's bit for bit.  Same pushes in the same order (internal children
 // in child order, then the isotropic and the anisotropic rows in row order), so the heap
 // holds the same entries and pops the same sequence.
-__device__ __forceinline__ float lazy_row_lp(const SimArgs& a, const float* s_x, int r, bool iso) {
+// The full lp of an anisotropic row, one row per lane (dim-major A / B: consecutive rows are
+// consecutive addresses).
+__device__ __forceinline__ float lazy_aniso_lp(const SimArgs& a, const float* s_x, int r) {
   const int NV16 = a.DP / 16;
-  float acc = 0.f;
-  if (iso) {
-    const float* __restrict__ m = a.isoM + r;
-    for (int v = 0; v < NV16; ++v) {
-      float part;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float t = s_x[v * 16 + j] - m[(size_t)(v * 16 + j) * a.ld_iso];
-        part = (j == 0) ? t * t : fmaf(t, t, part);
-      }
-      acc += part;
-    }
-    float lp;
-    (void)iso_key_tail(acc, a.meta[r], CWQ_INF, lp, 1, a.dconst);
-    return lp;
-  }
   const int ra = r - a.NL_iso;
   const float* __restrict__ A = a.anA + ra;
   const float* __restrict__ B = a.anB + ra;
+  float acc = 0.f;
   for (int v = 0; v < NV16; ++v) {
     float part;
 #pragma unroll
@@ -1462,8 +1449,55 @@ __device__ __forceinline__ float lazy_row_lp(const SimArgs& a, const float* s_x,
   return -0.5f * (md.logdet + a.dconst + acc);
 }
 
+// The full lp of m <= 64 isotropic rows rb.. (lane e: row rb + e): every (row, 16-dim slice)
+// partial by the wave's lanes from the row-major fp32 copy Mf (a lane a slice, 64 contiguous
+// bytes; four rows' loads in flight), then each row's lane adds its partials in slice order.
+__device__ __forceinline__ float lazy_iso_lp(const SimArgs& a, const float* s_x, float* s_part, int rb, int m,
+                                             int lane) {
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  for (int e0 = 0; e0 < m; e0 += 4) {
+    for (int v = lane; v < NV16; v += 64) {
+      float4 m4[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(e0 + u, m - 1);
+        const float* __restrict__ mr = a.Mf + (size_t)(rb + e) * a.DP + v * 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[u][j] = *reinterpret_cast<const float4*>(mr + j * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float4 t4 = m4[u][j >> 2];
+          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+          const float t = s_x[v * 16 + j] - mj;
+          part = (j == 0) ? t * t : fmaf(t, t, part);
+        }
+        if (e0 + u < m) s_part[(e0 + u) * LDP + v] = part;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float lp = 0.f;
+  if (lane < m) {
+    float acc = 0.f;
+    for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+    (void)iso_key_tail(acc, a.meta[rb + lane], CWQ_INF, lp, 1, a.dconst);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_part reused by the next batch
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return lp;
+}
+
+constexpr int kLazyMaxDP = 2048;
 __global__ __launch_bounds__(64) void simulate_lazy_kernel(const SimArgs a) {
-  __shared__ float s_x[2048];   // the query's padded dims (DP <= 2048)
+  __shared__ float s_x[kLazyMaxDP];                       // the query's padded dims
+  __shared__ float s_part[64 * (kLazyMaxDP / 16 + 1)];   // [row][slice] partials
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x;
   if (q >= a.nq) return;
@@ -1479,7 +1513,7 @@ __global__ __launch_bounds__(64) void simulate_lazy_kernel(const SimArgs a) {
   if (a.NI > 0) {
     wheap_push(h, hn, HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0}, lane);
   } else {   // single-node tree: the root is leaf row 0
-    const float lp = lazy_row_lp(a, s_x, 0, a.NL_iso > 0);
+    const float lp = a.NL_iso > 0 ? rl_f(lazy_iso_lp(a, s_x, s_part, 0, 1, lane), 0) : lazy_aniso_lp(a, s_x, 0);
     wheap_push(h, hn, HeapEnt{lp, 0.f, a.row_bfs[0], -1}, lane);
   }
   while (hn > 0) {
@@ -1502,10 +1536,14 @@ __global__ __launch_bounds__(64) void simulate_lazy_kernel(const SimArgs a) {
       const int r0 = pass ? a.int_leaf_b0[u] : a.int_leaf_a0[u];
       const int r1 = pass ? a.int_leaf_b1[u] : a.int_leaf_a1[u];
       for (int rb = r0; rb < r1; rb += 64) {
+        const int m = min(64, r1 - rb);
         const int r = rb + lane;
-        const bool in = r < r1;
-        const bool ok = in && !(a.row_flags[r] & FLAG_INT_COPY);
-        const float lp = ok ? lazy_row_lp(a, s_x, r, pass == 0) : 0.f;
+        const bool ok = lane < m && !(a.row_flags[r] & FLAG_INT_COPY);
+        float lp;
+        if (pass == 0)
+          lp = lazy_iso_lp(a, s_x, s_part, rb, m, lane);
+        else
+          lp = ok ? lazy_aniso_lp(a, s_x, r) : 0.f;
         const int tb = ok ? a.row_bfs[r] : 0;
         uint64_t bm = __ballot(ok);
         while (bm) {   // in row order, as the dense replay pushes them
@@ -1524,7 +1562,7 @@ __global__ __launch_bounds__(64) void simulate_lazy_kernel(const SimArgs a) {
 }
 
 hipError_t launch_simulate_lazy(const SimArgs& a, hipStream_t s) {
-  if (a.R != 0 || !a.X || a.DP <= 0 || a.DP > 2048 || a.DP % 16 || !a.meta || (a.NL_iso > 0 && !a.isoM) ||
+  if (a.R != 0 || !a.X || a.DP <= 0 || a.DP > kLazyMaxDP || a.DP % 16 || !a.meta || (a.NL_iso > 0 && !a.Mf) ||
       (a.NL > a.NL_iso && (!a.anA || !a.anB)))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(simulate_lazy_kernel, dim3((unsigned)a.nq), dim3(64), 0, s, a);
@@ -1880,6 +1918,301 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
 #endif
 }
 #undef TWO_ADD_RUN
+
+// The lazy DENSE replay as a k-way merge of sorted runs (round 6): simulate_two_kernel's
+// frontier (run heads in registers, entries in an LDS arena, a pop = one DPP argmax) with no
+// lists and nothing to certify -- every pushed entry's key is exact: an internal child's from
+// the exact internal pass (LPF), a leaf row's computed when its parent is popped, by the
+// whole workgroup (every (row, 16-dim slice) partial from the row-major Mf in parallel, each
+// row's partials added in slice order: the scan's arithmetic; anisotropic rows one per
+// thread).  The heap order is total (score, pscore, BFS index), so the pops are DENSE mode's
+// (simulate_wave_kernel R = 0) exactly, and so are n_found, the nodes and the call count.
+// Wave 0 runs the frontier; the other waves join only to score a popped node's leaf rows (64
+// per round).  An arena or run-slot overflow sets status 1: simulate_lazy_kernel (global
+// 64-ary heap) re-runs the query.
+constexpr int kLzArena = 3072, kLzThreads = 256;
+struct alignas(16) LzRec {
+  int cb, ce, nch, hs;   // internal: child range and count; has_sent
+};
+size_t lazy_runs_lds(int DP) {
+  return (size_t)kLzArena * (sizeof(HeapEnt) + sizeof(LzRec)) + (size_t)DP * 4 + (size_t)64 * (DP / 16 + 1) * 4;
+}
+
+__global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const SimArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lz_s[];
+  HeapEnt* ae = reinterpret_cast<HeapEnt*>(lz_s);
+  LzRec* ax = reinterpret_cast<LzRec*>(ae + kLzArena);
+  float* s_x = reinterpret_cast<float*>(ax + kLzArena);   // [DP]
+  float* s_part = s_x + a.DP;                             // [64][NV16 + 1]
+  __shared__ float s_lp[64];
+  __shared__ int s_job[4];   // [0] 0: score rows, 1: done; [1] first row; [2] rows; [3] 1: isotropic
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x;
+  if (q >= a.nq) return;
+  if (a.pre_status && a.status[q] == 0) return;
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  {
+    const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+    for (int d = tid; d < a.DP; d += kLzThreads) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+  }
+  // wave 0's frontier (the other waves keep unused copies)
+  uint64_t hk[kTwoSlots];
+  int htb[kTwoSlots], hix[kTwoSlots], hend[kTwoSlots];
+#pragma unroll
+  for (int j = 0; j < kTwoSlots; ++j) {
+    hk[j] = 0;
+    htb[j] = hix[j] = hend[j] = 0;
+  }
+  int nruns = 0, an = 0;
+#define LZ_ADD_RUN(i0, i1, sc, ps, tb)                    \
+  do {                                                    \
+    bool fr_ = false;                                     \
+    _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) fr_ |= hk[j_] == 0; \
+    const uint64_t fm_ = __ballot(fr_);                   \
+    const uint64_t nk_ = head_key((sc), (ps));            \
+    const int tb_ = (tb), i0_ = (i0), i1_ = (i1);         \
+    if (lane == __builtin_ctzll(fm_)) {                   \
+      bool done_ = false;                                 \
+      _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) { \
+        const bool put_ = !done_ && hk[j_] == 0;          \
+        hk[j_] = put_ ? nk_ : hk[j_];                     \
+        htb[j_] = put_ ? tb_ : htb[j_];                   \
+        hix[j_] = put_ ? i0_ : hix[j_];                   \
+        hend[j_] = put_ ? i1_ : hend[j_];                 \
+        done_ |= put_;                                    \
+      }                                                   \
+    }                                                     \
+    ++nruns;                                              \
+  } while (0)
+  int status = 0, found = 0;
+  int64_t calls = 1, visited = 0;
+  // the popped node whose leaf rows are being scored: its score (their pscore) and the row
+  // ranges left (isotropic [ra, rae), then anisotropic [rb, rbe))
+  float pend_ps = 0.f;
+  int ra = 0, rae = 0, rb = 0, rbe = 0;
+  int job_r0 = 0, job_m = 0, job_iso = 0;   // the chunk just scored (wave 0 ranks it)
+  if (wave == 0) {
+    if (a.NI <= 0) {
+      status = 1;   // single-node tree: simulate_lazy_kernel
+    } else {
+      if (lane == 0) {
+        ae[0] = HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0};
+        ax[0] = LzRec{a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0], a.int_has_sent[0] != 0 ? 1 : 0};
+      }
+      an = 1;
+      LZ_ADD_RUN(0, 1, a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0]);
+    }
+  }
+  for (;;) {
+    if (wave == 0) {
+      bool need = false, done = status != 0;
+      if (!done && job_m > 0) {
+        // rank the scored chunk (one pscore: by score, then BFS index) and write it as a run
+        const int r = job_r0 + lane;
+        const bool ok = lane < job_m && !(a.row_flags[r] & FLAG_INT_COPY);
+        const float lp = ok ? s_lp[lane] : 0.f;
+        const float lc = lp == lp ? lp : -CWQ_INF;
+        const int tb = ok ? a.row_bfs[r] : 0;
+        const uint64_t bm = __ballot(ok);
+        int rk = 0;
+        for (uint64_t mm = bm; mm;) {
+          const int j = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          rk += rank_before(rl_f(lc, j), rl_i(tb, j), lc, tb);
+        }
+        const int nr = __popcll(bm);
+        if (nr > 0) {
+          if (an + nr > kLzArena || nruns + 1 > 64 * kTwoSlots) {
+            status = 1;
+            done = true;
+          } else {
+            if (ok) {
+              ae[an + rk] = HeapEnt{lp, pend_ps, tb, -(r + 1)};
+              ax[an + rk] = LzRec{0, 0, 0, (a.row_flags[r] & FLAG_HAS_SENT) != 0 ? 1 : 0};
+            }
+            const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
+            LZ_ADD_RUN(an, an + nr, rl_f(lp, hl), pend_ps, rl_i(tb, hl));
+            an += nr;
+          }
+        }
+        job_m = 0;
+      }
+      // the next chunk of the popped node's rows, if any
+      if (!done && ra < rae) {
+        job_r0 = ra;
+        job_m = min(64, rae - ra);
+        job_iso = 1;
+        ra += job_m;
+        need = true;
+      } else if (!done && rb < rbe) {
+        job_r0 = rb;
+        job_m = min(64, rbe - rb);
+        job_iso = 0;
+        rb += job_m;
+        need = true;
+      }
+      while (!done && !need) {
+        if (nruns <= 0) {
+          done = true;
+          break;
+        }
+        uint64_t bk = 0;
+        int btb = 0x7fffffff, bj = -1, bix = 0, bend = 0;
+#pragma unroll
+        for (int j = 0; j < kTwoSlots; ++j) {
+          const bool bt = hk[j] > bk || (hk[j] == bk && hk[j] != 0 && htb[j] < btb);
+          bk = bt ? hk[j] : bk;
+          btb = bt ? htb[j] : btb;
+          bj = bt ? j : bj;
+          bix = bt ? hix[j] : bix;
+          bend = bt ? hend[j] : bend;
+        }
+        const int wl = wave_first(bk, btb);
+        if (wl < 0) {
+          status = 1;
+          done = true;
+          break;
+        }
+        const int idx = __builtin_amdgcn_readlane(bix, wl), iend = __builtin_amdgcn_readlane(bend, wl);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const HeapEnt e = ae[idx];
+        const LzRec x = ax[idx];
+        const bool more = idx + 1 < iend;
+        const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
+        const uint64_t nk = more ? head_key(nx.score, nx.pscore) : 0;
+#pragma unroll
+        for (int j = 0; j < kTwoSlots; ++j) {
+          const bool adv = lane == wl && bj == j;
+          hk[j] = adv ? nk : hk[j];
+          htb[j] = adv ? nx.tb : htb[j];
+          hix[j] = adv ? idx + 1 : hix[j];
+        }
+        if (!more) --nruns;
+        ++visited;
+        if (visited >= a.max_nodes) {
+          done = true;
+          break;
+        }
+        if (x.hs) {
+          if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+          ++found;
+        }
+        if (found == a.k) {
+          done = true;
+          break;
+        }
+        if (e.node < 0) continue;
+        const int u = e.node;
+        const int cb = x.cb, ce = x.ce;
+        calls += x.nch;
+        if (an + (ce - cb) > kLzArena || nruns + (ce - cb + 63) / 64 > 64 * kTwoSlots) {
+          status = 1;
+          done = true;
+          break;
+        }
+        for (int c0 = cb; c0 < ce; c0 += 64) {   // the internal children: one load round trip per 64, one run
+          const int c = c0 + lane;
+          const bool ok = c < ce;
+          const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
+          const int tb = ok ? a.int_bfs[c] : 0;
+          const int hs = ok ? (a.int_has_sent[c] != 0 ? 1 : 0) : 0;
+          const int ccb = ok ? a.int_child_begin[c] : 0, cce = ok ? a.int_child_end[c] : 0;
+          const int cnc = ok ? a.int_nchild[c] : 0;
+          const int m = min(64, ce - c0);
+          const float lc = lpf == lpf ? lpf : -CWQ_INF;
+          int rk = 0;
+          for (int j = 0; j < m; ++j) {
+            const float sj = rl_f(lc, j);
+            const int tj = rl_i(tb, j);
+            rk += sj > lc || (sj == lc && tj < tb);
+          }
+          if (ok) {
+            ae[an + rk] = HeapEnt{lpf, e.score, tb, c};
+            ax[an + rk] = LzRec{ccb, cce, cnc, hs};
+          }
+          const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
+          LZ_ADD_RUN(an, an + m, rl_f(lpf, hl), e.score, rl_i(tb, hl));
+          an += m;
+        }
+        ra = a.int_leaf_a0[u];
+        rae = a.int_leaf_a1[u];
+        rb = a.int_leaf_b0[u];
+        rbe = a.int_leaf_b1[u];
+        pend_ps = e.score;
+        if (ra < rae) {
+          job_r0 = ra;
+          job_m = min(64, rae - ra);
+          job_iso = 1;
+          ra += job_m;
+          need = true;
+        } else if (rb < rbe) {
+          job_r0 = rb;
+          job_m = min(64, rbe - rb);
+          job_iso = 0;
+          rb += job_m;
+          need = true;
+        }
+      }
+      if (lane == 0) {
+        s_job[0] = done ? 1 : 0;
+        s_job[1] = job_r0;
+        s_job[2] = job_m;
+        s_job[3] = job_iso;
+      }
+    }
+    __syncthreads();
+    if (s_job[0]) break;
+    // score the chunk: rows r0 .. r0 + m
+    const int r0 = s_job[1], m = s_job[2];
+    if (s_job[3]) {
+      for (int t = tid; t < m * NV16; t += kLzThreads) {
+        const int e = t / NV16, v = t - e * NV16;
+        const float* __restrict__ mr = a.Mf + (size_t)(r0 + e) * a.DP + v * 16;
+        float4 m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float4 t4 = m4[j >> 2];
+          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+          const float tt = s_x[v * 16 + j] - mj;
+          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+        }
+        s_part[e * LDP + v] = part;
+      }
+      __syncthreads();
+      if (tid < m) {
+        float acc = 0.f;
+        for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+        float lp;
+        (void)iso_key_tail(acc, a.meta[r0 + tid], CWQ_INF, lp, 1, a.dconst);
+        s_lp[tid] = lp;
+      }
+    } else if (tid < m) {
+      s_lp[tid] = lazy_aniso_lp(a, s_x, r0 + tid);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.n_found[q] = found < a.k ? found : a.k;
+    if (a.n_calls) a.n_calls[q] = calls;
+    a.status[q] = status;
+  }
+}
+#undef LZ_ADD_RUN
+
+hipError_t launch_simulate_lazy_runs(const SimArgs& a, hipStream_t s) {
+  if (a.R != 0 || !a.X || a.DP <= 0 || a.DP > kLazyMaxDP || a.DP % 16 || !a.meta || (a.NL_iso > 0 && !a.Mf) ||
+      (a.NL > a.NL_iso && (!a.anA || !a.anB)))
+    return hipErrorInvalidValue;
+  const size_t lds = lazy_runs_lds(a.DP);
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simulate_lazy_runs_kernel), lds)) return e;
+  hipLaunchKernelGGL(simulate_lazy_runs_kernel, dim3((unsigned)a.nq), dim3(kLzThreads), lds, s, a);
+  return hipGetLastError();
+}
 
 // nodes[q][i] = -1 for i >= n_found[q]: the entries past a query's retrievals are defined
 // whichever path (count, replay, two-level, DENSE) resolved it.

@@ -203,6 +203,13 @@ class CobwebIndex:
         return {"queries": int(out[0]), "dense_reruns": int(out[1]), "filter_reruns": int(out[2]),
                 "by_count": int(out[3]), "by_replay": int(out[4]), "two_level": int(out[5])}
 
+    def last_lazy_stats(self):
+        """The last categorize call's exact lazy replays (cwq_last_lazy_stats): queries replayed
+        straight away (the list paths skipped), and DENSE re-runs done by the lazy replay."""
+        out = np.zeros(2, np.int64)
+        check(self._L.cwq_last_lazy_stats(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return {"direct": int(out[0]), "dense_lazy": int(out[1])}
+
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
             self._L.cwq_index_destroy(self._h)

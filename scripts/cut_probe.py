@@ -61,8 +61,12 @@ def legs(ix, Q, k, tag):
 
 def basic(ix, Q, k, tag):
     ref = None
-    for lazy in ("0", "1"):
-        os.environ["CWQ_CAT_LAZY"] = lazy
+    for name, env in (("materialised", {"CWQ_CAT_LAZY": "0", "CWQ_CAT_DIRECT": "0"}),
+                      ("lazy-heap", {"CWQ_CAT_LAZY_RUNS": "0", "CWQ_CAT_DIRECT": "0"}),
+                      ("lazy-runs", {"CWQ_CAT_DIRECT": "0"}), ("direct", {"CWQ_CAT_DIRECT": "1"}), ("auto", {})):
+        for key in ("CWQ_CAT_LAZY", "CWQ_CAT_LAZY_RUNS", "CWQ_CAT_DIRECT"):
+            os.environ.pop(key, None)
+        os.environ.update(env)
         got = ix.categorize(Q, k, 100000)
         t = med(lambda: ix.categorize(Q, k, 100000), 3)
         st = ix.last_categorize_stats()
@@ -77,10 +81,11 @@ def basic(ix, Q, k, tag):
         ts.sort()
         same = ref is None or all(torch.equal(a, b) for a, b in zip(ref, got))
         ref = ref or got
-        print(f"[{tag}] Basic lazy={lazy} batch {Q.shape[0]}: {t * 1e3:.3f} ms; one query per call median "
-              f"{ts[8] * 1e6:.1f} us; == materialised {same}; calls/query {float(got[2].float().mean()):.0f}; {st}",
-              flush=True)
-    os.environ.pop("CWQ_CAT_LAZY", None)
+        print(f"[{tag}] Basic {name} batch {Q.shape[0]}: {t * 1e3:.3f} ms; one query per call median "
+              f"{ts[8] * 1e6:.1f} us; == materialised {same}; calls/query {float(got[2].float().mean()):.0f}; {st}; "
+              f"last call lazy {ix.last_lazy_stats()}", flush=True)
+    for key in ("CWQ_CAT_LAZY", "CWQ_CAT_LAZY_RUNS", "CWQ_CAT_DIRECT"):
+        os.environ.pop(key, None)
 
 
 def main():

@@ -210,11 +210,14 @@ def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
         ref = ix.categorize(Q, k, mx)
         st_ref = ix.last_categorize_stats()
         monkeypatch.delenv("CWQ_CAT_LAZY")
-        got = ix.categorize(Q, k, mx)
+        monkeypatch.setenv("CWQ_CAT_LAZY_RUNS", "0")   # the global-heap form alone
+        heap = ix.categorize(Q, k, mx)
+        monkeypatch.delenv("CWQ_CAT_LAZY_RUNS")
+        got = ix.categorize(Q, k, mx)                  # the LDS run-merge form (default)
         st = ix.last_categorize_stats()
         print(k, mx, "materialised", st_ref, "lazy", st)
-        for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
-            assert torch.equal(a, b), (k, mx, name)
+        for name, a, b, c in zip(("nodes", "n_found", "n_calls"), ref, got, heap):
+            assert torch.equal(a, b) and torch.equal(a, c), (k, mx, name)
         if k == 10:
             assert st["dense_reruns"] >= Q.shape[0] // 2, st
         for i in range(0, 16):
@@ -223,3 +226,56 @@ def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
                 assert torch.equal(a[i:i + 1], b), (k, mx, i, name)
     check_basic(ix, Q[:64])
     ix.close()
+
+
+@pytest.mark.parametrize("shape", ["nested ties", "ifit"])
+def test_direct_lazy_replay(gpu, monkeypatch, shape):
+    """Basic straight through the exact lazy replay (CWQ_CAT_DIRECT=1: the list paths
+    skipped) against the list paths (CWQ_CAT_DIRECT=0), one and eight queries per call, on
+    the nested-tie tree and on a device-ifit clustered tree; the automatic rule goes direct
+    once two calls in a row left every query to the DENSE re-run (and only then)."""
+    import random
+    if shape == "nested ties":
+        t, Q = broad_tree(gpu, 30_000, 96, (4, 30), 65, direct=0.02, nq=64)
+        ix = make_index(gpu, t, monkeypatch)
+    else:
+        rng = np.random.default_rng(66)
+        C = rng.standard_normal((30, 64)).astype(np.float32) * 2.0
+        X = (C[rng.integers(0, 30, 6000)] + 0.3 * rng.standard_normal((6000, 64))).astype(np.float32)
+        random.seed(66)
+        w = gpu.CobwebWrapper(corpus=None, corpus_embeddings=X)
+        w.build_prediction_index()
+        ix = w._index
+        Q = torch.from_numpy((X[:64] + 0.05 * rng.standard_normal((64, 64))).astype(np.float32)).cuda()
+    for k, mx in ((10, 100000), (4, 60)):
+        for m in (1, 8):
+            for a in range(0, 32, m):
+                q = Q[a:a + m].contiguous()
+                monkeypatch.setenv("CWQ_CAT_DIRECT", "0")
+                ref = ix.categorize(q, k, mx)
+                monkeypatch.setenv("CWQ_CAT_DIRECT", "1")
+                got = ix.categorize(q, k, mx)
+                assert ix.last_lazy_stats()["direct"] == m
+                for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
+                    assert torch.equal(x, y), (shape, k, mx, m, a, name)
+    monkeypatch.delenv("CWQ_CAT_DIRECT")
+    # a fresh index for the automatic rule (the calls above fed the old one's record)
+    if shape == "nested ties":
+        ix.close()
+        ix = make_index(gpu, t, monkeypatch)
+    else:
+        w._invalidate_prediction_index()
+        w.build_prediction_index()
+        ix = w._index
+    seen = []
+    for i in range(6):
+        ix.categorize(Q[i:i + 1].contiguous(), 10, 100000)
+        seen.append((ix.last_categorize_stats()["dense_reruns"], ix.last_lazy_stats()["direct"]))
+    print(shape, seen)
+    streak = 0   # the rule: direct once two list-path calls in a row went all DENSE
+    for r, d in seen:
+        assert d == (1 if streak >= 2 else 0), seen
+        if not d:
+            streak = streak + 1 if r == 1 else 0
+    if shape == "nested ties":   # every list-path call goes DENSE: direct from the third call on
+        assert seen[0] == (1, 0) and seen[1] == (1, 0) and all(d == 1 for _, d in seen[2:]), seen
