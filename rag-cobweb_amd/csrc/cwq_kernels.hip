@@ -1931,6 +1931,7 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
 // per round).  An arena or run-slot overflow sets status 1: simulate_lazy_kernel (global
 // 64-ary heap) re-runs the query.
 constexpr int kLzArena = 3072, kLzThreads = 256;
+constexpr int kLzSlots = 8;   // run heads per lane: 512 live runs (a row run and a child run per internal pop)
 struct alignas(16) LzRec {
   int cb, ce, nch, hs;   // internal: child range and count; has_sent
 };
@@ -1956,10 +1957,10 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
     for (int d = tid; d < a.DP; d += kLzThreads) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
   }
   // wave 0's frontier (the other waves keep unused copies)
-  uint64_t hk[kTwoSlots];
-  int htb[kTwoSlots], hix[kTwoSlots], hend[kTwoSlots];
+  uint64_t hk[kLzSlots];
+  int htb[kLzSlots], hix[kLzSlots], hend[kLzSlots];
 #pragma unroll
-  for (int j = 0; j < kTwoSlots; ++j) {
+  for (int j = 0; j < kLzSlots; ++j) {
     hk[j] = 0;
     htb[j] = hix[j] = hend[j] = 0;
   }
@@ -1967,13 +1968,13 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
 #define LZ_ADD_RUN(i0, i1, sc, ps, tb)                    \
   do {                                                    \
     bool fr_ = false;                                     \
-    _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) fr_ |= hk[j_] == 0; \
+    _Pragma("unroll") for (int j_ = 0; j_ < kLzSlots; ++j_) fr_ |= hk[j_] == 0; \
     const uint64_t fm_ = __ballot(fr_);                   \
     const uint64_t nk_ = head_key((sc), (ps));            \
     const int tb_ = (tb), i0_ = (i0), i1_ = (i1);         \
     if (lane == __builtin_ctzll(fm_)) {                   \
       bool done_ = false;                                 \
-      _Pragma("unroll") for (int j_ = 0; j_ < kTwoSlots; ++j_) { \
+      _Pragma("unroll") for (int j_ = 0; j_ < kLzSlots; ++j_) { \
         const bool put_ = !done_ && hk[j_] == 0;          \
         hk[j_] = put_ ? nk_ : hk[j_];                     \
         htb[j_] = put_ ? tb_ : htb[j_];                   \
@@ -2022,7 +2023,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
         }
         const int nr = __popcll(bm);
         if (nr > 0) {
-          if (an + nr > kLzArena || nruns + 1 > 64 * kTwoSlots) {
+          if (an + nr > kLzArena || nruns + 1 > 64 * kLzSlots) {
             status = 1;
             done = true;
           } else {
@@ -2059,7 +2060,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
         uint64_t bk = 0;
         int btb = 0x7fffffff, bj = -1, bix = 0, bend = 0;
 #pragma unroll
-        for (int j = 0; j < kTwoSlots; ++j) {
+        for (int j = 0; j < kLzSlots; ++j) {
           const bool bt = hk[j] > bk || (hk[j] == bk && hk[j] != 0 && htb[j] < btb);
           bk = bt ? hk[j] : bk;
           btb = bt ? htb[j] : btb;
@@ -2083,7 +2084,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
         const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
         const uint64_t nk = more ? head_key(nx.score, nx.pscore) : 0;
 #pragma unroll
-        for (int j = 0; j < kTwoSlots; ++j) {
+        for (int j = 0; j < kLzSlots; ++j) {
           const bool adv = lane == wl && bj == j;
           hk[j] = adv ? nk : hk[j];
           htb[j] = adv ? nx.tb : htb[j];
@@ -2107,7 +2108,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
         const int u = e.node;
         const int cb = x.cb, ce = x.ce;
         calls += x.nch;
-        if (an + (ce - cb) > kLzArena || nruns + (ce - cb + 63) / 64 > 64 * kTwoSlots) {
+        if (an + (ce - cb) > kLzArena || nruns + (ce - cb + 63) / 64 > 64 * kLzSlots) {
           status = 1;
           done = true;
           break;
