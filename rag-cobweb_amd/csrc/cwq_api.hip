@@ -161,12 +161,16 @@ struct cwq_index {
   // reading that status back (categorize_impl)
   bool cat_two_spec = false;
   bool cat_tail_done = false;   // categorize_impl: the node tails are cleared, nothing runs after its last sync
-  // categorize: small calls straight to the exact lazy replay (simulate_lazy_runs_kernel) once
-  // the list paths left every query of kCatDirectAfter calls in a row to the DENSE re-run
-  // (ties nested deeper than the two-level replay certifies); the lists are tried again every
-  // kCatDirectRetry direct calls.  lazy_stats: the last call's queries replayed lazily
-  // straight away / after the list paths (cwq_last_lazy_stats)
-  int cat_dense_streak = 0, cat_direct_calls = 0;
+  // categorize, calls of <= 64 queries: the list paths, or straight to the exact lazy replay
+  // (simulate_lazy_runs_kernel; categorize_impl's path choice).  The choice is measured: per-query
+  // wall time of each path (EMA), the faster one taken, the other tried every kCatExplore calls
+  // -- but the lazy path is only ever tried while the list paths recently left queries to the
+  // DENSE re-run (cat_dense_seen: ties nested deeper than the two-level replay certifies; a
+  // tree the lists resolve, C2's or a flat one, never pays for the trial).  lazy_stats: the last
+  // call's queries replayed lazily straight away / after the list paths (cwq_last_lazy_stats)
+  double cat_ema_list = -1.0, cat_ema_direct = -1.0;
+  int cat_dense_seen = 0, cat_pol_calls = 0;
+  bool cat_pref_direct = false;
   int64_t lazy_stats[2] = {0, 0};
   // categorize: calls since the counting pass last resolved a query (after 8 such calls
   // cat_count_kernel is skipped -- every query then goes to the replay anyway -- and tried
@@ -3038,7 +3042,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
 }
 
 constexpr int kCatCountRetry = 16;   // (cwq_index::cat_count_idle)
-constexpr int kCatDirectAfter = 2, kCatDirectRetry = 32;
+constexpr int kCatExplore = 32, kCatDenseMemory = 64;   // (cwq_index::cat_ema_*)
 int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
                     int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
@@ -3082,10 +3086,23 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const int cdv = cde && *cde ? atoi(cde) : -1;
   const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
   const bool direct_ok = nq <= 64 && nq <= cq && ix->NI > 0 && ix->DP <= 2048;
-  const bool direct = direct_ok && cdv != 0 &&
-                      (cdv == 1 || (ix->cat_dense_streak >= kCatDirectAfter && ix->cat_direct_calls < kCatDirectRetry));
-  if (direct) ++ix->cat_direct_calls;
-  else if (direct_ok) ix->cat_direct_calls = 0;   // the list paths again (a retry, or never left)
+  const bool top = allow_filter;   // (not the filter-overflow re-run of a call)
+  const bool measure = direct_ok && cdv < 0 && top;
+  bool direct = false;
+  if (direct_ok) {
+    if (cdv >= 0) {
+      direct = cdv == 1;
+    } else if (!top) {
+      direct = ix->cat_pref_direct;
+    } else {
+      ++ix->cat_pol_calls;
+      if (ix->cat_dense_seen <= 0) direct = false;               // the lists resolve this tree
+      else if (ix->cat_ema_direct < 0.0) direct = true;          // the first trial
+      else if (ix->cat_ema_list < 0.0) direct = false;
+      else direct = (ix->cat_ema_direct < ix->cat_ema_list) != (ix->cat_pol_calls % kCatExplore == 0);
+    }
+  }
+  const auto t_call = std::chrono::steady_clock::now();
   int64_t n_dense_call = 0;
   for (int64_t q0 = 0; q0 < nq; q0 += cq) {
     const int nqc = (int)std::min(cq, nq - q0);
@@ -3549,7 +3566,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
     }
   }
-  if (direct_ok && !direct) ix->cat_dense_streak = n_dense_call == nq ? ix->cat_dense_streak + 1 : 0;
+  if (measure && !direct) ix->cat_dense_seen = n_dense_call > 0 ? kCatDenseMemory : std::max(0, ix->cat_dense_seen - 1);
   ix->stats[2] += (int64_t)fredo.size();
   if (!fredo.empty()) {
     // filter overflow: those queries through the exact path, results scattered back
@@ -3580,6 +3597,14 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     if (n_calls) HIPCHK(launch_copy_rows(cl, 2, nullptr, n_calls, 2, d_idx, n, 2, s));
     HIPCHK(hipStreamSynchronize(s));
     ix->cat_tail_done = false;
+  }
+  if (measure) {   // the path's per-query wall time, completed (the caller syncs after a small call anyway)
+    HIPCHK(hipStreamSynchronize(s));
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count() /
+                      (double)nq;
+    double& ema = direct ? ix->cat_ema_direct : ix->cat_ema_list;
+    ema = ema < 0.0 ? us : 0.75 * ema + 0.25 * us;
+    ix->cat_pref_direct = ix->cat_ema_direct >= 0.0 && ix->cat_ema_list >= 0.0 && ix->cat_ema_direct < ix->cat_ema_list;
   }
   return CWQ_OK;
 }

@@ -232,8 +232,8 @@ def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
 def test_direct_lazy_replay(gpu, monkeypatch, shape):
     """Basic straight through the exact lazy replay (CWQ_CAT_DIRECT=1: the list paths
     skipped) against the list paths (CWQ_CAT_DIRECT=0), one and eight queries per call, on
-    the nested-tie tree and on a device-ifit clustered tree; the automatic rule goes direct
-    once two calls in a row left every query to the DENSE re-run (and only then)."""
+    the nested-tie tree and on a device-ifit clustered tree; the automatic choice tries the
+    lazy path only after the lists left a query to the DENSE re-run, then keeps the faster."""
     import random
     if shape == "nested ties":
         t, Q = broad_tree(gpu, 30_000, 96, (4, 30), 65, direct=0.02, nq=64)
@@ -272,10 +272,11 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
         ix.categorize(Q[i:i + 1].contiguous(), 10, 100000)
         seen.append((ix.last_categorize_stats()["dense_reruns"], ix.last_lazy_stats()["direct"]))
     print(shape, seen)
-    streak = 0   # the rule: direct once two list-path calls in a row went all DENSE
-    for r, d in seen:
-        assert d == (1 if streak >= 2 else 0), seen
-        if not d:
-            streak = streak + 1 if r == 1 else 0
-    if shape == "nested ties":   # every list-path call goes DENSE: direct from the third call on
-        assert seen[0] == (1, 0) and seen[1] == (1, 0) and all(d == 1 for _, d in seen[2:]), seen
+    # the rule: the lazy path is tried only after a list-path call left a query to DENSE; then
+    # the faster of the two (measured) is taken
+    first_dense = next((i for i, (r, d) in enumerate(seen) if not d and r >= 1), None)
+    for i, (r, d) in enumerate(seen):
+        if d:
+            assert first_dense is not None and i > first_dense, seen
+    if shape == "nested ties":   # the lists leave every query DENSE; the lazy path is ~2.5x faster
+        assert seen[0] == (1, 0) and seen[1][1] == 1 and sum(d for _, d in seen[2:]) >= 3, seen
