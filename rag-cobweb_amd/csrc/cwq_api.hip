@@ -168,9 +168,12 @@ struct cwq_index {
   // DENSE re-run (cat_dense_seen: ties nested deeper than the two-level replay certifies; a
   // tree the lists resolve, C2's or a flat one, never pays for the trial).  lazy_stats: the last
   // call's queries replayed lazily straight away / after the list paths (cwq_last_lazy_stats)
-  double cat_ema_list = -1.0, cat_ema_direct = -1.0;
-  int cat_dense_seen = 0, cat_pol_calls = 0;
-  bool cat_pref_direct = false;
+  // [0]: calls of <= 64 queries, [1]: batches (tried on any tree whose widest node fits the
+  // replay's arena, max_fanout <= kLzFanout: the lazy replays of a batch run side by side)
+  double cat_ema_list[2] = {-1.0, -1.0}, cat_ema_direct[2] = {-1.0, -1.0};
+  int cat_dense_seen = 0, cat_pol_calls[2] = {0, 0};
+  bool cat_pref_direct[2] = {false, false};
+  int max_fanout = 0;   // the most children (internal + leaf rows) of one internal node
   int64_t lazy_stats[2] = {0, 0};
   // categorize: calls since the counting pass last resolved a query (after 8 such calls
   // cat_count_kernel is skipped -- every query then goes to the replay anyway -- and tried
@@ -1068,6 +1071,7 @@ int index_create_impl(int device, int64_t n_nodes, int32_t dim, const float* mea
     ibfs[i] = (int)nd;
     ihs[i] = sents[nd].empty() ? 0 : 1;
     inch[i] = nchild[nd];
+    ix->max_fanout = std::max(ix->max_fanout, (int)nchild[nd]);
     w_int[i] = (float)wdepth(depth[nd]);
     cb[i] = ce[i] = -1;
     la0[i] = la1[i] = lb0[i] = lb1[i] = -1;
@@ -3043,6 +3047,7 @@ int stream_cat_list(cwq_index* ix, Chunk& c, const float* q, int nqc, int R, con
 
 constexpr int kCatCountRetry = 16;   // (cwq_index::cat_count_idle)
 constexpr int kCatExplore = 32, kCatDenseMemory = 64;   // (cwq_index::cat_ema_*)
+constexpr int kLzFanout = 1024;   // batches try the lazy path when no node has more children
 int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_t max_nodes, int64_t* nodes,
                     int32_t* n_found, int64_t* n_calls, hipStream_t s, bool allow_filter) {
   const float dfull = (float)((double)ix->D * (double)logf(2.0f * (float)M_PI));
@@ -3085,7 +3090,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
   const char* cde = getenv("CWQ_CAT_DIRECT");
   const int cdv = cde && *cde ? atoi(cde) : -1;
   const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
-  const bool direct_ok = nq <= 64 && nq <= cq && ix->NI > 0 && ix->DP <= 2048;
+  const int pk = nq <= 64 ? 0 : 1;   // the policy slot: small call / batch
+  const bool direct_ok = (pk == 1 || nq <= cq) && ix->NI > 0 && ix->DP <= 2048;
   const bool top = allow_filter;   // (not the filter-overflow re-run of a call)
   const bool measure = direct_ok && cdv < 0 && top;
   bool direct = false;
@@ -3093,13 +3099,14 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     if (cdv >= 0) {
       direct = cdv == 1;
     } else if (!top) {
-      direct = ix->cat_pref_direct;
+      direct = ix->cat_pref_direct[pk];
     } else {
-      ++ix->cat_pol_calls;
-      if (ix->cat_dense_seen <= 0) direct = false;               // the lists resolve this tree
-      else if (ix->cat_ema_direct < 0.0) direct = true;          // the first trial
-      else if (ix->cat_ema_list < 0.0) direct = false;
-      else direct = (ix->cat_ema_direct < ix->cat_ema_list) != (ix->cat_pol_calls % kCatExplore == 0);
+      ++ix->cat_pol_calls[pk];
+      const bool may = ix->cat_dense_seen > 0 || (pk == 1 && ix->max_fanout <= kLzFanout);
+      if (!may) direct = false;                                     // the lists resolve this tree
+      else if (ix->cat_ema_list[pk] < 0.0) direct = false;          // the lists first
+      else if (ix->cat_ema_direct[pk] < 0.0) direct = true;         // then one trial
+      else direct = (ix->cat_ema_direct[pk] < ix->cat_ema_list[pk]) != (ix->cat_pol_calls[pk] % kCatExplore == 0);
     }
   }
   const auto t_call = std::chrono::steady_clock::now();
@@ -3113,7 +3120,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     size_t need = chunk_bytes(ix, nq_pad) + (size_t)nq_pad * ((size_t)slabs * R * 12 + (size_t)R * 12 +
                                                               (size_t)cap_list * 16 + 12) + 17 * 256 +
                   (filt ? (size_t)nqf * filt_q + 4096 * 8 : 0);
-    if (direct) need += (size_t)nq_pad * ((size_t)cap_dense * 16 + 16) + 2 * 256;
+    if (direct && pk == 0) need += (size_t)nq_pad * ((size_t)cap_dense * 16 + 16) + 2 * 256;
     if (scat || small2)   // + the second list's stream pass, T2, lists and heap (the two-level replay in place)
       need += (scat ? 2 * stream_cat_bytes(ix, nqc) : 0) + (size_t)nq_pad * ((size_t)std::max(ix->NI, 1) * 4 + (size_t)slabs * R * 12 +
                                                                  (size_t)R * 12 + (size_t)cap2 * 16 + 16) + 32 * 256;
@@ -3129,22 +3136,16 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     int* orow = b.take<int>((size_t)nq_pad * R);
     HeapEnt* heap = b.take<HeapEnt>((size_t)nq_pad * cap_list);
     int* status = b.take<int>((size_t)nq_pad);
-    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
-    if ((rc = run_internal(ix, c, s, true, q + q0 * ix->D, direct ? -1 : (filt ? 1 : -1)))) return rc;
-    if (direct) {
-      // the exact replay straight away: every pushed entry scored when its parent is popped
-      HeapEnt* hd = b.take<HeapEnt>((size_t)nq_pad * cap_dense);
+    // the replay arguments every path shares (the tree; the per-chunk fields set by the caller)
+    auto base_args = [&]() {
       SimArgs sd;
       memset(&sd, 0, sizeof(sd));
-      sd.nq = nqc;
       sd.k = k;
-      sd.R = 0;
       sd.max_nodes = max_nodes;
       sd.NI = ix->NI;
       sd.NL = ix->NL;
-      sd.LPF = c.LPF ? c.LPF : ix->dummy;
-      sd.BF = c.BF ? c.BF : ix->dummy;
       sd.ldI = std::max(ix->NI, 1);
+      sd.complete = complete ? 1 : 0;
       sd.int_child_begin = ix->int_child_begin;
       sd.int_child_end = ix->int_child_end;
       sd.int_nchild = ix->int_nchild;
@@ -3157,14 +3158,8 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       sd.row_par = ix->row_par;
       sd.row_bfs = ix->row_bfs;
       sd.row_flags = ix->row_flags;
-      sd.heap = hd;
-      sd.heap_cap = cap_dense;
-      sd.out_nodes = nodes + q0 * k;
-      sd.n_found = n_found + q0;
-      sd.n_calls = n_calls ? n_calls + q0 : nullptr;
-      sd.status = status;
       sd.par_int = ix->par_int;
-      sd.X = c.X;
+      sd.X = nullptr;
       sd.DP = ix->DP;
       sd.Mf = ix->iso_Mf;
       sd.NL_iso = ix->NL_iso;
@@ -3173,12 +3168,134 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
       sd.ld_an = ix->ld_an;
       sd.meta = ix->row_meta;
       sd.dconst = dfull;
-      HIPCHK(launch_simulate_lazy_runs(sd, s));
-      sd.pre_status = 1;   // arena overflows: the global-heap form
-      HIPCHK(launch_simulate_lazy(sd, s));
-      ix->stats[4] += nqc;
-      ix->lazy_stats[0] += nqc;
+      return sd;
+    };
+    // the DENSE re-run of the chunk's queries `redo` (chunk-local indices): the exact heap replay
+    // (exact by construction), results scattered into the outputs
+    auto dense_rerun = [&](const std::vector<int>& redo) -> int {
+      ix->cat_tail_done = false;   // the DENSE re-run below writes after the last flag gather
+
+      // DENSE re-run: the exact heap replay of the hard queries (exact by construction).  By
+      // default lazily (simulate_lazy_kernel: a popped node's leaf rows scored when their
+      // parent is popped); CWQ_CAT_LAZY=0: every leaf row materialised first by the exact scan.
+      const char* lze = getenv("CWQ_CAT_LAZY");
+      const bool lazy = !(lze && *lze && atoi(lze) == 0) && ix->DP <= 2048;
+      const int64_t ldL = lazy ? 1 : std::max(ix->NL, 1);
+      const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
+      const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ldL * 4 +
+                           (size_t)cap_dense * 16 + 64 + (size_t)k * 8 + (size_t)ix->D * 4;
+      const int64_t sub = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q));
+      std::vector<float> hx;
+      for (size_t r0 = 0; r0 < redo.size(); r0 += sub) {
+        const int ns = (int)std::min<int64_t>(sub, (int64_t)redo.size() - (int64_t)r0);
+        const int64_t ns_pad = round_up(ns, kQPad);
+        // per hard query: dense keys, heap, then status / nodes[k] / found / calls
+        if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) +
+                              (size_t)ns_pad * ((size_t)ldL * 4 + cap_dense * 16 + 64 + (size_t)k * 8) + 16 * 256 +
+                              (size_t)ns_pad * ix->D * 4)))
+          return rc;
+        Bump b2(ix->ws, ix->ws_size);
+        Chunk c2;
+        carve_chunk(ix, b2, c2, ns);
+        float* qsub = b2.take<float>((size_t)ns * ix->D);
+        float* dense = b2.take<float>((size_t)ns_pad * ldL);
+        HeapEnt* heap2 = b2.take<HeapEnt>((size_t)ns_pad * cap_dense);
+        int* status2 = b2.take<int>(ns_pad);
+        int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
+        int* found2 = b2.take<int>(ns_pad);
+        int64_t* calls2 = b2.take<int64_t>(ns_pad);
+        std::vector<int64_t> gq(ns);   // global query index of each hard query
+        for (int i = 0; i < ns; ++i) gq[i] = q0 + redo[r0 + i];
+        if ((rc = ix->reserve_fb((size_t)ns * 8))) return rc;
+        int64_t* d_gq = (int64_t*)ix->fb;
+        HIPCHK(hipMemcpyAsync(d_gq, gq.data(), (size_t)ns * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(launch_copy_rows(q, ix->D, d_gq, qsub, ix->D, nullptr, ns, ix->D, s));
+        HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
+        if ((rc = run_internal(ix, c2, s))) return rc;
+        if (!lazy && (rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1,
+                                         nullptr, s)))
+          return rc;
+        SimArgs sd = base_args();
+        sd.pre_status = 0;   // every hard query replays (status2 is fresh scratch)
+        sd.nq = ns;
+        sd.R = 0;
+        sd.LPF = c2.LPF ? c2.LPF : ix->dummy;
+        sd.BF = c2.BF ? c2.BF : ix->dummy;
+        sd.dense_lpf = dense;
+        sd.ldL = ldL;
+        sd.heap = heap2;
+        sd.heap_cap = cap_dense;
+        sd.out_nodes = nodes2;
+        sd.n_found = found2;
+        sd.n_calls = calls2;
+        sd.status = status2;
+        if (lazy) {
+          sd.X = c2.X;
+          sd.DP = ix->DP;
+          sd.Mf = ix->iso_Mf;
+          sd.NL_iso = ix->NL_iso;
+          sd.anA = ix->an_A;
+          sd.anB = ix->an_B;
+          sd.ld_an = ix->ld_an;
+          sd.meta = ix->row_meta;
+          sd.dconst = dfull;
+          // the run-merge replay in LDS; a query that overflows its arena is re-run on the
+          // global heap (status 1 gates it; the second kernel writes status 0)
+          const char* lre = getenv("CWQ_CAT_LAZY_RUNS");
+          if (!(lre && *lre && atoi(lre) == 0)) {
+            HIPCHK(launch_simulate_lazy_runs(sd, s));
+            sd.pre_status = 1;
+          }
+          HIPCHK(launch_simulate_lazy(sd, s));
+          ix->lazy_stats[1] += ns;
+        } else {
+          HIPCHK(launch_simulate(sd, s));
+        }
+        HIPCHK(launch_copy_rows(nodes2, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_gq, ns, 2 * (int64_t)k, s));
+        HIPCHK(launch_copy_rows(found2, 1, nullptr, n_found, 1, d_gq, ns, 1, s));
+        if (n_calls) HIPCHK(launch_copy_rows(calls2, 2, nullptr, n_calls, 2, d_gq, ns, 2, s));
+        HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
+      }
+      return CWQ_OK;
+    };
+    HIPCHK(launch_pad_queries(q + q0 * ix->D, nqc, ix->D, c.X, c.nq_pad, ix->DP, s));
+    if ((rc = run_internal(ix, c, s, true, q + q0 * ix->D, direct ? -1 : (filt ? 1 : -1)))) return rc;
+    if (direct) {
+      // the exact replay straight away: every pushed entry scored when its parent is popped
+      SimArgs sd = base_args();
+      sd.nq = nqc;
+      sd.R = 0;
+      sd.LPF = c.LPF ? c.LPF : ix->dummy;
+      sd.BF = c.BF ? c.BF : ix->dummy;
+      sd.out_nodes = nodes + q0 * k;
+      sd.n_found = n_found + q0;
+      sd.n_calls = n_calls ? n_calls + q0 : nullptr;
+      sd.status = status;
+      sd.X = c.X;
       ix->cat_tail_done = false;
+      if (pk == 0) {   // a few queries: the global-heap form queued behind for arena overflows
+        sd.heap = b.take<HeapEnt>((size_t)nq_pad * cap_dense);
+        sd.heap_cap = cap_dense;
+        HIPCHK(launch_simulate_lazy_runs(sd, s));
+        sd.pre_status = 1;
+        HIPCHK(launch_simulate_lazy(sd, s));
+        ix->stats[4] += nqc;
+        ix->lazy_stats[0] += nqc;
+        continue;
+      }
+      // a batch: the run-merge replays side by side; a query that overflows its arena goes
+      // to the DENSE re-run (its heap memory only for those)
+      HIPCHK(launch_simulate_lazy_runs(sd, s));
+      std::vector<int> hst(nqc);
+      HIPCHK(hipMemcpyAsync(hst.data(), status, (size_t)nqc * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      std::vector<int> redo;
+      for (int i = 0; i < nqc; ++i)
+        if (hst[i]) redo.push_back(i);
+      ix->stats[4] += nqc - (int64_t)redo.size();
+      ix->lazy_stats[0] += nqc - (int64_t)redo.size();
+      ix->stats[1] += (int64_t)redo.size();
+      if (!redo.empty() && (rc = dense_rerun(redo))) return rc;
       continue;
     }
     if (filt && (rc = group_tables(ix, c, q + q0 * ix->D, true, s))) return rc;
@@ -3479,92 +3596,7 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     ix->stats[1] += (int64_t)redo.size();
     n_dense_call += (int64_t)redo.size();
     if (redo.empty()) continue;
-    ix->cat_tail_done = false;   // the DENSE re-run below writes after the last flag gather
-
-    // DENSE re-run: the exact heap replay of the hard queries (exact by construction).  By
-    // default lazily (simulate_lazy_kernel: a popped node's leaf rows scored when their
-    // parent is popped); CWQ_CAT_LAZY=0: every leaf row materialised first by the exact scan.
-    const char* lze = getenv("CWQ_CAT_LAZY");
-    const bool lazy = !(lze && *lze && atoi(lze) == 0) && ix->DP <= 2048;
-    const int64_t ldL = lazy ? 1 : std::max(ix->NL, 1);
-    const int64_t cap_dense = 1 + (int64_t)ix->NI + ix->NL;
-    const size_t per_q = (size_t)ix->DP * 4 + 4 * (size_t)std::max(ix->NI, 1) * 4 + (size_t)ldL * 4 +
-                         (size_t)cap_dense * 16 + 64 + (size_t)k * 8 + (size_t)ix->D * 4;
-    const int64_t sub = std::max<int64_t>(1, std::min<int64_t>((int64_t)redo.size(), ((size_t)2 << 30) / per_q));
-    std::vector<float> hx;
-    for (size_t r0 = 0; r0 < redo.size(); r0 += sub) {
-      const int ns = (int)std::min<int64_t>(sub, (int64_t)redo.size() - (int64_t)r0);
-      const int64_t ns_pad = round_up(ns, kQPad);
-      // per hard query: dense keys, heap, then status / nodes[k] / found / calls
-      if ((rc = ix->reserve(chunk_bytes(ix, ns_pad) +
-                            (size_t)ns_pad * ((size_t)ldL * 4 + cap_dense * 16 + 64 + (size_t)k * 8) + 16 * 256 +
-                            (size_t)ns_pad * ix->D * 4)))
-        return rc;
-      Bump b2(ix->ws, ix->ws_size);
-      Chunk c2;
-      carve_chunk(ix, b2, c2, ns);
-      float* qsub = b2.take<float>((size_t)ns * ix->D);
-      float* dense = b2.take<float>((size_t)ns_pad * ldL);
-      HeapEnt* heap2 = b2.take<HeapEnt>((size_t)ns_pad * cap_dense);
-      int* status2 = b2.take<int>(ns_pad);
-      int64_t* nodes2 = b2.take<int64_t>((size_t)ns_pad * k);
-      int* found2 = b2.take<int>(ns_pad);
-      int64_t* calls2 = b2.take<int64_t>(ns_pad);
-      std::vector<int64_t> gq(ns);   // global query index of each hard query
-      for (int i = 0; i < ns; ++i) gq[i] = q0 + redo[r0 + i];
-      if ((rc = ix->reserve_fb((size_t)ns * 8))) return rc;
-      int64_t* d_gq = (int64_t*)ix->fb;
-      HIPCHK(hipMemcpyAsync(d_gq, gq.data(), (size_t)ns * 8, hipMemcpyHostToDevice, s));
-      HIPCHK(launch_copy_rows(q, ix->D, d_gq, qsub, ix->D, nullptr, ns, ix->D, s));
-      HIPCHK(launch_pad_queries(qsub, ns, ix->D, c2.X, c2.nq_pad, ix->DP, s));
-      if ((rc = run_internal(ix, c2, s))) return rc;
-      if (!lazy && (rc = run_leaf_scan(ix, c2, EPI_KEY, true, 16, dfull, dense, ix->NL, nullptr, nullptr, nullptr, 1,
-                                       nullptr, s)))
-        return rc;
-      SimArgs sd = sa;
-      sd.pre_status = 0;   // every hard query replays (status2 is fresh scratch)
-      sd.nq = ns;
-      sd.R = 0;
-      sd.LPF = c2.LPF ? c2.LPF : ix->dummy;
-      sd.BF = c2.BF ? c2.BF : ix->dummy;
-      sd.dense_lpf = dense;
-      sd.ldL = ldL;
-      sd.lkey = okey;
-      sd.laux = oaux;
-      sd.lrow = orow;
-      sd.heap = heap2;
-      sd.heap_cap = cap_dense;
-      sd.out_nodes = nodes2;
-      sd.n_found = found2;
-      sd.n_calls = calls2;
-      sd.status = status2;
-      if (lazy) {
-        sd.X = c2.X;
-        sd.DP = ix->DP;
-        sd.Mf = ix->iso_Mf;
-        sd.NL_iso = ix->NL_iso;
-        sd.anA = ix->an_A;
-        sd.anB = ix->an_B;
-        sd.ld_an = ix->ld_an;
-        sd.meta = ix->row_meta;
-        sd.dconst = dfull;
-        // the run-merge replay in LDS; a query that overflows its arena is re-run on the
-        // global heap (status 1 gates it; the second kernel writes status 0)
-        const char* lre = getenv("CWQ_CAT_LAZY_RUNS");
-        if (!(lre && *lre && atoi(lre) == 0)) {
-          HIPCHK(launch_simulate_lazy_runs(sd, s));
-          sd.pre_status = 1;
-        }
-        HIPCHK(launch_simulate_lazy(sd, s));
-        ix->lazy_stats[1] += ns;
-      } else {
-        HIPCHK(launch_simulate(sd, s));
-      }
-      HIPCHK(launch_copy_rows(nodes2, 2 * (int64_t)k, nullptr, nodes, 2 * (int64_t)k, d_gq, ns, 2 * (int64_t)k, s));
-      HIPCHK(launch_copy_rows(found2, 1, nullptr, n_found, 1, d_gq, ns, 1, s));
-      if (n_calls) HIPCHK(launch_copy_rows(calls2, 2, nullptr, n_calls, 2, d_gq, ns, 2, s));
-      HIPCHK(hipStreamSynchronize(s));   // gq (pageable host memory) must outlive the upload
-    }
+    if ((rc = dense_rerun(redo))) return rc;
   }
   if (measure && !direct) ix->cat_dense_seen = n_dense_call > 0 ? kCatDenseMemory : std::max(0, ix->cat_dense_seen - 1);
   ix->stats[2] += (int64_t)fredo.size();
@@ -3602,9 +3634,10 @@ int categorize_impl(cwq_index* ix, const float* q, int64_t nq, int32_t k, int64_
     HIPCHK(hipStreamSynchronize(s));
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count() /
                       (double)nq;
-    double& ema = direct ? ix->cat_ema_direct : ix->cat_ema_list;
+    double& ema = direct ? ix->cat_ema_direct[pk] : ix->cat_ema_list[pk];
     ema = ema < 0.0 ? us : 0.75 * ema + 0.25 * us;
-    ix->cat_pref_direct = ix->cat_ema_direct >= 0.0 && ix->cat_ema_list >= 0.0 && ix->cat_ema_direct < ix->cat_ema_list;
+    ix->cat_pref_direct[pk] = ix->cat_ema_direct[pk] >= 0.0 && ix->cat_ema_list[pk] >= 0.0 &&
+                              ix->cat_ema_direct[pk] < ix->cat_ema_list[pk];
   }
   return CWQ_OK;
 }

@@ -29,3 +29,12 @@ def pkg():
     """The product package (directory rag-cobweb_amd/, imported as rag_cobweb_amd)."""
     import cobweb_pkg
     return cobweb_pkg.load()
+
+
+@pytest.fixture(autouse=True)
+def _categorize_list_paths(monkeypatch):
+    """Basic's path choice (cwq_api.hip categorize_impl) is measured at run time: a call may go
+    straight to the exact lazy replay instead of the list paths.  The tests that check a
+    particular resolution path (counting, replay, two-level, DENSE) pin the list paths; the
+    tests of the automatic choice (tests/test_gpu_cut.py) clear this themselves."""
+    monkeypatch.setenv("CWQ_CAT_DIRECT", "0")

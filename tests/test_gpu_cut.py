@@ -231,12 +231,13 @@ def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
 @pytest.mark.parametrize("shape", ["nested ties", "ifit"])
 def test_direct_lazy_replay(gpu, monkeypatch, shape):
     """Basic straight through the exact lazy replay (CWQ_CAT_DIRECT=1: the list paths
-    skipped) against the list paths (CWQ_CAT_DIRECT=0), one and eight queries per call, on
+    skipped) against the list paths (CWQ_CAT_DIRECT=0), one and eight queries per call and a
+    160-query batch, on
     the nested-tie tree and on a device-ifit clustered tree; the automatic choice tries the
     lazy path only after the lists left a query to the DENSE re-run, then keeps the faster."""
     import random
     if shape == "nested ties":
-        t, Q = broad_tree(gpu, 30_000, 96, (4, 30), 65, direct=0.02, nq=64)
+        t, Q = broad_tree(gpu, 30_000, 96, (4, 30), 65, direct=0.02, nq=160)
         ix = make_index(gpu, t, monkeypatch)
     else:
         rng = np.random.default_rng(66)
@@ -246,7 +247,7 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
         w = gpu.CobwebWrapper(corpus=None, corpus_embeddings=X)
         w.build_prediction_index()
         ix = w._index
-        Q = torch.from_numpy((X[:64] + 0.05 * rng.standard_normal((64, 64))).astype(np.float32)).cuda()
+        Q = torch.from_numpy((X[:160] + 0.05 * rng.standard_normal((160, 64))).astype(np.float32)).cuda()
     for k, mx in ((10, 100000), (4, 60)):
         for m in (1, 8):
             for a in range(0, 32, m):
@@ -258,6 +259,15 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
                 assert ix.last_lazy_stats()["direct"] == m
                 for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
                     assert torch.equal(x, y), (shape, k, mx, m, a, name)
+        # a batch (> 64 queries): the run-merge replays side by side, arena overflows DENSE
+        monkeypatch.setenv("CWQ_CAT_DIRECT", "0")
+        ref = ix.categorize(Q, k, mx)
+        monkeypatch.setenv("CWQ_CAT_DIRECT", "1")
+        got = ix.categorize(Q, k, mx)
+        lz, st = ix.last_lazy_stats(), ix.last_categorize_stats()
+        assert lz["direct"] + st["dense_reruns"] == Q.shape[0], (lz, st)
+        for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
+            assert torch.equal(x, y), (shape, k, mx, "batch", name)
     monkeypatch.delenv("CWQ_CAT_DIRECT")
     # a fresh index for the automatic rule (the calls above fed the old one's record)
     if shape == "nested ties":
@@ -269,8 +279,19 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
         ix = w._index
     seen = []
     for i in range(6):
-        ix.categorize(Q[i:i + 1].contiguous(), 10, 100000)
+        got = ix.categorize(Q[i:i + 1].contiguous(), 10, 100000)
         seen.append((ix.last_categorize_stats()["dense_reruns"], ix.last_lazy_stats()["direct"]))
+        monkeypatch.setenv("CWQ_CAT_DIRECT", "0")
+        ref = ix.categorize(Q[i:i + 1].contiguous(), 10, 100000)
+        monkeypatch.delenv("CWQ_CAT_DIRECT")
+        assert all(torch.equal(x, y) for x, y in zip(ref, got)), (shape, i)
+    # batches under the automatic choice: the same results whichever path it takes
+    for i in range(4):
+        got = ix.categorize(Q, 10, 100000)
+        monkeypatch.setenv("CWQ_CAT_DIRECT", "0")
+        ref = ix.categorize(Q, 10, 100000)
+        monkeypatch.delenv("CWQ_CAT_DIRECT")
+        assert all(torch.equal(x, y) for x, y in zip(ref, got)), (shape, "batch", i)
     print(shape, seen)
     # the rule: the lazy path is tried only after a list-path call left a query to DENSE; then
     # the faster of the two (measured) is taken
