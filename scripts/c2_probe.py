@@ -57,6 +57,10 @@ def main():
     ap.add_argument("--load-struct", default=None,
                     help="skip ifit: the tree structure from a --save-struct file, node statistics by batch "
                          "Welford over the same corpus (synth.tree_synth) -- the same shape for the query legs")
+    ap.add_argument("--save-load", default=None,
+                    help="round-trip the ifit tree (full stats: count / mean / meanSq) through the F2 .npz "
+                         "(CobwebWrapper.save_binary / load_binary) at this path, check the loaded stats equal "
+                         "the ifit's bit for bit, and run the query legs on the loaded wrapper")
     ap.add_argument("--index-env", default=None,
                     help="';'-separated variants of '&'-separated KEY=VAL set at index creation (e.g. "
                          "'CWQ_GROUP_CUT=1;' = the depth-1 cut, then the default): the index is rebuilt from "
@@ -105,6 +109,22 @@ def main():
     torch.cuda.synchronize()
     t_ix = time.perf_counter() - t0
     ix = w._index
+    if args.save_load and not args.load_struct:
+        t0 = time.perf_counter()
+        w.save_binary(args.save_load)
+        w2 = pkg.CobwebWrapper.load_binary(args.save_load)
+        a1, a2 = w.tree.to_arrays(), w2.tree.to_arrays()
+        same = all(np.array_equal(a1[key], a2[key]) for key in ("parent", "count", "mean", "meanSq", "sid_ptr", "sid_list"))
+        assert same, "loaded tree differs from the ifit tree"
+        w2.build_prediction_index()
+        torch.cuda.synchronize()
+        print(f"tree round trip through {args.save_load}: {os.path.getsize(args.save_load) / 1e6:.0f} MB, "
+              f"stats equal to the ifit's: {same} ({time.perf_counter() - t0:.1f} s); the legs run on the loaded tree",
+              flush=True)
+        os.remove(args.save_load)
+        w._invalidate_prediction_index()
+        w = w2
+        ix = w._index
     if args.save_struct:
         nodes, parent, _, _, nos, _ = w.tree.flatten(args.n)
         np.savez_compressed(args.save_struct, parent=parent.astype(np.int32), node_of_sentence=nos.astype(np.int32))
