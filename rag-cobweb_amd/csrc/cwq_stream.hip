@@ -73,7 +73,7 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 // internal k order inside a fragment does not matter for the dot product.
 // CH: K fragments per load chunk (8; 12 for int8 rows of 12 fragments, D = 768, so that no
 // chunk is partial and every wave keeps a whole chunk of HBM loads in flight).
-template <int MODE, int MQB, bool I8 = false, int CH = SK_CH>
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false>
 __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   static_assert(!I8 || MODE == 0, "int8 operands: filter pass only");
   typedef typename std::conditional<I8, i32x4, bf16x8>::type frag_t;
@@ -262,7 +262,13 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   frag_t bA[CH], bB[CH];
   auto issue = [&](frag_t (&b)[CH], const char* p, int nfr) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const frag_t*>(p + min(i, nfr - 1) * 64);
+    for (int i = 0; i < CH; ++i) {
+      const frag_t* pp = reinterpret_cast<const frag_t*>(p + min(i, nfr - 1) * 64);
+      if constexpr (NT)   // read once: nontemporal (the guide's streamed-once policy)
+        b[i] = __builtin_nontemporal_load(pp);
+      else
+        b[i] = *pp;
+    }
   };
   acc_t acc[MQB];
 #pragma unroll
@@ -601,12 +607,13 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   }
 }
 
-template <int MODE, int MQB, bool I8 = false, int CH = SK_CH>
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false>
 static hipError_t launch_one(const StreamArgs& a, int n_wg, size_t lds, hipStream_t s) {
   // dynamic LDS above the 64 KiB default (once per kernel and device, thread-safe)
-  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH>), kStreamMaxLds))
+  if (hipError_t e =
+          ensure_dyn_lds(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH, NT>), kStreamMaxLds))
     return e;
-  hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH>), dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
+  hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH, NT>), dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
   return hipGetLastError();
 }
 
@@ -614,8 +621,14 @@ template <int MQB>
 static hipError_t launch_mqb(const StreamArgs& a, int mode, bool i8, bool ch12, int n_wg, size_t lds, hipStream_t s) {
   if (mode == 1) return launch_one<1, MQB>(a, n_wg, lds, s);
   if (mode == 2) return launch_one<2, MQB>(a, n_wg, lds, s);
-  if (i8) return ch12 ? launch_one<0, MQB, true, 12>(a, n_wg, lds, s) : launch_one<0, MQB, true>(a, n_wg, lds, s);
-  return launch_one<0, MQB>(a, n_wg, lds, s);
+  // CWQ_STREAM_NT=1: the filter pass's row panel by nontemporal loads (A/B knob)
+  const char* ne = getenv("CWQ_STREAM_NT");
+  const bool ntc = ne && *ne && atoi(ne) != 0;
+  if (i8) {
+    if (ch12) return ntc ? launch_one<0, MQB, true, 12, true>(a, n_wg, lds, s) : launch_one<0, MQB, true, 12>(a, n_wg, lds, s);
+    return launch_one<0, MQB, true>(a, n_wg, lds, s);
+  }
+  return ntc ? launch_one<0, MQB, false, SK_CH, true>(a, n_wg, lds, s) : launch_one<0, MQB>(a, n_wg, lds, s);
 }
 
 hipError_t launch_stream(const StreamArgs& a, int mode, int n_wg, hipStream_t s) {

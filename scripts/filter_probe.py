@@ -31,7 +31,7 @@ def main():
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
     if args.balanced:
-        b, lv = (int(v) for v in args.balanced.split(","))
+        b, lv = (int(v) for v in args.balanced.replace("x", ",").split(","))
         fs = pkg.synth.balanced_synth(X, b, lv)
         print(f"balanced tree: branching {b}, depth {lv}: {fs['n_internal']} internal nodes", flush=True)
     elif args.clusters:
@@ -42,6 +42,7 @@ def main():
     else:
         fs = pkg.synth.flat_synth(X)
     ix = pkg.index.CobwebIndex(fs["mean"], fs["var"], fs["parent"], fs["node_of_sentence"], device=dev)
+    print(f"filter rows {ix.filter_info()}; cut {ix.cut_info()}", flush=True)
     del fs
     Q, _ = pkg.synth.synthetic_queries(X, args.queries, seed=1)
     del X

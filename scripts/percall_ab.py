@@ -39,7 +39,7 @@ def main():
     dev = torch.device("cuda", 0)
     X = pkg.synth.synthetic_corpus(args.n, args.dim, seed=0, device=dev)
     if args.balanced:
-        b, L = (int(v) for v in args.balanced.split(","))
+        b, L = (int(v) for v in args.balanced.replace("x", ",").split(","))
         fs = pkg.synth.balanced_synth(X, b, L, seed=1)
     else:
         fs = pkg.synth.flat_synth(X)
