@@ -1930,11 +1930,16 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
 // Wave 0 runs the frontier; the other waves join only to score a popped node's leaf rows (64
 // per round).  An arena or run-slot overflow sets status 1: simulate_lazy_kernel (global
 // 64-ary heap) re-runs the query.
-constexpr int kLzArena = 3072, kLzThreads = 256;
+constexpr int kLzArena = 2560, kLzThreads = 256;   // 24-B entries: 60 KiB, two workgroups per CU at D = 768
 constexpr int kLzSlots = 8;   // run heads per lane: 512 live runs (a row run and a child run per internal pop)
-struct alignas(16) LzRec {
-  int cb, ce, nch, hs;   // internal: child range and count; has_sent
+struct alignas(8) LzRec {   // internal: first child, then (children - first) | nch << 16 | has_sent << 31
+  int cb;
+  uint32_t pk;
 };
+__device__ __forceinline__ LzRec lz_rec(int cb, int ce, int nch, int hs) {
+  return LzRec{cb, (uint32_t)(ce - cb) | ((uint32_t)nch << 16) | ((uint32_t)hs << 31)};
+}
+__device__ __forceinline__ bool lz_fits(int cb, int ce, int nch) { return ce - cb <= 0xffff && nch <= 0x7fff; }
 size_t lazy_runs_lds(int DP) {
   return (size_t)kLzArena * (sizeof(HeapEnt) + sizeof(LzRec)) + (size_t)DP * 4 + (size_t)64 * (DP / 16 + 1) * 4;
 }
@@ -1993,12 +1998,12 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
   int ra = 0, rae = 0, rb = 0, rbe = 0;
   int job_r0 = 0, job_m = 0, job_iso = 0;   // the chunk just scored (wave 0 ranks it)
   if (wave == 0) {
-    if (a.NI <= 0) {
-      status = 1;   // single-node tree: simulate_lazy_kernel
+    if (a.NI <= 0 || !lz_fits(a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0])) {
+      status = 1;   // single-node tree / a root too wide for its record: simulate_lazy_kernel
     } else {
       if (lane == 0) {
         ae[0] = HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0};
-        ax[0] = LzRec{a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0], a.int_has_sent[0] != 0 ? 1 : 0};
+        ax[0] = lz_rec(a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0], a.int_has_sent[0] != 0 ? 1 : 0);
       }
       an = 1;
       LZ_ADD_RUN(0, 1, a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0]);
@@ -2029,7 +2034,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
           } else {
             if (ok) {
               ae[an + rk] = HeapEnt{lp, pend_ps, tb, -(r + 1)};
-              ax[an + rk] = LzRec{0, 0, 0, (a.row_flags[r] & FLAG_HAS_SENT) != 0 ? 1 : 0};
+              ax[an + rk] = lz_rec(0, 0, 0, (a.row_flags[r] & FLAG_HAS_SENT) != 0 ? 1 : 0);
             }
             const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
             LZ_ADD_RUN(an, an + nr, rl_f(lp, hl), pend_ps, rl_i(tb, hl));
@@ -2096,7 +2101,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
           done = true;
           break;
         }
-        if (x.hs) {
+        if (x.pk >> 31) {
           if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
           ++found;
         }
@@ -2106,8 +2111,8 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
         }
         if (e.node < 0) continue;
         const int u = e.node;
-        const int cb = x.cb, ce = x.ce;
-        calls += x.nch;
+        const int cb = x.cb, ce = x.cb + (int)(x.pk & 0xffffu);
+        calls += (int)((x.pk >> 16) & 0x7fffu);
         if (an + (ce - cb) > kLzArena || nruns + (ce - cb + 63) / 64 > 64 * kLzSlots) {
           status = 1;
           done = true;
@@ -2122,6 +2127,11 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
           const int ccb = ok ? a.int_child_begin[c] : 0, cce = ok ? a.int_child_end[c] : 0;
           const int cnc = ok ? a.int_nchild[c] : 0;
           const int m = min(64, ce - c0);
+          if (__ballot(ok && !lz_fits(ccb, cce, cnc))) {   // a child too wide for its record
+            status = 1;
+            done = true;
+            break;
+          }
           const float lc = lpf == lpf ? lpf : -CWQ_INF;
           int rk = 0;
           for (int j = 0; j < m; ++j) {
@@ -2131,7 +2141,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
           }
           if (ok) {
             ae[an + rk] = HeapEnt{lpf, e.score, tb, c};
-            ax[an + rk] = LzRec{ccb, cce, cnc, hs};
+            ax[an + rk] = lz_rec(ccb, cce, cnc, hs);
           }
           const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
           LZ_ADD_RUN(an, an + m, rl_f(lpf, hl), e.score, rl_i(tb, hl));
