@@ -2215,13 +2215,338 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
 }
 #undef LZ_ADD_RUN
 
+
+// The lazy replay with every pop's loads in one round trip (round 6): as
+// simulate_lazy_runs_kernel, but an internal entry carries its leaf-row ranges in the arena
+// (read with the child's other fields when its parent is popped), so a popped node's rows
+// are scored while wave 0 pushes its internal children -- the row panel (Mf), the rows'
+// meta / flags / BFS indices and the children's fields all in flight together.  Same pushes,
+// same total order, so the same pops, retrievals and call counts.  40-B entries: one
+// workgroup per CU at D = 768 (the packed kernel fits two), so the choice is by batch size.
+constexpr int kLpArena = 2560;
+size_t lazy_pre_lds(int DP) {
+  return (size_t)kLpArena * (sizeof(HeapEnt) + sizeof(LzRec) + sizeof(int4)) + (size_t)DP * 4 +
+         (size_t)64 * (DP / 16 + 1) * 4;
+}
+
+__global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const SimArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lp_s[];
+  HeapEnt* ae = reinterpret_cast<HeapEnt*>(lp_s);
+  int4* ar = reinterpret_cast<int4*>(ae + kLpArena);     // internal: iso rows [x, y), aniso rows [z, w)
+  LzRec* ax = reinterpret_cast<LzRec*>(ar + kLpArena);
+  float* s_x = reinterpret_cast<float*>(ax + kLpArena);   // [DP]
+  float* s_part = s_x + a.DP;                             // [64][NV16 + 1]
+  __shared__ float s_lp[64];
+  __shared__ int s_job[4];   // [0] 0: score rows, 1: done; [1] first row; [2] rows; [3] 1: isotropic
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x;
+  if (q >= a.nq) return;
+  if (a.pre_status && a.status[q] == 0) return;
+  const int NV16 = a.DP / 16, LDP = NV16 + 1;
+  {
+    const float* xq = a.X + ((size_t)(q / kXQ) * NV16 * kXQ + (q % kXQ)) * 16;
+    for (int d = tid; d < a.DP; d += kLzThreads) s_x[d] = xq[(size_t)(d >> 4) * kXQ * 16 + (d & 15)];
+  }
+  uint64_t hk[kLzSlots];
+  int htb[kLzSlots], hix[kLzSlots], hend[kLzSlots];
+#pragma unroll
+  for (int j = 0; j < kLzSlots; ++j) {
+    hk[j] = 0;
+    htb[j] = hix[j] = hend[j] = 0;
+  }
+  int nruns = 0, an = 0;
+#define LP_ADD_RUN(i0, i1, sc, ps, tb)                    \
+  do {                                                    \
+    bool fr_ = false;                                     \
+    _Pragma("unroll") for (int j_ = 0; j_ < kLzSlots; ++j_) fr_ |= hk[j_] == 0; \
+    const uint64_t fm_ = __ballot(fr_);                   \
+    const uint64_t nk_ = head_key((sc), (ps));            \
+    const int tb_ = (tb), i0_ = (i0), i1_ = (i1);         \
+    if (lane == __builtin_ctzll(fm_)) {                   \
+      bool done_ = false;                                 \
+      _Pragma("unroll") for (int j_ = 0; j_ < kLzSlots; ++j_) { \
+        const bool put_ = !done_ && hk[j_] == 0;          \
+        hk[j_] = put_ ? nk_ : hk[j_];                     \
+        htb[j_] = put_ ? tb_ : htb[j_];                   \
+        hix[j_] = put_ ? i0_ : hix[j_];                   \
+        hend[j_] = put_ ? i1_ : hend[j_];                 \
+        done_ |= put_;                                    \
+      }                                                   \
+    }                                                     \
+    ++nruns;                                              \
+  } while (0)
+  int status = 0, found = 0;
+  int64_t calls = 1, visited = 0;
+  float pend_ps = 0.f;
+  int ra = 0, rae = 0, rb = 0, rbe = 0;
+  int job_r0 = 0, job_m = 0, job_iso = 0;
+  // the popped node whose internal children wave 0 pushes while the other waves score its rows
+  int dcb = 0, dce = 0;
+  float dsc = 0.f;
+  bool defer = false;
+  // wave 0, lane e of a job: row job_r0 + e's flags, BFS index and meta (loaded with the panel)
+  int jflag = 0, jbfs = 0;
+  RowMeta jmeta{};
+  // push the internal children [cb, ce) of a node popped with score sc: one run per 64
+  auto push_children = [&](int cb, int ce, float sc) {
+    for (int c0 = cb; c0 < ce; c0 += 64) {
+      const int c = c0 + lane;
+      const bool ok = c < ce;
+      const float lpf = ok ? a.LPF[(size_t)q * a.ldI + c] : 0.f;
+      const int tb = ok ? a.int_bfs[c] : 0;
+      const int hs = ok ? (a.int_has_sent[c] != 0 ? 1 : 0) : 0;
+      const int ccb = ok ? a.int_child_begin[c] : 0, cce = ok ? a.int_child_end[c] : 0;
+      const int cnc = ok ? a.int_nchild[c] : 0;
+      const int4 rr = ok ? make_int4(a.int_leaf_a0[c], a.int_leaf_a1[c], a.int_leaf_b0[c], a.int_leaf_b1[c])
+                         : make_int4(0, 0, 0, 0);
+      const int m = min(64, ce - c0);
+      if (__ballot(ok && !lz_fits(ccb, cce, cnc))) {   // a child too wide for its record
+        status = 1;
+        return;
+      }
+      const float lc = lpf == lpf ? lpf : -CWQ_INF;
+      int rk = 0;
+      for (int j = 0; j < m; ++j) {
+        const float sj = rl_f(lc, j);
+        const int tj = rl_i(tb, j);
+        rk += sj > lc || (sj == lc && tj < tb);
+      }
+      if (ok) {
+        ae[an + rk] = HeapEnt{lpf, sc, tb, c};
+        ax[an + rk] = lz_rec(ccb, cce, cnc, hs);
+        ar[an + rk] = rr;
+      }
+      const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
+      LP_ADD_RUN(an, an + m, rl_f(lpf, hl), sc, rl_i(tb, hl));
+      an += m;
+    }
+  };
+  if (wave == 0) {
+    if (a.NI <= 0 || !lz_fits(a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0])) {
+      status = 1;   // single-node tree / a root too wide for its record: simulate_lazy_kernel
+    } else {
+      if (lane == 0) {
+        ae[0] = HeapEnt{a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0], 0};
+        ax[0] = lz_rec(a.int_child_begin[0], a.int_child_end[0], a.int_nchild[0], a.int_has_sent[0] != 0 ? 1 : 0);
+        ar[0] = make_int4(a.int_leaf_a0[0], a.int_leaf_a1[0], a.int_leaf_b0[0], a.int_leaf_b1[0]);
+      }
+      an = 1;
+      LP_ADD_RUN(0, 1, a.LPF[(size_t)q * a.ldI], 0.f, a.int_bfs[0]);
+    }
+  }
+  for (;;) {
+    if (wave == 0) {
+      bool need = false, done = status != 0;
+      if (!done && job_m > 0) {
+        // the scored chunk: isotropic rows sum their partials here (slice order), anisotropic
+        // ones come from s_lp; rank it (one pscore: by score, then BFS index), write it as a run
+        const int r = job_r0 + lane;
+        const bool in = lane < job_m;
+        float lp = 0.f;
+        if (in) {
+          if (job_iso) {
+            float acc = 0.f;
+            for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+            (void)iso_key_tail(acc, jmeta, CWQ_INF, lp, 1, a.dconst);
+          } else {
+            lp = s_lp[lane];
+          }
+        }
+        const bool ok = in && !(jflag & FLAG_INT_COPY);
+        const float lc = lp == lp ? lp : -CWQ_INF;
+        const int tb = ok ? jbfs : 0;
+        const uint64_t bm = __ballot(ok);
+        int rk = 0;
+        for (uint64_t mm = bm; mm;) {
+          const int j = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          rk += rank_before(rl_f(lc, j), rl_i(tb, j), lc, tb);
+        }
+        const int nr = __popcll(bm);
+        if (nr > 0) {
+          if (an + nr > kLpArena || nruns + 1 > 64 * kLzSlots) {
+            status = 1;
+            done = true;
+          } else {
+            if (ok) {
+              ae[an + rk] = HeapEnt{lp, pend_ps, tb, -(r + 1)};
+              ax[an + rk] = lz_rec(0, 0, 0, (jflag & FLAG_HAS_SENT) != 0 ? 1 : 0);
+            }
+            const int hl = __builtin_ctzll(__ballot(ok && rk == 0));
+            LP_ADD_RUN(an, an + nr, rl_f(lp, hl), pend_ps, rl_i(tb, hl));
+            an += nr;
+          }
+        }
+        job_m = 0;
+      }
+      if (!done && ra < rae) {
+        job_r0 = ra;
+        job_m = min(64, rae - ra);
+        job_iso = 1;
+        ra += job_m;
+        need = true;
+      } else if (!done && rb < rbe) {
+        job_r0 = rb;
+        job_m = min(64, rbe - rb);
+        job_iso = 0;
+        rb += job_m;
+        need = true;
+      }
+      while (!done && !need) {
+        if (nruns <= 0) {
+          done = true;
+          break;
+        }
+        uint64_t bk = 0;
+        int btb = 0x7fffffff, bj = -1, bix = 0, bend = 0;
+#pragma unroll
+        for (int j = 0; j < kLzSlots; ++j) {
+          const bool bt = hk[j] > bk || (hk[j] == bk && hk[j] != 0 && htb[j] < btb);
+          bk = bt ? hk[j] : bk;
+          btb = bt ? htb[j] : btb;
+          bj = bt ? j : bj;
+          bix = bt ? hix[j] : bix;
+          bend = bt ? hend[j] : bend;
+        }
+        const int wl = wave_first(bk, btb);
+        if (wl < 0) {
+          status = 1;
+          done = true;
+          break;
+        }
+        const int idx = __builtin_amdgcn_readlane(bix, wl), iend = __builtin_amdgcn_readlane(bend, wl);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const HeapEnt e = ae[idx];
+        const LzRec x = ax[idx];
+        const bool more = idx + 1 < iend;
+        const HeapEnt nx = more ? ae[idx + 1] : HeapEnt{0.f, 0.f, 0, 0};
+        const uint64_t nk = more ? head_key(nx.score, nx.pscore) : 0;
+#pragma unroll
+        for (int j = 0; j < kLzSlots; ++j) {
+          const bool adv = lane == wl && bj == j;
+          hk[j] = adv ? nk : hk[j];
+          htb[j] = adv ? nx.tb : htb[j];
+          hix[j] = adv ? idx + 1 : hix[j];
+        }
+        if (!more) --nruns;
+        ++visited;
+        if (visited >= a.max_nodes) {
+          done = true;
+          break;
+        }
+        if (x.pk >> 31) {
+          if (found < a.k && lane == 0) a.out_nodes[(size_t)q * a.k + found] = e.tb;
+          ++found;
+        }
+        if (found == a.k) {
+          done = true;
+          break;
+        }
+        if (e.node < 0) continue;
+        const int4 rr = ar[idx];
+        const int cb = x.cb, ce = x.cb + (int)(x.pk & 0xffffu);
+        calls += (int)((x.pk >> 16) & 0x7fffu);
+        if (an + (ce - cb) > kLpArena || nruns + (ce - cb + 63) / 64 > 64 * kLzSlots) {
+          status = 1;
+          done = true;
+          break;
+        }
+        ra = rr.x;
+        rae = rr.y;
+        rb = rr.z;
+        rbe = rr.w;
+        pend_ps = e.score;
+        if (ra < rae) {
+          job_r0 = ra;
+          job_m = min(64, rae - ra);
+          job_iso = 1;
+          ra += job_m;
+          need = true;
+        } else if (rb < rbe) {
+          job_r0 = rb;
+          job_m = min(64, rbe - rb);
+          job_iso = 0;
+          rb += job_m;
+          need = true;
+        }
+        if (need) {   // its children go out with the rows' loads
+          dcb = cb;
+          dce = ce;
+          dsc = e.score;
+          defer = ce > cb;
+        } else {
+          push_children(cb, ce, e.score);
+          done = status != 0;
+        }
+      }
+      if (lane == 0) {
+        s_job[0] = done ? 1 : 0;
+        s_job[1] = job_r0;
+        s_job[2] = job_m;
+        s_job[3] = job_iso;
+      }
+    }
+    __syncthreads();
+    if (s_job[0]) break;
+    const int r0 = s_job[1], m = s_job[2], iso = s_job[3];
+    if (wave == 0) {
+      if (lane < m) {
+        jflag = a.row_flags[r0 + lane];
+        jbfs = a.row_bfs[r0 + lane];
+        if (iso) jmeta = a.meta[r0 + lane];
+      }
+      if (defer) {
+        push_children(dcb, dce, dsc);
+        defer = false;
+      }
+    } else if (iso) {
+      for (int t = tid - 64; t < m * NV16; t += kLzThreads - 64) {
+        const int e = t / NV16, v = t - e * NV16;
+        const float* __restrict__ mr = a.Mf + (size_t)(r0 + e) * a.DP + v * 16;
+        float4 m4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float4 t4 = m4[j >> 2];
+          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+          const float tt = s_x[v * 16 + j] - mj;
+          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+        }
+        s_part[e * LDP + v] = part;
+      }
+    } else if (wave == 1 && lane < m) {
+      s_lp[lane] = lazy_aniso_lp(a, s_x, r0 + lane);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.n_found[q] = found < a.k ? found : a.k;
+    if (a.n_calls) a.n_calls[q] = calls;
+    a.status[q] = status;
+  }
+}
+#undef LP_ADD_RUN
+
+// Which lazy replay: the one-round-trip kernel (one workgroup per CU) while the queries fit
+// the chip once; the packed one (two per CU) for larger batches.  CWQ_LAZY_PRE=0 / 1 forces.
 hipError_t launch_simulate_lazy_runs(const SimArgs& a, hipStream_t s) {
   if (a.R != 0 || !a.X || a.DP <= 0 || a.DP > kLazyMaxDP || a.DP % 16 || !a.meta || (a.NL_iso > 0 && !a.Mf) ||
       (a.NL > a.NL_iso && (!a.anA || !a.anB)))
     return hipErrorInvalidValue;
-  const size_t lds = lazy_runs_lds(a.DP);
-  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simulate_lazy_runs_kernel), lds)) return e;
-  hipLaunchKernelGGL(simulate_lazy_runs_kernel, dim3((unsigned)a.nq), dim3(kLzThreads), lds, s, a);
+  const char* ev = getenv("CWQ_LAZY_PRE");
+  const bool pre = ev && *ev ? ev[0] != '0' : a.nq <= 256;
+  const void* fn = pre ? reinterpret_cast<const void*>(&simulate_lazy_pre_kernel)
+                       : reinterpret_cast<const void*>(&simulate_lazy_runs_kernel);
+  const size_t lds = pre ? lazy_pre_lds(a.DP) : lazy_runs_lds(a.DP);
+  if (hipError_t e = ensure_dyn_lds(fn, lds)) return e;
+  if (pre)
+    hipLaunchKernelGGL(simulate_lazy_pre_kernel, dim3((unsigned)a.nq), dim3(kLzThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL(simulate_lazy_runs_kernel, dim3((unsigned)a.nq), dim3(kLzThreads), lds, s, a);
   return hipGetLastError();
 }
 

@@ -50,8 +50,9 @@ def main():
                     help="list (comma or +) of fbatch,fpc1,fpc8,fpc64,fphase,fharness,bbatch,bpc (default all)")
     ap.add_argument("--chunk", type=int, default=0, help="device ifit in add_sentences calls of this many rows")
     ap.add_argument("--env-ab", default=None,
-                    help="';'-separated variants of '&'-separated KEY=VAL (read per call): Fast one query per call "
-                         "(nq = 1, 64) under each, interleaved over 3 rounds, after the other legs")
+                    help="';'-separated variants of '&'-separated KEY=VAL (read per call): the legs named in --legs "
+                         "(fpc: Fast nq = 1, 64; bbatch: Basic batch, checked == the first variant; bpc: "
+                         "Basic per call) under each, interleaved over 3 rounds, after the other legs")
     ap.add_argument("--save-struct", default=None,
                     help="write the ifit tree's structure (BFS parent, node of each row) to this .npz")
     ap.add_argument("--load-struct", default=None,
@@ -183,22 +184,32 @@ def env_ab(args, w, ix, Q, Qn, k):
     ix.set_filter(0)
     ids0, _ = ix.score_topk(Q, k)
     ix.set_filter(-1)
+    legs = args.legs.replace("+", ",").split(",")
+    ref = ix.categorize(Q, k, w.max_init_search) if "bbatch" in legs else None
     for r in range(3):
         for v in variants:
             for key in keys:
                 os.environ.pop(key, None)
             os.environ.update(v)
             print(f"-- round {r} env {v or 'default'}", flush=True)
-            for nq in (1, 64):
-                fast_percall(args, ix, Q, k, ids0, nq)
-            if "bpc" in args.legs.replace("+", ","):
+            if "fpc" in legs or args.legs == "all":
+                for nq in (1, 64):
+                    fast_percall(args, ix, Q, k, ids0, nq)
+            if "bbatch" in legs:
+                got = ix.categorize(Q, k, w.max_init_search)
+                same = all(torch.equal(a, b) for a, b in zip(ref, got))
+                t_b = med(lambda: ix.categorize(Q, k, w.max_init_search), 5)
+                print(f"Basic batch nq={args.nq}: {t_b * 1e3:.3f} ms = {args.nq / t_b:.0f} q/s; == first variant "
+                      f"{same}; resolved {ix.last_categorize_stats()}; lazy {ix.last_lazy_stats()}", flush=True)
+            if "bpc" in legs:
                 ts = []
                 for i in range(100):
                     t0 = time.perf_counter()
                     w.cobweb_predict(Qn[i % args.nq], k)
                     ts.append(time.perf_counter() - t0)
                 ts.sort()
-                print(f"Basic per call cobweb_predict(numpy, {k}): median {ts[50] * 1e6:.1f} us", flush=True)
+                print(f"Basic per call cobweb_predict(numpy, {k}): median {ts[50] * 1e6:.1f} us; last call lazy "
+                      f"{ix.last_lazy_stats()}", flush=True)
     for key in keys:
         os.environ.pop(key, None)
 

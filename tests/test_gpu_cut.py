@@ -196,15 +196,18 @@ def test_cut_forced_depth1_matches(gpu, monkeypatch):
     ixd.close()
 
 
-def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch):
+@pytest.mark.parametrize("pre", ["0", "1"])
+def test_lazy_dense_replay_equals_materialised(gpu, monkeypatch, pre):
     """Basic on a tree whose ties nest two levels deep (4 broad root children x 40 clusters:
     the root's lp is the lowest on every path, each broad child's the next lowest for all of
     its rows, so the two-level replay cannot certify and every query takes the DENSE re-run).
     The lazy DENSE replay (leaf rows scored when their parent is popped, CWQ_CAT_LAZY default)
     must give the materialised one's nodes, n_found and log_prob calls (CWQ_CAT_LAZY=0), for
-    the batch and one query per call, k = 10 and k = 3 with a small max_nodes."""
+    the batch and one query per call, k = 10 and k = 3 with a small max_nodes.  Both run-merge
+    kernels: the packed one (CWQ_LAZY_PRE=0) and the one-round-trip one (1)."""
     t, Q = broad_tree(gpu, 40_000, 128, (4, 40), 64, direct=0.02, nq=128)
     ix = make_index(gpu, t, monkeypatch)
+    monkeypatch.setenv("CWQ_LAZY_PRE", pre)
     for k, mx in ((10, 100000), (3, 40)):
         monkeypatch.setenv("CWQ_CAT_LAZY", "0")
         ref = ix.categorize(Q, k, mx)
@@ -263,11 +266,14 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
         monkeypatch.setenv("CWQ_CAT_DIRECT", "0")
         ref = ix.categorize(Q, k, mx)
         monkeypatch.setenv("CWQ_CAT_DIRECT", "1")
-        got = ix.categorize(Q, k, mx)
-        lz, st = ix.last_lazy_stats(), ix.last_categorize_stats()
-        assert lz["direct"] + st["dense_reruns"] == Q.shape[0], (lz, st)
-        for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
-            assert torch.equal(x, y), (shape, k, mx, "batch", name)
+        for pre in ("0", "1"):   # both run-merge kernels (packed / one round trip per pop)
+            monkeypatch.setenv("CWQ_LAZY_PRE", pre)
+            got = ix.categorize(Q, k, mx)
+            lz, st = ix.last_lazy_stats(), ix.last_categorize_stats()
+            assert lz["direct"] + st["dense_reruns"] == Q.shape[0], (lz, st)
+            for name, x, y in zip(("nodes", "n_found", "n_calls"), ref, got):
+                assert torch.equal(x, y), (shape, k, mx, "batch", pre, name)
+        monkeypatch.delenv("CWQ_LAZY_PRE")
     monkeypatch.delenv("CWQ_CAT_DIRECT")
     # a fresh index for the automatic rule (the calls above fed the old one's record)
     if shape == "nested ties":

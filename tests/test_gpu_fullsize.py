@@ -132,8 +132,9 @@ def _full_size_case(pkg, N, D, NQ, seed, qseed, oracle_q, k=10):
 
 
 def test_c4_full_per_gpu_index_10m_x_1024(gpu):
-    # C4: 10M x 1024 = 1.02e10 fp32 elements per replica
-    _full_size_case(gpu, 10_000_000, 1024, 1024, seed=0, qseed=1, oracle_q=[0, 700])
+    # C4: 10M x 1024 = 1.02e10 fp32 elements per replica; 12,500 queries = the bench's
+    # per-rank batch of the 8-GPU C4 run (100k queries split over 8 ranks)
+    _full_size_case(gpu, 10_000_000, 1024, 12_500, seed=0, qseed=1, oracle_q=[0, 700, 12_499])
 
 
 def test_c5_full_index_8_8m_x_256(gpu):
