@@ -26,6 +26,22 @@ enum Epi { EPI_RAW = 0, EPI_KEY = 1, EPI_TOPK = 2 };
 // fmaf(pp, invL, cw lp) (pp = the parent's prefix), categorize min(pp, lp) (pp = BF).  One
 // expression shared by the rerank kernels and group pruning's seed, so their keys agree bit
 // for bit with each other and with the scan's epilogue.
+// The sum of n partials p[0] + p[1] + ... in index order (the scan's slice order, so the
+// rounding is the scan's): 16 LDS reads issued before their adds, not one read latency per add.
+__device__ __forceinline__ float sum_in_order(const float* p, int n) {
+  float acc = 0.f;
+  int v = 0;
+  for (; v + 16 <= n; v += 16) {
+    float t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = p[v + u];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += t[u];
+  }
+  for (; v < n; ++v) acc += p[v];
+  return acc;
+}
+
 __device__ __forceinline__ float iso_key_tail(float acc, const RowMeta& md, float pp, float& lp, int cat,
                                               float dconst) {
   const float S = md.iv * acc;

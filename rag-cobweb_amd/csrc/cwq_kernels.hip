@@ -1484,8 +1484,7 @@ __device__ __forceinline__ float lazy_iso_lp(const SimArgs& a, const float* s_x,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float lp = 0.f;
   if (lane < m) {
-    float acc = 0.f;
-    for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+    const float acc = sum_in_order(s_part + lane * LDP, NV16);
     (void)iso_key_tail(acc, a.meta[rb + lane], CWQ_INF, lp, 1, a.dconst);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // s_part reused by the next batch
@@ -1676,8 +1675,17 @@ extern "C" int cwq_debug_two_stamp(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_two_stamp), sizeof(unsigned long long) * (size_t)std::min(n, 16));
 }
 #define TWO_CLK() ((unsigned long long)clock64())
+#define LZ_WALL() ((unsigned long long)wall_clock64())
+// simulate_lazy_pre_kernel, query 0 of the last launch: cycles total, wall ticks total, then
+// cycles in the pop loop / inline child pushes / scoring phases / deferred child pushes / rank
+// phases, counts of pops / internal pops / jobs / rows / arena entries
+__device__ unsigned long long g_lz_stamp[16];
+extern "C" int cwq_debug_lz_stamp(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lz_stamp), sizeof(unsigned long long) * (size_t)std::min(n, 16));
+}
 #else
 #define TWO_CLK() 0ull
+#define LZ_WALL() 0ull
 #endif
 
 __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
@@ -1930,6 +1938,46 @@ __global__ __launch_bounds__(64) void simulate_two_kernel(const SimArgs a) {
 // Wave 0 runs the frontier; the other waves join only to score a popped node's leaf rows (64
 // per round).  An arena or run-slot overflow sets status 1: simulate_lazy_kernel (global
 // 64-ary heap) re-runs the query.
+// The (row, 16-dim slice) partials of rows r0 .. r0 + m (task t = row * NV16 + slice), tasks
+// t0, t0 + stride, ... of this thread: U tasks' 64-B panel loads in flight before any is used
+// (one dependent round trip per U * stride tasks, not per task).  Each partial is the scan's
+// t*t then fmaf(t, t, .) over the slice's 16 dims.
+template <int U>
+__device__ __forceinline__ void lz_score_panel(const SimArgs& a, const float* s_x, float* s_part, int r0, int m,
+                                               int t0, int stride) {
+  const int NV16 = a.DP / 16, LDP = NV16 + 1, n = m * NV16;
+  for (int tb = t0; tb < n; tb += U * stride) {
+    float4 m4[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tb + u * stride, n - 1);
+      const int e = t / NV16, v = t - e * NV16;
+      const float* __restrict__ mr = a.Mf + (size_t)(r0 + e) * a.DP + v * 16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m4[u][j] = *reinterpret_cast<const float4*>(mr + j * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tb + u * stride;
+      if (t < n) {
+        const int e = t / NV16, v = t - e * NV16;
+        float part;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float4 t4 = m4[u][j >> 2];
+          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
+          const float tt = s_x[v * 16 + j] - mj;
+          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
+        }
+        s_part[e * LDP + v] = part;
+      }
+    }
+  }
+}
+
+#ifndef CWQ_LZ_U
+#define CWQ_LZ_U 1   // panel tasks in flight per thread (A/B builds: -DCWQ_LZ_U=4 / 8 measured no faster)
+#endif
 constexpr int kLzArena = 2560, kLzThreads = 256;   // 24-B entries: 60 KiB, two workgroups per CU at D = 768
 constexpr int kLzSlots = 8;   // run heads per lane: 512 live runs (a row run and a child run per internal pop)
 struct alignas(8) LzRec {   // internal: first child, then (children - first) | nch << 16 | has_sent << 31
@@ -2178,26 +2226,10 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_runs_kernel(const Si
     // score the chunk: rows r0 .. r0 + m
     const int r0 = s_job[1], m = s_job[2];
     if (s_job[3]) {
-      for (int t = tid; t < m * NV16; t += kLzThreads) {
-        const int e = t / NV16, v = t - e * NV16;
-        const float* __restrict__ mr = a.Mf + (size_t)(r0 + e) * a.DP + v * 16;
-        float4 m4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
-        float part;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float4 t4 = m4[j >> 2];
-          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
-          const float tt = s_x[v * 16 + j] - mj;
-          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
-        }
-        s_part[e * LDP + v] = part;
-      }
+      lz_score_panel<CWQ_LZ_U>(a, s_x, s_part, r0, m, tid, kLzThreads);
       __syncthreads();
       if (tid < m) {
-        float acc = 0.f;
-        for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+        const float acc = sum_in_order(s_part + tid * LDP, NV16);
         float lp;
         (void)iso_key_tail(acc, a.meta[r0 + tid], CWQ_INF, lp, 1, a.dconst);
         s_lp[tid] = lp;
@@ -2277,6 +2309,8 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
   } while (0)
   int status = 0, found = 0;
   int64_t calls = 1, visited = 0;
+  unsigned long long c_popl = 0, c_chi = 0, c_ph2 = 0, c_def = 0, c_rank = 0, n_int = 0, n_job = 0, n_rows = 0;
+  const unsigned long long t_start = TWO_CLK(), w_start = LZ_WALL();
   float pend_ps = 0.f;
   int ra = 0, rae = 0, rb = 0, rbe = 0;
   int job_r0 = 0, job_m = 0, job_iso = 0;
@@ -2337,6 +2371,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
   for (;;) {
     if (wave == 0) {
       bool need = false, done = status != 0;
+      const unsigned long long tk0 = TWO_CLK();
       if (!done && job_m > 0) {
         // the scored chunk: isotropic rows sum their partials here (slice order), anisotropic
         // ones come from s_lp; rank it (one pscore: by score, then BFS index), write it as a run
@@ -2345,8 +2380,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
         float lp = 0.f;
         if (in) {
           if (job_iso) {
-            float acc = 0.f;
-            for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+            const float acc = sum_in_order(s_part + lane * LDP, NV16);
             (void)iso_key_tail(acc, jmeta, CWQ_INF, lp, 1, a.dconst);
           } else {
             lp = s_lp[lane];
@@ -2379,6 +2413,8 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
         }
         job_m = 0;
       }
+      c_rank += TWO_CLK() - tk0;
+      const unsigned long long tp0 = TWO_CLK();
       if (!done && ra < rae) {
         job_r0 = ra;
         job_m = min(64, rae - ra);
@@ -2471,16 +2507,20 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
           rb += job_m;
           need = true;
         }
+        ++n_int;
         if (need) {   // its children go out with the rows' loads
           dcb = cb;
           dce = ce;
           dsc = e.score;
           defer = ce > cb;
         } else {
+          const unsigned long long tc0 = TWO_CLK();
           push_children(cb, ce, e.score);
+          c_chi += TWO_CLK() - tc0;
           done = status != 0;
         }
       }
+      c_popl += TWO_CLK() - tp0;
       if (lane == 0) {
         s_job[0] = done ? 1 : 0;
         s_job[1] = job_r0;
@@ -2491,6 +2531,9 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
     __syncthreads();
     if (s_job[0]) break;
     const int r0 = s_job[1], m = s_job[2], iso = s_job[3];
+    const unsigned long long th0 = TWO_CLK();
+    ++n_job;
+    n_rows += m;
     if (wave == 0) {
       if (lane < m) {
         jflag = a.row_flags[r0 + lane];
@@ -2498,36 +2541,34 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
         if (iso) jmeta = a.meta[r0 + lane];
       }
       if (defer) {
+        const unsigned long long td0 = TWO_CLK();
         push_children(dcb, dce, dsc);
+        c_def += TWO_CLK() - td0;
         defer = false;
       }
     } else if (iso) {
-      for (int t = tid - 64; t < m * NV16; t += kLzThreads - 64) {
-        const int e = t / NV16, v = t - e * NV16;
-        const float* __restrict__ mr = a.Mf + (size_t)(r0 + e) * a.DP + v * 16;
-        float4 m4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) m4[j] = *reinterpret_cast<const float4*>(mr + j * 4);
-        float part;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float4 t4 = m4[j >> 2];
-          const float mj = (j & 3) == 0 ? t4.x : (j & 3) == 1 ? t4.y : (j & 3) == 2 ? t4.z : t4.w;
-          const float tt = s_x[v * 16 + j] - mj;
-          part = (j == 0) ? tt * tt : fmaf(tt, tt, part);
-        }
-        s_part[e * LDP + v] = part;
-      }
+      lz_score_panel<CWQ_LZ_U>(a, s_x, s_part, r0, m, tid - 64, kLzThreads - 64);
     } else if (wave == 1 && lane < m) {
       s_lp[lane] = lazy_aniso_lp(a, s_x, r0 + lane);
     }
     __syncthreads();
+    c_ph2 += TWO_CLK() - th0;
   }
   if (tid == 0) {
     a.n_found[q] = found < a.k ? found : a.k;
     if (a.n_calls) a.n_calls[q] = calls;
     a.status[q] = status;
   }
+#if CWQ_STAMP
+  if (tid == 0 && q == 0) {
+    const unsigned long long v[12] = {TWO_CLK() - t_start, LZ_WALL() - w_start, c_popl, c_chi, c_ph2, c_def, c_rank,
+                                      (unsigned long long)visited, n_int, n_job, n_rows, (unsigned long long)an};
+    for (int i = 0; i < 12; ++i) g_lz_stamp[i] = v[i];
+  }
+#else
+  (void)t_start, (void)w_start, (void)c_popl, (void)c_chi, (void)c_ph2, (void)c_def, (void)c_rank, (void)n_int,
+      (void)n_job, (void)n_rows;
+#endif
 }
 #undef LP_ADD_RUN
 

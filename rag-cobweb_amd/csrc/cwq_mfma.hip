@@ -328,8 +328,7 @@ __global__ __launch_bounds__(256) void sb_prep_kernel(const SbPrepArgs a) {
   float* Pl = part + a.NI * NV16;
   for (int lv = 0; lv < a.nlev; ++lv) {
     for (int i = a.lv0[lv] + tid; i < a.lv0[lv + 1]; i += 256) {
-      float acc = 0.f;
-      for (int v = 0; v < NV16; ++v) acc += part[i * NV16 + v];
+      const float acc = sum_in_order(part + i * NV16, NV16);
       const float lp = -0.5f * (a.logdet_int[i] + acc);
       const int p = a.par_int[i];
       const float P = p >= 0 ? fmaf(a.w_int[i], lp, Pl[p]) : a.w_int[i] * lp;
@@ -2021,8 +2020,7 @@ __device__ bool fw_chain_prefixes(FwChainLds& L, const f32x16* __restrict__ xg, 
     }
     __syncthreads();
     for (int e = tid; e < nc; e += kFwThreads) {
-      float acc = 0.f;
-      for (int v = 0; v < NV16; ++v) acc += L.part[e * NV16 + v];
+      const float acc = sum_in_order(L.part + e * NV16, NV16);
       L.val[c0 + e] = -0.5f * (ch.logdet_int[L.node[c0 + e]] + acc);
     }
     __syncthreads();

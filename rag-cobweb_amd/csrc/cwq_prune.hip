@@ -217,8 +217,7 @@ __device__ __forceinline__ void prune_nodes_S(const PruneArgs& a, int q, int c0,
   }
   __syncthreads();
   if (tid < cnt) {
-    float acc = 0.f;
-    for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+    const float acc = sum_in_order(s_part + tid * LDP, NV16);
     a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
   }
   __syncthreads();
@@ -309,8 +308,7 @@ __global__ __launch_bounds__(kHdThreads) void prune_head_kernel(const PruneArgs 
     }
     __syncthreads();
     if (tid < cnt) {
-      float acc = 0.f;
-      for (int v = 0; v < NV16; ++v) acc += s_tp[tid * LDP + v];
+      const float acc = sum_in_order(s_tp + tid * LDP, NV16);
       a.S[(size_t)q * a.ldS + a.top_nodes[c0 + tid]] = acc;
       s_St[c0 + tid] = acc;
     }
@@ -465,8 +463,7 @@ __global__ __launch_bounds__(kGgThreads) void prune_gstar_grouped_kernel(const P
       }
       __syncthreads();
       if (tid < cnt) {
-        float acc = 0.f;
-        for (int v = 0; v < NV16; ++v) acc += s_part[tid * LDP + v];
+        const float acc = sum_in_order(s_part + tid * LDP, NV16);
         a.S[(size_t)q * a.ldS + a.gi_nodes[c0 + tid]] = acc;
       }
       __syncthreads();   // s_x and s_part reused by the next query
@@ -530,8 +527,7 @@ __global__ __launch_bounds__(kSeedThreads) void prune_seed_kernel(const PruneArg
     int rid = 0x7fffffff;
     if (lane < n) {
       const int rr = a.gs_rows[a.gs_ptr[g] + lane];
-      float acc = 0.f;
-      for (int v = 0; v < NV16; ++v) acc += s_part[lane * LDP + v];
+      const float acc = sum_in_order(s_part + lane * LDP, NV16);
       const int p = a.row_par[rr];
       const float pp = p >= 0 ? a.P[(size_t)q * a.ldS + p] : 0.f;
       float lp;

@@ -172,8 +172,7 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
     }
     __syncthreads();
     if ((int)threadIdx.x < a.nq) {
-      float acc = 0.f;
-      for (int vv = 0; vv < NV16; ++vv) acc += s_part[threadIdx.x * NV16 + vv];
+      const float acc = sum_in_order(s_part + threadIdx.x * NV16, NV16);
       const float P = a.fw0 * (-0.5f * (a.flogdet0 + acc));
       s_pr[threadIdx.x] = P;
       if (blockIdx.x == 0) a.fP[(size_t)threadIdx.x * a.fldP] = P;

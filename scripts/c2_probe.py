@@ -343,6 +343,18 @@ def print_stamps(w, Qn, k):
         for ln in lines[:4] + (["..."] if len(lines) > 8 else []) + lines[-4:] if len(lines) > 8 else lines:
             print("   ", ln)
         print("   simulate_two q0 (cycles):", {n: int(two[j]) for j, n in enumerate(names)}, flush=True)
+    if hasattr(L, "cwq_debug_lz_stamp"):   # the lazy replay of the direct path, query 0 of one-query calls
+        lz = (ctypes.c_ulonglong * 16)()
+        lz_names = ["total_cyc", "total_wall", "pop_loop", "inline_children", "score_phase", "deferred_children",
+                    "rank_phase", "pops", "int_pops", "jobs", "rows", "arena"]
+        os.environ["CWQ_CAT_DIRECT"] = "1"
+        for i in range(5):
+            w.cobweb_predict(Qn[i], k)
+            torch.cuda.synchronize()
+            L.cwq_debug_lz_stamp(lz, 16)
+            print(f"   lazy replay call {i} (cycles; wall at 100 MHz):", {n: int(lz[j]) for j, n in enumerate(lz_names)},
+                  flush=True)
+        os.environ.pop("CWQ_CAT_DIRECT", None)
 
 
 if __name__ == "__main__":
