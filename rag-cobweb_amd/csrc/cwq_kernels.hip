@@ -2310,6 +2310,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
   int status = 0, found = 0;
   int64_t calls = 1, visited = 0;
   unsigned long long c_popl = 0, c_chi = 0, c_ph2 = 0, c_def = 0, c_rank = 0, n_int = 0, n_job = 0, n_rows = 0;
+  unsigned long long c_sel = 0, c_rd = 0;
   const unsigned long long t_start = TWO_CLK(), w_start = LZ_WALL();
   float pend_ps = 0.f;
   int ra = 0, rae = 0, rb = 0, rbe = 0;
@@ -2433,6 +2434,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
           done = true;
           break;
         }
+        const unsigned long long ts0 = TWO_CLK();
         uint64_t bk = 0;
         int btb = 0x7fffffff, bj = -1, bix = 0, bend = 0;
 #pragma unroll
@@ -2451,6 +2453,8 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
           break;
         }
         const int idx = __builtin_amdgcn_readlane(bix, wl), iend = __builtin_amdgcn_readlane(bend, wl);
+        const unsigned long long ts1 = TWO_CLK();
+        c_sel += ts1 - ts0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2480,6 +2484,7 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
           done = true;
           break;
         }
+        c_rd += TWO_CLK() - ts1;
         if (e.node < 0) continue;
         const int4 rr = ar[idx];
         const int cb = x.cb, ce = x.cb + (int)(x.pk & 0xffffu);
@@ -2561,11 +2566,13 @@ __global__ __launch_bounds__(kLzThreads) void simulate_lazy_pre_kernel(const Sim
   }
 #if CWQ_STAMP
   if (tid == 0 && q == 0) {
-    const unsigned long long v[12] = {TWO_CLK() - t_start, LZ_WALL() - w_start, c_popl, c_chi, c_ph2, c_def, c_rank,
-                                      (unsigned long long)visited, n_int, n_job, n_rows, (unsigned long long)an};
-    for (int i = 0; i < 12; ++i) g_lz_stamp[i] = v[i];
+    const unsigned long long v[14] = {TWO_CLK() - t_start, LZ_WALL() - w_start, c_popl, c_chi, c_ph2, c_def, c_rank,
+                                      (unsigned long long)visited, n_int, n_job, n_rows, (unsigned long long)an,
+                                      c_sel, c_rd};
+    for (int i = 0; i < 14; ++i) g_lz_stamp[i] = v[i];
   }
 #else
+  (void)c_sel, (void)c_rd;
   (void)t_start, (void)w_start, (void)c_popl, (void)c_chi, (void)c_ph2, (void)c_def, (void)c_rank, (void)n_int,
       (void)n_job, (void)n_rows;
 #endif

@@ -346,7 +346,7 @@ def print_stamps(w, Qn, k):
     if hasattr(L, "cwq_debug_lz_stamp"):   # the lazy replay of the direct path, query 0 of one-query calls
         lz = (ctypes.c_ulonglong * 16)()
         lz_names = ["total_cyc", "total_wall", "pop_loop", "inline_children", "score_phase", "deferred_children",
-                    "rank_phase", "pops", "int_pops", "jobs", "rows", "arena"]
+                    "rank_phase", "pops", "int_pops", "jobs", "rows", "arena", "pop_select", "pop_read"]
         os.environ["CWQ_CAT_DIRECT"] = "1"
         for i in range(5):
             w.cobweb_predict(Qn[i], k)
