@@ -84,6 +84,36 @@ def test_categorize(gpu, name):
     np.testing.assert_array_equal(calls, g["cat_calls"])
 
 
+@pytest.mark.parametrize("pre", ["0", "1"])
+@pytest.mark.parametrize("name", HIER)
+def test_categorize_lazy_replay_goldens(gpu, name, pre, monkeypatch):
+    """The exact lazy replay straight from the internal pass (CWQ_CAT_DIRECT=1, no lists),
+    both run-merge kernels (CWQ_LAZY_PRE=0: packed arena; 1: one load round trip per pop),
+    against the reference's own pop order and log_prob call counts -- goldens with internal
+    nodes and an anisotropic leaf (g1, g4) exercise the lazily scored anisotropic rows; whole
+    batch and one query per call; k past the retrievable leaves and a tiny max_nodes end as
+    the reference's IndexError cases do."""
+    g = load_golden(name)
+    ix = index_from_golden(gpu, g)
+    monkeypatch.setenv("CWQ_CAT_DIRECT", "1")
+    monkeypatch.setenv("CWQ_LAZY_PRE", pre)
+    k = int(g["k"])
+    nodes, found, calls = ix.categorize(g["Xq"], k)
+    assert ix.last_lazy_stats()["direct"] + ix.last_categorize_stats()["dense_reruns"] == len(g["Xq"])
+    np.testing.assert_array_equal(found.cpu().numpy(), k)
+    np.testing.assert_array_equal(nodes.cpu().numpy(), g["cat_nodes"])
+    np.testing.assert_array_equal(calls.cpu().numpy(), g["cat_calls"])
+    for qi in range(min(4, len(g["Xq"]))):
+        n1, f1, c1 = ix.categorize(g["Xq"][qi:qi + 1], k)
+        np.testing.assert_array_equal(n1.cpu().numpy()[0], g["cat_nodes"][qi])
+        assert int(c1[0]) == int(g["cat_calls"][qi])
+    if "err_k_too_big" in g:
+        x = g["Xq"][:1]
+        for kk, mx, key in [(int(g["n_leaf_nodes"]) + 1, 100000, "err_k_too_big"), (k, 4, "err_max_nodes")]:
+            _, found, _ = ix.categorize(x, kk, mx)
+            assert (int(found[0]) < kk) == bool(g[key])
+
+
 @pytest.mark.parametrize("name", ["g1_hier_d32", "g5_hier_d384", "g2_flat_d768"])
 def test_categorize_index_errors(gpu, name):
     """k > retrievable leaves, and a tiny max_nodes: n_found < k exactly where the
