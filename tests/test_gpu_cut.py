@@ -307,3 +307,35 @@ def test_direct_lazy_replay(gpu, monkeypatch, shape):
             assert first_dense is not None and i > first_dense, seen
     if shape == "nested ties":   # the lists leave every query DENSE; the lazy path is ~2.5x faster
         assert seen[0] == (1, 0) and seen[1][1] == 1 and sum(d for _, d in seen[2:]) >= 3, seen
+
+
+def test_cut_500k_scale(gpu, monkeypatch):
+    """The scale of the 500k x 768 device-ifit tree: 500k x 768 rows under 37
+    broad root children x 14 clusters (518 clusters).  Fast: the filter engages with no
+    fallback query and ids AND scores equal the exact scan (batch, 1 and 64 queries per
+    call, pruning on and off).  Basic: the list paths, the exact heap replay and the exact
+    lazy replay (CWQ_CAT_DIRECT=1, both run-merge kernels) give the same pop order, n_found
+    and log_prob calls."""
+    t, Q = broad_tree(gpu, 500_000, 768, (37, 14), 67, direct=0.02, nq=256)
+    ix = make_index(gpu, t, monkeypatch)
+    del t
+    cut, fi = ix.cut_info(), ix.filter_info()
+    print("cut", cut, "filter", fi)
+    assert fi["group_centred"] and cut["max_centre_depth"] == 2 and cut["groups"] >= 500, (cut, fi)
+    out = check_fast(ix, Q, per_call=(1, 64), n_pc=64)
+    st, ps = out[True]
+    print("pruned", st, ps)
+    assert st["filter_used"] and st["fallback_queries"] == 0, st
+    assert ps["available"] and ps["extra_pairs"] <= 0.05 * Q.shape[0] * ps["groups"], ps
+    check_basic(ix, Q[:128])
+    ref = ix.categorize(Q[:128], 10, 100000)
+    for pre in ("0", "1"):
+        monkeypatch.setenv("CWQ_CAT_DIRECT", "1")
+        monkeypatch.setenv("CWQ_LAZY_PRE", pre)
+        got = ix.categorize(Q[:128], 10, 100000)
+        for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, got):
+            assert torch.equal(a, b), (pre, name)
+        one = ix.categorize(Q[:1].contiguous(), 10, 100000)
+        for name, a, b in zip(("nodes", "n_found", "n_calls"), ref, one):
+            assert torch.equal(a[:1], b), (pre, "one query", name)
+    ix.close()
