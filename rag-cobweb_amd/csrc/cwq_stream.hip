@@ -73,8 +73,11 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 // internal k order inside a fragment does not matter for the dot product.
 // CH: K fragments per load chunk (8; 12 for int8 rows of 12 fragments, D = 768, so that no
 // chunk is partial and every wave keeps a whole chunk of HBM loads in flight).
-template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false>
-__global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
+// MINB: workgroups per CU the register allocation must allow (2: <= 128 VGPRs, twice the
+// waves in flight per CU).
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false, int MINB = 1>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MINB == 2 ? 4 : 1))) void stream_kernel(
+    const StreamArgs a) {
   static_assert(!I8 || MODE == 0, "int8 operands: filter pass only");
   typedef typename std::conditional<I8, i32x4, bf16x8>::type frag_t;
   typedef typename std::conditional<I8, i32x4, f32x4>::type acc_t;
@@ -606,14 +609,21 @@ __global__ __launch_bounds__(512) void stream_kernel(const StreamArgs a) {
   }
 }
 
-template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false>
+template <int MODE, int MQB, bool I8 = false, int CH = SK_CH, bool NT = false, int MINB = 1>
 static hipError_t launch_one(const StreamArgs& a, int n_wg, size_t lds, hipStream_t s) {
   // dynamic LDS above the 64 KiB default (once per kernel and device, thread-safe)
-  if (hipError_t e =
-          ensure_dyn_lds(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH, NT>), kStreamMaxLds))
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&stream_kernel<MODE, MQB, I8, CH, NT, MINB>),
+                                    kStreamMaxLds))
     return e;
-  hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH, NT>), dim3((unsigned)n_wg), dim3(64 * SK_WAVES), lds, s, a);
+  hipLaunchKernelGGL((stream_kernel<MODE, MQB, I8, CH, NT, MINB>), dim3((unsigned)(n_wg * MINB)), dim3(64 * SK_WAVES),
+                     lds, s, a);
   return hipGetLastError();
+}
+
+// the bf16 pass's two-workgroup form (A/B: CWQ_STREAM_OCC2_BF16=1 until measured)
+static bool occ2_bf16() {
+  const char* e = getenv("CWQ_STREAM_OCC2_BF16");
+  return e && *e == '1';
 }
 
 template <int MQB>
@@ -623,10 +633,19 @@ static hipError_t launch_mqb(const StreamArgs& a, int mode, bool i8, bool ch12, 
   // CWQ_STREAM_NT=1: the filter pass's row panel by nontemporal loads (A/B knob)
   const char* ne = getenv("CWQ_STREAM_NT");
   const bool ntc = ne && *ne && atoi(ne) != 0;
+  // One query block (nq <= 16, the per-call case): half-size chunks at two workgroups per CU
+  // -- twice the waves, so one wave's bounds epilogue no longer leaves its SIMD's loads idle
+  // (C3 one query per call 252.0 -> 237.8 us, profiles/r06_stream_occ2_ab.log).
+  // CWQ_STREAM_OCC2=0 restores one workgroup per CU.
+  const char* oe = getenv("CWQ_STREAM_OCC2");
+  const int occ = oe && *oe ? atoi(oe) : 1;
+  const bool two = MQB == 1 && occ == 1 && !ntc && lds * 2 <= (size_t)kStreamMaxLds;
   if (i8) {
+    if (ch12 && two) return launch_one<0, MQB, true, 6, false, 2>(a, n_wg, lds, s);
     if (ch12) return ntc ? launch_one<0, MQB, true, 12, true>(a, n_wg, lds, s) : launch_one<0, MQB, true, 12>(a, n_wg, lds, s);
     return launch_one<0, MQB, true>(a, n_wg, lds, s);
   }
+  if (two && occ2_bf16()) return launch_one<0, MQB, false, 4, false, 2>(a, n_wg, lds, s);
   return ntc ? launch_one<0, MQB, false, SK_CH, true>(a, n_wg, lds, s) : launch_one<0, MQB>(a, n_wg, lds, s);
 }
 
