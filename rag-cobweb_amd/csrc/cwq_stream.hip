@@ -620,6 +620,13 @@ static hipError_t launch_one(const StreamArgs& a, int n_wg, size_t lds, hipStrea
   return hipGetLastError();
 }
 
+// fragments per chunk of the two-workgroup int8 pass (4; CWQ_STREAM_CHI8=3 / 6 for A/Bs)
+static int chi8() {
+  const char* e = getenv("CWQ_STREAM_CHI8");
+  const int v = e && *e ? atoi(e) : 4;
+  return v == 3 || v == 6 ? v : 4;
+}
+
 // the bf16 pass's two-workgroup form (A/B: CWQ_STREAM_OCC2_BF16=1 until measured)
 static bool occ2_bf16() {
   const char* e = getenv("CWQ_STREAM_OCC2_BF16");
@@ -641,7 +648,12 @@ static hipError_t launch_mqb(const StreamArgs& a, int mode, bool i8, bool ch12, 
   const int occ = oe && *oe ? atoi(oe) : 1;
   const bool two = MQB == 1 && occ == 1 && !ntc && lds * 2 <= (size_t)kStreamMaxLds;
   if (i8) {
-    if (ch12 && two) return launch_one<0, MQB, true, 6, false, 2>(a, n_wg, lds, s);
+    if (ch12 && two) {
+      const int c = chi8();
+      if (c == 6) return launch_one<0, MQB, true, 6, false, 2>(a, n_wg, lds, s);
+      if (c == 3) return launch_one<0, MQB, true, 3, false, 2>(a, n_wg, lds, s);
+      return launch_one<0, MQB, true, 4, false, 2>(a, n_wg, lds, s);
+    }
     if (ch12) return ntc ? launch_one<0, MQB, true, 12, true>(a, n_wg, lds, s) : launch_one<0, MQB, true, 12>(a, n_wg, lds, s);
     return launch_one<0, MQB, true>(a, n_wg, lds, s);
   }
